@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X sampling SRBD MPC step (BASELINE.json metric).
+
+metric : "SRBD rollouts/sec + p50 MPC-step ms at N=10k H=12; 1/2/4/8 GPU"
+workload (N=1): BASELINE configs[1] = C2, Go2 trot flat, MPPI, N=10 000, H=12, zero-order control.
+A step = one full sampling-MPC iteration over one batch of N rollouts: device Philox RNG ->
+fused rollout + cost + block softmax partials -> merge (argmin, MPPI update, GRFs, predicted
+state) -> warm start of the next step written back on the device.  Inputs are resident in
+HBM when the timed region starts; `value` = rollouts of all ranks / max-over-ranks wall time.
+`p50_step_ms` / `p99_step_ms` are the host-to-host latency of one `srbd_step` call (state,
+reference, contact and parameters in; GRFs, predicted state, parameters out; PCIe included).
+
+N>1 GPUs (torchrun, one rank per GPU): weak scaling, N = 10 000 rows per GPU of ONE MPC problem;
+each step ends in one RCCL all-gather of the per-rank partial records (the path's only exchange).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "quadruped-pympc-tamols_amd"))
+if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    import torch  # noqa: F401  -- before libsrbd_hip.so: one HIP runtime per process (see _lib.py)
+
+from quadruped_pympc_amd import _lib  # noqa: E402
+from quadruped_pympc_amd.synthetic import CONFIGS, Workload, inputs  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+METRIC = "SRBD rollouts/sec + p50 MPC-step ms at N=10k H=12; 1/2/4/8 GPU"
+
+
+def make_cfg(w: Workload, n_total: int, rank: int, world: int, device: int):
+    return _lib.make_config(num_samples=n_total, horizon=w.horizon, method=w.method,
+                            parametrization=w.parametrization, num_splines=w.num_splines, mass=w.mass,
+                            inertia=w.inertia, dts=np.full(w.horizon, w.dt, np.float32), device_id=device,
+                            rank=rank, world_size=world, use_graph=True, sigma_mppi=w.sigma)
+
+
+def roofline(w: Workload, n_local: int, rollout_us: float, traffic):
+    P = w.num_params()
+    algo = n_local * (4 * P + 4)  # read each noise row once, write one cost
+    achieved = algo / (rollout_us * 1e-6) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "rollout_kernel",
+            "kernel_us": round(rollout_us, 3), "algorithmic_bytes_per_launch": algo}
+
+
+def pmc_traffic(workload_name: str):
+    """HBM bytes per rollout launch from the committed rocprofv3 PMC summary, if present."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(workload_name, {}).get("rollout_hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(w: Workload, seconds: float):
+    """The C oracle (OpenMP, all host threads offered) on bounded full C2 steps."""
+    sys.path.insert(0, ROOT)
+    from oracle import c_oracle as co  # test-infrastructure CPU port, used only as this baseline
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
+    cfg = co.make_cfg(N=w.num_samples, H=w.horizon, method=1 if w.method == "mppi" else 0, param_kind=0,
+                      mass=w.mass, inertia=w.inertia, sigma_mppi=w.sigma)
+    s, r, c = inputs(w, 0)
+    best = np.zeros(w.num_params(), np.float32)
+    co.step(cfg, s, r, c, best, seed=42, counter=0, nthreads=threads)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds and n < 2000:
+        best, *_ = co.step(cfg, s, r, c, best, seed=42, counter=n + 1, nthreads=threads)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(w.num_samples * n / dt, 1), "unit": "rollouts/s", "cores": threads, "kind": "port",
+            "sample": f"{n} full MPPI steps of C2 (N={w.num_samples}, H={w.horizon}; Philox noise, rollouts, "
+                      f"softmax update, GRFs) in {dt:.1f} s, oracle/srbd_oracle.c OpenMP",
+            "ms_per_step": round(1e3 * dt / max(n, 1), 3)}
+
+
+def bench_single(w, args):
+    ctx = _lib.Context(make_cfg(w, w.num_samples, 0, 1, 0))
+    s, r, c = inputs(w, 0)
+    best = np.zeros(ctx.P, np.float32)
+    for k in range(max(1, args.warmup)):
+        best, _, res, _ = ctx.step(s, r, c, best, seed=42, counter=k)
+    # host-to-host latency of one MPC step
+    lat = []
+    for k in range(args.latency_steps):
+        t0 = time.perf_counter()
+        best, _, res, _ = ctx.step(s, r, c, best, seed=42, counter=1000 + k)
+        lat.append(time.perf_counter() - t0)
+    # throughput: K device-resident steps, warm-started on the device
+    ctx.bench_device_steps(max(1, args.warmup))
+    t0 = time.perf_counter()
+    ms_dev = ctx.bench_device_steps(args.steps)
+    wall = time.perf_counter() - t0
+    kern = ctx.time_kernels(50)
+    ctx.close()
+    return dict(n_total=w.num_samples, n_local=w.num_samples, wall=wall, ms_dev=ms_dev, lat=lat, kern=kern)
+
+
+def bench_multi(w, args, rank, world, local_rank):
+    import ctypes as C
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    n_total = w.num_samples * world
+    ctx = _lib.Context(make_cfg(w, n_total, rank, world, local_rank))
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream.cuda_stream)
+    recf = ctx.record_floats()
+    rec = torch.zeros(recf, dtype=torch.float32, device="cuda")
+    gathered = torch.zeros(world * recf, dtype=torch.float32, device="cuda")
+    s, r, c = inputs(w, 0)
+    f = lambda a: _lib.fptr(np.ascontiguousarray(a, np.float32))  # noqa: E731
+    state, ref, contact = (np.ascontiguousarray(a, np.float32) for a in (s, r, c))
+    best = np.zeros(ctx.P, np.float32)
+    res = _lib.SrbdResult()
+
+    def host_step(counter):
+        nonlocal best
+        rc = _lib.lib.srbd_step_local(ctx.h, f(state), f(ref), f(contact), contact.shape[1], f(best), None, None,
+                                      42, counter, C.c_void_p(rec.data_ptr()))
+        ctx.check(rc, "srbd_step_local")
+        dist.all_gather_into_tensor(gathered, rec)
+        rc = _lib.lib.srbd_step_finish(ctx.h, C.c_void_p(gathered.data_ptr()), world, _lib.fptr(best), None,
+                                       C.byref(res), None)
+        ctx.check(rc, "srbd_step_finish")
+
+    def device_step():
+        ctx.check(_lib.lib.srbd_device_step_local(ctx.h, C.c_void_p(rec.data_ptr())), "device_step_local")
+        dist.all_gather_into_tensor(gathered, rec)
+        ctx.check(_lib.lib.srbd_device_step_finish(ctx.h, C.c_void_p(gathered.data_ptr()), world),
+                  "device_step_finish")
+
+    for k in range(max(1, args.warmup)):
+        host_step(k)
+    lat = []
+    for k in range(args.latency_steps):
+        dist.barrier()
+        t0 = time.perf_counter()
+        host_step(1000 + k)
+        lat.append(time.perf_counter() - t0)
+    for _ in range(max(1, args.warmup)):
+        device_step()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        device_step()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t.item())
+    ctx.set_stream(None)
+    kern = ctx.time_kernels(20)
+    ctx.close()
+    dist.destroy_process_group()
+    return dict(n_total=n_total, n_local=ctx.n_local, wall=wall, ms_dev=None, lat=lat, kern=kern)
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--latency-steps", type=int, default=500)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    w = CONFIGS[args.config]
+    if world > 1:
+        out = bench_multi(w, args, rank, world, local_rank)
+    else:
+        out = bench_single(w, args)
+    if rank != 0:
+        return
+    lat = np.array(out["lat"]) * 1e3
+    ms_per_step = 1e3 * out["wall"] / args.steps
+    value = out["n_total"] * args.steps / out["wall"]
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "rollouts/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "p50_step_ms": round(float(np.percentile(lat, 50)), 4),
+        "p99_step_ms": round(float(np.percentile(lat, 99)), 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (fixed-seed Go2 state/reference, PGG trot contact sequence, device Philox noise)",
+        "config": {"workload": w.name, "num_samples": out["n_total"], "horizon": w.horizon, "method": w.method,
+                   "parametrization": w.parametrization, "robot": w.robot, "gait": w.gait,
+                   "parallelism": f"rows sharded over {world} GPU(s)" if world > 1 else "single GPU"},
+        "kernels_us": {k: round(v, 3) for k, v in out["kern"].items()},
+        "roofline": roofline(w, out["n_local"], out["kern"]["rollout_us"], pmc_traffic(w.name)),
+    }
+    if out["ms_dev"] is not None:
+        line["device_ms_per_step"] = round(out["ms_dev"] / args.steps, 5)
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
+    else:
+        line["cpu_baseline"] = None
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

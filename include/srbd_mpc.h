@@ -1,0 +1,185 @@
+/*
+ * srbd_mpc.h -- C-ABI of the MI355X-native sampling SRBD MPC (libsrbd_hip.so).
+ *
+ * This is the drop-in boundary for the reference's sampling controller hot path.
+ * Each entry point names the reference interface it replaces (paths relative to
+ * the reference repository root Magicyw/Quadruped-PyMPC-TAMOLS):
+ *
+ *   srbd_create            <- Sampling_MPC.__init__            centroidal_nmpc_jax.py:23-178
+ *   srbd_step              <- Sampling_MPC.jitted_compute_control, i.e.
+ *                             compute_control_random_sampling   centroidal_nmpc_jax.py:629-787
+ *                             compute_control_mppi              centroidal_nmpc_jax.py:789-932
+ *                             compute_control_cem_mppi          centroidal_nmpc_jax.py:934-1094
+ *                             (called from srbd_controller_interface.py:140,159)
+ *   srbd_step_local /
+ *   srbd_step_finish       <- the same call, split around the one cross-GPU exchange
+ *                             (row-sharded rollouts)
+ *   srbd_tamols_run        <- VisualFootholdAdaptation.compute_adaptation, strategy 'tamols'
+ *                             visual_foothold_adaptation.py:153-231 (+ helpers :261-714)
+ *
+ * Conventions: plain pointers and sizes, caller owns every host array, nothing is
+ * retained past a call, 0 = success and negative SRBD_E* codes on failure (message
+ * via srbd_last_error), nothing throws across the ABI.  One context per thread or
+ * process; a context creates its HIP state lazily in srbd_create (never at load).
+ * Results are bitwise reproducible for identical inputs (fixed reduction order).
+ */
+#ifndef SRBD_MPC_H
+#define SRBD_MPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRBD_ABI_VERSION 1
+#define SRBD_MAX_HORIZON 32
+#define SRBD_MAX_PARAMS 384
+#define SRBD_MAX_ELITE 16
+
+enum {
+    SRBD_OK = 0,
+    SRBD_E_INVALID = -1,  /* bad argument / unsupported configuration */
+    SRBD_E_HIP = -2,      /* HIP runtime error */
+    SRBD_E_NODEVICE = -3, /* no HIP device visible: there is no CPU fallback */
+    SRBD_E_STATE = -4,    /* call out of order */
+    SRBD_E_NOMEM = -5
+};
+
+/* mpc_params['sampling_method'] (config.py:181) */
+enum { SRBD_RANDOM_SAMPLING = 0, SRBD_MPPI = 1, SRBD_CEM_MPPI = 2 };
+/* mpc_params['control_parametrization'] (config.py:182) */
+enum { SRBD_ZERO_ORDER = 0, SRBD_LINEAR_SPLINE = 1, SRBD_CUBIC_SPLINE = 2 };
+
+typedef struct srbd_config {
+    int32_t num_samples;     /* N = num_parallel_computations (global, all ranks) */
+    int32_t horizon;         /* H (<= SRBD_MAX_HORIZON) */
+    int32_t method;          /* SRBD_RANDOM_SAMPLING | SRBD_MPPI | SRBD_CEM_MPPI */
+    int32_t parametrization; /* SRBD_ZERO_ORDER | SRBD_LINEAR_SPLINE | SRBD_CUBIC_SPLINE */
+    int32_t num_splines;     /* S (linear / cubic) */
+    int32_t num_elite;       /* CEM elite count; reference: 10 (centroidal_nmpc_jax.py:1075) */
+    int32_t device_id;       /* HIP ordinal */
+    int32_t rank;            /* shard index: rows [rank*N/world, (rank+1)*N/world) */
+    int32_t world_size;      /* 1 for single GPU */
+    int32_t use_graph;       /* 1: replay srbd_step as one hipGraph */
+    float mass;              /* config.mass */
+    float mg;                /* float32(mass * 9.81), rounded once from double as the reference does */
+    float grf_min, grf_max, mu;
+    float inertia[9];        /* config.inertia, row-major, float32 */
+    float dts[SRBD_MAX_HORIZON]; /* Centroidal_Model_JAX.dts (centroidal_model_jax.py:42-53) */
+    float q_diag[24];        /* diag(Q), centroidal_nmpc_jax.py:118-130 */
+    float sigma_mppi;        /* mpc_params['sigma_mppi'] */
+    float sigma_random_sampling[3]; /* mpc_params['sigma_random_sampling'] */
+} srbd_config;
+
+typedef struct srbd_result {
+    float grf[12];             /* nmpc_GRFs (FL, FR, RL, RR) x (x, y, z) */
+    float predicted_state[24]; /* nmpc_predicted_state */
+    float best_cost;           /* saturated cost of the best sample */
+    int32_t best_index;        /* global row of the best sample (nanargmin, first on ties) */
+    int32_t status;
+    int32_t _pad;
+} srbd_result;
+
+typedef struct srbd_ctx srbd_ctx;
+
+/* Parameter count P for a configuration (centroidal_nmpc_jax.py:52-93), or < 0. */
+int srbd_num_params(const srbd_config* cfg);
+int srbd_device_count(int32_t* count);
+int srbd_abi_version(void);
+
+int srbd_create(const srbd_config* cfg, srbd_ctx** out);
+void srbd_destroy(srbd_ctx* ctx);
+/* Last error of ctx, or of the calling thread's last failed srbd_create when ctx == NULL. */
+const char* srbd_last_error(const srbd_ctx* ctx);
+/* Launch on a caller-owned hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); disables graphs. */
+int srbd_set_stream(srbd_ctx* ctx, void* hip_stream);
+
+/*
+ * One sampling iteration (one jitted_compute_control call).
+ *   state, ref        : 24 floats each (prepare_state_and_reference output, cast to f32)
+ *   contact           : 4 rows x contact_stride floats, row-major; the first H columns are used
+ *   best_params       : P floats, in: previous best, out: updated best (reassigned by the interface)
+ *   sigma             : P floats (CEM only, in/out; NULL otherwise)
+ *   noise             : NULL -> device Philox4x32-10 RNG keyed by (seed, counter);
+ *                       else N x P row-major additional_random_parameters (row 0 must be zero)
+ *   out_costs         : N floats (saturated) or NULL
+ */
+int srbd_step(srbd_ctx* ctx, const float* state, const float* ref, const float* contact, int32_t contact_stride,
+              float* best_params, float* sigma, const float* noise, uint64_t seed, uint64_t counter,
+              srbd_result* out, float* out_costs);
+
+/* Sharded form.  Record size in floats (identical on every rank). */
+int srbd_record_floats(const srbd_ctx* ctx);
+/* Rows of this rank only; writes this rank's partial record to d_record (device pointer).
+ * noise_local: NULL or (rows of this shard) x P row-major.  Asynchronous on the context stream. */
+int srbd_step_local(srbd_ctx* ctx, const float* state, const float* ref, const float* contact, int32_t contact_stride,
+                    const float* best_params, const float* sigma, const float* noise_local, uint64_t seed,
+                    uint64_t counter, void* d_record);
+/* Merge num_records gathered records (device pointer, rank order) and finish the step. */
+int srbd_step_finish(srbd_ctx* ctx, const void* d_records, int32_t num_records, float* best_params, float* sigma,
+                     srbd_result* out, float* out_costs_local);
+/* Host-only merge of rank records (same math; no device needed). */
+int srbd_finish_host(const srbd_config* cfg, const float* records, int32_t num_records, const float* state,
+                     const float* contact, int32_t contact_stride, float* best_params, float* sigma,
+                     srbd_result* out);
+/* Host-only: build one rank record from a shard's saturated costs and noise rows (shard x P row-major). */
+int srbd_make_record_host(const srbd_config* cfg, int32_t rank, int32_t world_size, const float* costs,
+                          const float* noise_rows, float* record);
+
+/* Measurement: replay `steps` device-resident steps (RNG -> rollout -> reduction -> warm start
+ * written back on device) back to back; returns elapsed ms (hipEvents on the context stream). */
+int srbd_bench_device_steps(srbd_ctx* ctx, int32_t steps, float* elapsed_ms);
+/* Average per-launch duration (us) of each kernel of one step, hipEvents around every launch. */
+int srbd_time_kernels(srbd_ctx* ctx, int32_t iters, float* rollout_us, float* rng_us, float* reduce_us);
+
+/* Device-resident sharded chain (benchmark / pipelined callers): reuses the inputs of the last
+ * srbd_step_local on the device.  srbd_device_step_local: RNG -> rollout -> rank record into d_record;
+ * srbd_device_step_finish: merge -> outputs -> warm start (best/sigma/counter) written back on
+ * device.  Both are asynchronous on the context stream. */
+int srbd_device_step_local(srbd_ctx* ctx, void* d_record);
+int srbd_device_step_finish(srbd_ctx* ctx, const void* d_records, int32_t num_records);
+/* Block until the context stream is idle and copy the last step's outputs. */
+int srbd_sync_result(srbd_ctx* ctx, float* best_params, float* sigma, srbd_result* out);
+/* Saturated costs of this rank's rows from the last step (lazy materialisation). */
+int srbd_copy_costs(srbd_ctx* ctx, float* out_costs);
+
+/* Self-test of the correctly rounded division used in the rollout (a/b; b == 3 uses the constant
+ * path).  Host results always; device results when out_dev != NULL (needs a GPU). */
+int srbd_selftest_div(const float* a, const float* b, int32_t n, float* out_host, float* out_dev);
+
+/* ------------------------------------------------------------------ TAMOLS */
+typedef struct srbd_tamols_params {
+    double gradient_delta;    /* 0.04 */
+    double slope_threshold;   /* 0.7 */
+    double w_edge, w_rough, w_dev, w_nominal, w_tracking, w_stability;
+    double stability_margin;  /* 0.06 */
+    double swing_time;        /* estimated_swing_time 0.25 */
+    double h_des;             /* hip height */
+    double l_min, l_max;      /* per-robot reach */
+    double box_dx, box_dy;    /* constraint box */
+    double stance_duration;   /* 0.3 (visual_foothold_adaptation.py:387) */
+    double alphas[5];         /* np.linspace(0.2, 0.8, 5) (visual_foothold_adaptation.py:402) */
+} srbd_tamols_params;
+
+typedef struct srbd_tamols_ctx srbd_tamols_ctx;
+
+int srbd_tamols_create(int32_t device_id, srbd_tamols_ctx** out);
+void srbd_tamols_destroy(srbd_tamols_ctx* ctx);
+const char* srbd_tamols_last_error(const srbd_tamols_ctx* ctx);
+/*
+ * heightmaps : 4 legs x rows x cols x 3 (x, y, z) doubles (HeightMap.data[:, :, 0, :])
+ * seeds, hips: 4 x 3;  forward_vel: 3 or NULL;  base_pos: 3 or NULL;
+ * contact    : 4 (1 stance, 0 swing) or NULL (-> all swing);  feet: 4 x 3 or NULL
+ * outputs    : footholds 4x3, boxes 4x2x3, valid 4, scores 4 x rows*cols (or NULL),
+ *              seed_heights 4 (nearest height + 0.02 at the seed, or NULL)
+ */
+int srbd_tamols_run(srbd_tamols_ctx* ctx, const double* heightmaps, int32_t rows, int32_t cols, const double* seeds,
+                    const double* hips, const double* forward_vel, const double* base_pos, const int32_t* contact,
+                    const double* feet, const srbd_tamols_params* params, double* out_footholds, double* out_boxes,
+                    int32_t* out_valid, double* out_scores, double* out_seed_heights);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SRBD_MPC_H */

@@ -1,0 +1,767 @@
+// srbd_api.hip -- C-ABI of libsrbd_hip.so (declared in include/srbd_mpc.h).
+//
+// A context owns: the per-context constants (ModelConst, kernarg), a pinned StepInput staging
+// buffer and its device copy (one H2D per step), the noise matrix in SoA layout [P][ldn]
+// (ldn = rows rounded up to 256, padding zero), the per-block partial records, a StepOutput
+// (one D2H per step) and, optionally, a captured hipGraph of the whole step.
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "srbd_launch.h"
+
+using namespace srbd;
+
+namespace {
+thread_local std::string g_last_error;
+
+int rollout_threads(int n_local) {
+    if (n_local <= 16384) return 64;
+    if (n_local <= 65536) return 128;
+    return 256;
+}
+constexpr int MAX_RECORDS = 8192;
+}  // namespace
+
+struct srbd_ctx {
+    srbd_config cfg;
+    ModelConst mc;
+    int threads = 64, nblocks = 0, wrec_stride = 0, rrec_stride = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = true;
+    StepInput* d_in = nullptr;
+    StepInput* h_in = nullptr;
+    StepOutput* d_out = nullptr;
+    StepOutput* h_out = nullptr;
+    float* d_noise = nullptr;
+    float* d_noise_rm = nullptr;
+    size_t noise_rm_cap = 0;
+    float* d_costs = nullptr;
+    float* d_wrec = nullptr;
+    hipGraphExec_t g_step = nullptr, g_dev = nullptr;
+    bool input_ready = false;
+    std::string err;
+};
+
+#define HIP_TRY(ctx, expr)                                                                          \
+    do {                                                                                            \
+        hipError_t _e = (expr);                                                                     \
+        if (_e != hipSuccess) {                                                                     \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(_e);                        \
+            return SRBD_E_HIP;                                                                      \
+        }                                                                                           \
+    } while (0)
+
+static int fail(srbd_ctx* c, int code, const std::string& m) {
+    if (c) c->err = m;
+    else g_last_error = m;
+    return code;
+}
+
+// ------------------------------------------------------------------ configuration
+static int params_leg(const srbd_config* c) {
+    if (c->parametrization == SRBD_LINEAR_SPLINE) return (c->num_splines + 1) * 3;
+    if (c->parametrization == SRBD_CUBIC_SPLINE) return 12 * c->num_splines;
+    return 3 * c->horizon;
+}
+
+extern "C" int srbd_num_params(const srbd_config* cfg) {
+    if (!cfg || cfg->horizon < 1 || cfg->horizon > SRBD_MAX_HORIZON) return SRBD_E_INVALID;
+    if (cfg->parametrization < 0 || cfg->parametrization > 2) return SRBD_E_INVALID;
+    if (cfg->parametrization != SRBD_ZERO_ORDER && cfg->num_splines < 1) return SRBD_E_INVALID;
+    const int P = 4 * params_leg(cfg);
+    return P > SRBD_MAX_PARAMS ? SRBD_E_INVALID : P;
+}
+
+extern "C" int srbd_abi_version(void) { return SRBD_ABI_VERSION; }
+
+extern "C" int srbd_device_count(int32_t* count) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (count) *count = (e == hipSuccess) ? n : 0;
+    return e == hipSuccess ? SRBD_OK : SRBD_E_NODEVICE;
+}
+
+// Spline coefficients at `step` (NMPC:181-257): idx from the f32 linspace comparison, q = step /
+// f32(horizon_leg / S) - idx, and the Hermite weights in the reference's f32 order.
+static void spline_coef(const srbd_config* c, float step, int horizon_leg, int* idx, float* q, float* omq, float* a,
+                        float* b, float* cc, float* d) {
+    *idx = 0;
+    *q = *omq = *a = *b = *cc = *d = 0.0f;
+    if (c->parametrization == SRBD_ZERO_ORDER) {
+        *idx = (int)(int16_t)step;
+        return;
+    }
+    const int S = c->num_splines;
+    int ix = 0;
+    for (int i = 0; i <= S; ++i) {
+        const float cb = (float)((double)c->horizon * (double)i / (double)S);
+        if (step >= cb) ix = i;
+    }
+    float tau = step / (float)((double)horizon_leg / (double)S);
+    tau = tau - (float)ix;
+    const float qq = tau / 1.0f;
+    *idx = ix;
+    *q = qq;
+    *omq = 1.0f - qq;
+    *a = 2.0f * qq * qq * qq - 3.0f * qq * qq + 1.0f;
+    *b = (qq * qq * qq - 2.0f * qq * qq + qq) * 1.0f;
+    *cc = -2.0f * qq * qq * qq + 3.0f * qq * qq;
+    *d = (qq * qq * qq - qq * qq) * 1.0f;
+}
+
+static int build_model(const srbd_config* cfg, ModelConst* mc, std::string* why) {
+    const int P = srbd_num_params(cfg);
+    if (P < 0) {
+        *why = "unsupported horizon/parametrization/num_splines";
+        return SRBD_E_INVALID;
+    }
+    if (cfg->num_samples < 1) {
+        *why = "num_samples must be >= 1";
+        return SRBD_E_INVALID;
+    }
+    if (cfg->method < 0 || cfg->method > 2) {
+        *why = "unknown sampling method";
+        return SRBD_E_INVALID;
+    }
+    const int world = cfg->world_size < 1 ? 1 : cfg->world_size;
+    if (cfg->rank < 0 || cfg->rank >= world || cfg->num_samples < world) {
+        *why = "bad rank/world_size";
+        return SRBD_E_INVALID;
+    }
+    if (cfg->parametrization == SRBD_CUBIC_SPLINE && 10 * (cfg->num_splines - 1) + 11 >= params_leg(cfg)) {
+        *why = "cubic spline needs num_splines >= 1";
+        return SRBD_E_INVALID;
+    }
+    memset(mc, 0, sizeof(*mc));
+    mc->H = cfg->horizon;
+    mc->P = P;
+    mc->PL = P / 4;
+    mc->kind = cfg->parametrization;
+    mc->S = cfg->num_splines;
+    mc->method = cfg->method;
+    const int ne = cfg->num_elite > 0 ? cfg->num_elite : 10;
+    mc->K = num_elite(cfg->method, ne);
+    if (mc->K > MAXK) {
+        *why = "num_elite too large";
+        return SRBD_E_INVALID;
+    }
+    mc->N = cfg->num_samples;
+    mc->row0 = (int)((long long)cfg->rank * cfg->num_samples / world);
+    mc->n_local = (int)((long long)(cfg->rank + 1) * cfg->num_samples / world) - mc->row0;
+    mc->ldn = (mc->n_local + 255) / 256 * 256;
+    mc->inv_m = 1.0f / cfg->mass;
+    mc->mg = cfg->mg;
+    mc->grf_min = cfg->grf_min;
+    mc->grf_max = cfg->grf_max;
+    mc->mu = cfg->mu;
+    mc->neg_mu = -cfg->mu;
+    memcpy(mc->inertia, cfg->inertia, sizeof(mc->inertia));
+    inv3(cfg->inertia, mc->Iinv);
+    for (int i = 0; i < 12; ++i) mc->Q[i] = cfg->q_diag[i];
+    for (int n = 0; n < MAXH; ++n) mc->dts[n] = n < cfg->horizon ? cfg->dts[n] : 0.0f;
+    for (int n = 0; n < cfg->horizon; ++n)
+        spline_coef(cfg, (float)n, cfg->horizon, &mc->sidx[n], &mc->sq[n], &mc->somq[n], &mc->sa[n], &mc->sb[n],
+                    &mc->sc[n], &mc->sd[n]);
+    spline_coef(cfg, 0.0f, 1, &mc->fidx, &mc->fq, &mc->fomq, &mc->fa, &mc->fb, &mc->fc, &mc->fd);
+    mc->sigma_mppi = cfg->sigma_mppi;
+    for (int i = 0; i < 3; ++i) mc->sigma_rs[i] = cfg->sigma_random_sampling[i];
+    return SRBD_OK;
+}
+
+// Host part of the per-step input (StepInput) -- identical on every rank.
+static int fill_input(const srbd_config* cfg, const ModelConst& mc, StepInput* in, const float* state,
+                      const float* ref, const float* contact, int stride, const float* best, const float* sigma,
+                      uint64_t seed, uint64_t counter) {
+    if (!state || !ref || !contact || !best || stride < mc.H) return SRBD_E_INVALID;
+    if (mc.method == SRBD_CEM_MPPI && !sigma) return SRBD_E_INVALID;
+    memcpy(in->state, state, sizeof(in->state));
+    memcpy(in->ref, ref, sizeof(in->ref));
+    memset(in->contact, 0, sizeof(in->contact));
+    for (int l = 0; l < 4; ++l)
+        for (int n = 0; n < mc.H; ++n) in->contact[l][n] = contact[(size_t)l * stride + n];
+    for (int n = 0; n < mc.H; ++n) {
+        const float ns = in->contact[0][n] + in->contact[1][n] + in->contact[2][n] + in->contact[3][n];
+        in->fzref[n] = mc.mg / ns;  // inf when no leg is in stance: neutralised by the clip (App. A.3)
+    }
+    float cf = 0.0f;
+    for (int i = 12; i < 24; ++i) {
+        const float e = state[i] - ref[i];
+        cf = cf + (e * cfg->q_diag[i]) * e;
+    }
+    in->cost_feet = cf;
+    in->seed_lo = (uint32_t)seed;
+    in->seed_hi = (uint32_t)(seed >> 32);
+    in->ctr_lo = (uint32_t)counter;
+    in->ctr_hi = (uint32_t)(counter >> 32);
+    memcpy(in->best, best, sizeof(float) * mc.P);
+    if (sigma) memcpy(in->sigma, sigma, sizeof(float) * mc.P);
+    else memset(in->sigma, 0, sizeof(in->sigma));
+    return SRBD_OK;
+}
+
+// ------------------------------------------------------------------ lifetime
+extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
+    if (!cfg || !out) return fail(nullptr, SRBD_E_INVALID, "null argument");
+    *out = nullptr;
+    ModelConst mc;
+    std::string why;
+    int rc = build_model(cfg, &mc, &why);
+    if (rc) return fail(nullptr, rc, why);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(nullptr, SRBD_E_NODEVICE, "no HIP device visible (this library has no CPU fallback)");
+    if (cfg->device_id < 0 || cfg->device_id >= ndev) return fail(nullptr, SRBD_E_NODEVICE, "bad device_id");
+    srbd_ctx* c = new srbd_ctx();
+    c->cfg = *cfg;
+    c->mc = mc;
+    c->threads = rollout_threads(mc.n_local);
+    c->nblocks = (mc.n_local + c->threads - 1) / c->threads;
+    if (c->nblocks > MAX_RECORDS) {
+        delete c;
+        return fail(nullptr, SRBD_E_INVALID, "too many samples per rank");
+    }
+    c->wrec_stride = rec_floats_wave(mc.P, mc.K);
+    c->rrec_stride = rec_floats_rank(mc.P, mc.K);
+    auto cleanup_fail = [&](const char* what, hipError_t e) {
+        std::string m = std::string(what) + ": " + hipGetErrorString(e);
+        srbd_destroy(c);
+        return fail(nullptr, SRBD_E_HIP, m);
+    };
+    hipError_t e;
+    if ((e = hipSetDevice(cfg->device_id)) != hipSuccess) return cleanup_fail("hipSetDevice", e);
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
+        return cleanup_fail("hipStreamCreate", e);
+    if ((e = hipHostMalloc((void**)&c->h_in, sizeof(StepInput), hipHostMallocDefault)) != hipSuccess)
+        return cleanup_fail("hipHostMalloc", e);
+    if ((e = hipHostMalloc((void**)&c->h_out, sizeof(StepOutput), hipHostMallocDefault)) != hipSuccess)
+        return cleanup_fail("hipHostMalloc", e);
+    memset(c->h_in, 0, sizeof(StepInput));
+    memset(c->h_out, 0, sizeof(StepOutput));
+    const size_t noise_bytes = sizeof(float) * (size_t)mc.P * mc.ldn;
+    if ((e = hipMalloc((void**)&c->d_in, sizeof(StepInput))) != hipSuccess) return cleanup_fail("hipMalloc", e);
+    if ((e = hipMalloc((void**)&c->d_out, sizeof(StepOutput))) != hipSuccess) return cleanup_fail("hipMalloc", e);
+    if ((e = hipMalloc((void**)&c->d_noise, noise_bytes)) != hipSuccess) return cleanup_fail("hipMalloc", e);
+    if ((e = hipMalloc((void**)&c->d_costs, sizeof(float) * mc.ldn)) != hipSuccess)
+        return cleanup_fail("hipMalloc", e);
+    if ((e = hipMalloc((void**)&c->d_wrec, sizeof(float) * (size_t)c->nblocks * c->wrec_stride)) != hipSuccess)
+        return cleanup_fail("hipMalloc", e);
+    if ((e = hipMemsetAsync(c->d_noise, 0, noise_bytes, c->stream)) != hipSuccess)
+        return cleanup_fail("hipMemset", e);
+    if ((e = hipMemsetAsync(c->d_in, 0, sizeof(StepInput), c->stream)) != hipSuccess)
+        return cleanup_fail("hipMemset", e);
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return cleanup_fail("hipStreamSynchronize", e);
+    *out = c;
+    return SRBD_OK;
+}
+
+extern "C" void srbd_destroy(srbd_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->cfg.device_id);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->g_step) (void)hipGraphExecDestroy(c->g_step);
+    if (c->g_dev) (void)hipGraphExecDestroy(c->g_dev);
+    (void)hipFree(c->d_in);
+    (void)hipFree(c->d_out);
+    (void)hipFree(c->d_noise);
+    (void)hipFree(c->d_noise_rm);
+    (void)hipFree(c->d_costs);
+    (void)hipFree(c->d_wrec);
+    if (c->h_in) (void)hipHostFree(c->h_in);
+    if (c->h_out) (void)hipHostFree(c->h_out);
+    if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" const char* srbd_last_error(const srbd_ctx* c) { return c ? c->err.c_str() : g_last_error.c_str(); }
+
+extern "C" int srbd_set_stream(srbd_ctx* c, void* s) {
+    if (!c) return SRBD_E_INVALID;
+    (void)hipSetDevice(c->cfg.device_id);
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->own_stream) HIP_TRY(c, hipStreamDestroy(c->stream));
+    if (c->g_step) (void)hipGraphExecDestroy(c->g_step);
+    if (c->g_dev) (void)hipGraphExecDestroy(c->g_dev);
+    c->g_step = c->g_dev = nullptr;
+    if (s) {
+        c->stream = (hipStream_t)s;
+        c->own_stream = false;
+    } else {
+        HIP_TRY(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->own_stream = true;
+    }
+    return SRBD_OK;
+}
+
+// ------------------------------------------------------------------ step
+static int upload_noise(srbd_ctx* c, const float* noise) {
+    const ModelConst& mc = c->mc;
+    const size_t bytes = sizeof(float) * (size_t)mc.n_local * mc.P;
+    if (c->noise_rm_cap < bytes) {
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        (void)hipFree(c->d_noise_rm);
+        c->d_noise_rm = nullptr;
+        HIP_TRY(c, hipMalloc((void**)&c->d_noise_rm, bytes));
+        c->noise_rm_cap = bytes;
+    }
+    HIP_TRY(c, hipMemcpyAsync(c->d_noise_rm, noise, bytes, hipMemcpyHostToDevice, c->stream));
+    launch_transpose(c->d_noise_rm, mc.n_local, mc.P, mc.ldn, c->d_noise, c->stream);
+    return SRBD_OK;
+}
+
+// The device part of one step: [noise] -> rollout -> merge.
+static void enqueue_device_step(srbd_ctx* c, bool gen_noise, float* rank_out, StepOutput* out) {
+    const ModelConst& mc = c->mc;
+    if (gen_noise) launch_rng(mc, c->d_in, c->d_noise, c->stream);
+    launch_rollout(mc, c->d_in, c->d_noise, c->d_costs, c->d_wrec, c->wrec_stride, c->threads, c->stream);
+    launch_merge(mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, 0, c->d_noise, rank_out, out, c->stream);
+}
+
+static int enqueue_full_step(srbd_ctx* c, bool gen_noise) {
+    HIP_TRY(c, hipMemcpyAsync(c->d_in, c->h_in, sizeof(StepInput), hipMemcpyHostToDevice, c->stream));
+    enqueue_device_step(c, gen_noise, nullptr, c->d_out);
+    HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(StepOutput), hipMemcpyDeviceToHost, c->stream));
+    return SRBD_OK;
+}
+
+static int copy_out(srbd_ctx* c, float* best, float* sigma, srbd_result* out) {
+    const StepOutput& o = *c->h_out;
+    memcpy(best, o.best, sizeof(float) * c->mc.P);
+    if (sigma && c->mc.method == SRBD_CEM_MPPI) memcpy(sigma, o.sigma, sizeof(float) * c->mc.P);
+    if (out) {
+        memcpy(out->grf, o.grf, sizeof(out->grf));
+        memcpy(out->predicted_state, o.pred, sizeof(out->predicted_state));
+        out->best_cost = o.best_cost;
+        out->best_index = o.best_index;
+        out->status = o.status;
+    }
+    return SRBD_OK;
+}
+
+extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, const float* contact,
+                         int32_t contact_stride, float* best, float* sigma, const float* noise, uint64_t seed,
+                         uint64_t counter, srbd_result* out, float* out_costs) {
+    if (!c) return SRBD_E_INVALID;
+    if (c->cfg.world_size > 1) return fail(c, SRBD_E_STATE, "sharded context: use srbd_step_local/finish");
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    int rc = fill_input(&c->cfg, c->mc, c->h_in, state, ref, contact, contact_stride, best, sigma, seed, counter);
+    if (rc) return fail(c, rc, "invalid step arguments");
+    if (noise) {
+        if ((rc = upload_noise(c, noise))) return rc;
+        if ((rc = enqueue_full_step(c, false))) return rc;
+    } else if (c->cfg.use_graph && c->own_stream) {
+        if (!c->g_step) {
+            hipGraph_t g;
+            HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+            rc = enqueue_full_step(c, true);
+            hipError_t e = hipStreamEndCapture(c->stream, &g);
+            if (rc) return rc;
+            HIP_TRY(c, e);
+            e = hipGraphInstantiate(&c->g_step, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            HIP_TRY(c, e);
+        }
+        HIP_TRY(c, hipGraphLaunch(c->g_step, c->stream));
+    } else {
+        if ((rc = enqueue_full_step(c, true))) return rc;
+    }
+    if (out_costs)
+        HIP_TRY(c, hipMemcpyAsync(out_costs, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,
+                                  c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipGetLastError());
+    c->input_ready = true;
+    return copy_out(c, best, sigma, out);
+}
+
+// ------------------------------------------------------------------ sharded step
+extern "C" int srbd_record_floats(const srbd_ctx* c) { return c ? c->rrec_stride : SRBD_E_INVALID; }
+
+extern "C" int srbd_step_local(srbd_ctx* c, const float* state, const float* ref, const float* contact,
+                               int32_t contact_stride, const float* best, const float* sigma, const float* noise_local,
+                               uint64_t seed, uint64_t counter, void* d_record) {
+    if (!c || !d_record) return SRBD_E_INVALID;
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    // the pinned staging buffer may still feed an in-flight H2D of the previous call
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    int rc = fill_input(&c->cfg, c->mc, c->h_in, state, ref, contact, contact_stride, best, sigma, seed, counter);
+    if (rc) return fail(c, rc, "invalid step arguments");
+    if (noise_local && (rc = upload_noise(c, noise_local))) return rc;
+    HIP_TRY(c, hipMemcpyAsync(c->d_in, c->h_in, sizeof(StepInput), hipMemcpyHostToDevice, c->stream));
+    enqueue_device_step(c, noise_local == nullptr, (float*)d_record, nullptr);
+    HIP_TRY(c, hipGetLastError());
+    c->input_ready = true;
+    return SRBD_OK;
+}
+
+extern "C" int srbd_step_finish(srbd_ctx* c, const void* d_records, int32_t nrec, float* best, float* sigma,
+                                srbd_result* out, float* out_costs_local) {
+    if (!c || !d_records || nrec < 1 || !best) return SRBD_E_INVALID;
+    if (!c->input_ready) return fail(c, SRBD_E_STATE, "srbd_step_finish before srbd_step_local");
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    launch_merge(c->mc, c->d_in, (const float*)d_records, nrec, c->rrec_stride, 1, nullptr, nullptr, c->d_out,
+                 c->stream);
+    HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(StepOutput), hipMemcpyDeviceToHost, c->stream));
+    if (out_costs_local)
+        HIP_TRY(c, hipMemcpyAsync(out_costs_local, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,
+                                  c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipGetLastError());
+    return copy_out(c, best, sigma, out);
+}
+
+extern "C" int srbd_device_step_local(srbd_ctx* c, void* d_record) {
+    if (!c || !d_record) return SRBD_E_INVALID;
+    if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step_local once first");
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    enqueue_device_step(c, true, (float*)d_record, nullptr);
+    HIP_TRY(c, hipGetLastError());
+    return SRBD_OK;
+}
+
+extern "C" int srbd_device_step_finish(srbd_ctx* c, const void* d_records, int32_t nrec) {
+    if (!c || !d_records || nrec < 1) return SRBD_E_INVALID;
+    if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step_local once first");
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    launch_merge(c->mc, c->d_in, (const float*)d_records, nrec, c->rrec_stride, 1, nullptr, nullptr, c->d_out,
+                 c->stream);
+    launch_advance(c->mc, c->d_in, c->d_out, c->stream);
+    HIP_TRY(c, hipGetLastError());
+    return SRBD_OK;
+}
+
+extern "C" int srbd_sync_result(srbd_ctx* c, float* best, float* sigma, srbd_result* out) {
+    if (!c || !best) return SRBD_E_INVALID;
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(StepOutput), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return copy_out(c, best, sigma, out);
+}
+
+extern "C" int srbd_copy_costs(srbd_ctx* c, float* out_costs) {
+    if (!c || !out_costs) return SRBD_E_INVALID;
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    HIP_TRY(c, hipMemcpyAsync(out_costs, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return SRBD_OK;
+}
+
+// ------------------------------------------------------------------ host merge (no device)
+static uint64_t host_rec_key(const float* R, int P, int q) {
+    return ((uint64_t)f2u(R[REC_HDR + P + 2 * q + 1]) << 32) | (uint64_t)f2u(R[REC_HDR + P + 2 * q]);
+}
+
+extern "C" int srbd_make_record_host(const srbd_config* cfg, int32_t rank, int32_t world, const float* costs,
+                                     const float* noise_rows, float* rec) {
+    srbd_config cc = *cfg;
+    cc.rank = rank;
+    cc.world_size = world;
+    ModelConst mc;
+    std::string why;
+    int rc = build_model(&cc, &mc, &why);
+    if (rc) return fail(nullptr, rc, why);
+    const int P = mc.P, K = mc.K, n = mc.n_local;
+    std::vector<uint64_t> keys(n);
+    for (int k = 0; k < n; ++k) keys[k] = cost_key(costs[k], (uint32_t)(mc.row0 + k));
+    std::vector<uint64_t> sorted(keys);
+    std::sort(sorted.begin(), sorted.end());
+    const float m = u2f((uint32_t)(sorted[0] >> 32));
+    memset(rec, 0, sizeof(float) * rec_floats_rank(P, K));
+    rec[0] = m;
+    rec[2] = u2f((uint32_t)sorted[0]);
+    if (mc.method != SRBD_RANDOM_SAMPLING) {
+        float s = 0.0f;
+        std::vector<float> v(P, 0.0f);
+        for (int k = 0; k < n; ++k) {
+            const float e = expf(-1.0f * (costs[k] - m));
+            s = s + e;
+            for (int j = 0; j < P; ++j) v[j] = v[j] + e * noise_rows[(size_t)k * P + j];
+        }
+        rec[1] = s;
+        for (int j = 0; j < P; ++j) rec[REC_HDR + j] = v[j];
+    } else {
+        rec[1] = 1.0f;
+    }
+    for (int e = 0; e < K; ++e) {
+        const uint64_t kk = e < n ? sorted[e] : ~0ull;
+        rec[REC_HDR + P + 2 * e] = u2f((uint32_t)kk);
+        rec[REC_HDR + P + 2 * e + 1] = u2f((uint32_t)(kk >> 32));
+        for (int j = 0; j < P; ++j)
+            rec[REC_HDR + P + 2 * K + e * P + j] =
+                kk == ~0ull ? 0.0f : noise_rows[(size_t)((uint32_t)kk - mc.row0) * P + j];
+    }
+    return SRBD_OK;
+}
+
+extern "C" int srbd_finish_host(const srbd_config* cfg, const float* recs, int32_t nrec, const float* state,
+                                const float* contact, int32_t stride, float* best, float* sigma, srbd_result* out) {
+    srbd_config cc = *cfg;
+    cc.rank = 0;
+    cc.world_size = 1;
+    ModelConst mc;
+    std::string why;
+    int rc = build_model(&cc, &mc, &why);
+    if (rc) return fail(nullptr, rc, why);
+    const int P = mc.P, K = mc.K, stridef = rec_floats_rank(P, K);
+    StepInput* in = new StepInput();
+    rc = fill_input(&cc, mc, in, state, state, contact, stride, best, sigma, 0, 0);  // ref unused here
+    if (rc) {
+        delete in;
+        return fail(nullptr, rc, "invalid arguments");
+    }
+    uint64_t bk = ~0ull;
+    for (int r = 0; r < nrec; ++r) {
+        const float* R = recs + (size_t)r * stridef;
+        const uint64_t kk = ((uint64_t)f2u(R[0]) << 32) | f2u(R[2]);
+        bk = kk < bk ? kk : bk;
+    }
+    const float beta = u2f((uint32_t)(bk >> 32));
+    std::vector<float> V(P + 1, 0.0f);
+    if (mc.method != SRBD_RANDOM_SAMPLING) {
+        for (int r = 0; r < nrec; ++r) {
+            const float* R = recs + (size_t)r * stridef;
+            const float sc = expf(-1.0f * (R[0] - beta));
+            for (int j = 0; j < P; ++j) V[j] = V[j] + sc * R[REC_HDR + j];
+            V[P] = V[P] + sc * R[1];
+        }
+    }
+    // global top-K keys with their rows
+    std::vector<std::pair<uint64_t, const float*>> cand;
+    for (int r = 0; r < nrec; ++r)
+        for (int q = 0; q < K; ++q) {
+            const float* R = recs + (size_t)r * stridef;
+            const uint64_t kk = host_rec_key(R, P, q);
+            if (kk != ~0ull) cand.push_back({kk, R + REC_HDR + P + 2 * K + (size_t)q * P});
+        }
+    std::sort(cand.begin(), cand.end(), [](auto& a, auto& b) { return a.first < b.first; });
+    const int Kv = std::min<int>(K, (int)cand.size());
+    std::vector<float> nb(P);
+    for (int j = 0; j < P; ++j) {
+        nb[j] = mc.method == SRBD_RANDOM_SAMPLING ? in->best[j] + cand[0].second[j] : in->best[j] + V[j] / V[P];
+        if (mc.method == SRBD_CEM_MPPI && sigma) {
+            float s = 0.0f;
+            for (int e = 0; e < Kv; ++e) s = s + cand[e].second[j];
+            const float mean = s / (float)Kv;
+            float var = 0.0f;
+            for (int e = 0; e < Kv; ++e) {
+                const float d = cand[e].second[j] - mean;
+                var = var + d * d;
+            }
+            var = var / (float)(Kv - 1);
+            float sg = sqrtf(var + 1e-8f);
+            sg = sg > 5.0f ? 5.0f : sg;
+            sg = sg < 0.2f ? 0.2f : sg;
+            sigma[j] = sg;
+        }
+    }
+    float grf[12], pred[24];
+    final_grf_pred(mc, *in, nb.data(), grf, pred);
+    memcpy(best, nb.data(), sizeof(float) * P);
+    if (out) {
+        memcpy(out->grf, grf, sizeof(grf));
+        memcpy(out->predicted_state, pred, sizeof(pred));
+        out->best_cost = beta;
+        out->best_index = (int32_t)(uint32_t)bk;
+        out->status = 0;
+    }
+    delete in;
+    return SRBD_OK;
+}
+
+// ------------------------------------------------------------------ measurement
+extern "C" int srbd_bench_device_steps(srbd_ctx* c, int32_t steps, float* ms) {
+    if (!c || steps < 1 || !ms) return SRBD_E_INVALID;
+    if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step once before benchmarking");
+    if (c->cfg.world_size > 1) return fail(c, SRBD_E_STATE, "sharded context");
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    if (!c->g_dev) {
+        hipGraph_t g;
+        HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        enqueue_device_step(c, true, nullptr, c->d_out);
+        launch_advance(c->mc, c->d_in, c->d_out, c->stream);
+        HIP_TRY(c, hipStreamEndCapture(c->stream, &g));
+        hipError_t e = hipGraphInstantiate(&c->g_dev, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        HIP_TRY(c, e);
+    }
+    hipEvent_t e0, e1;
+    HIP_TRY(c, hipEventCreate(&e0));
+    HIP_TRY(c, hipEventCreate(&e1));
+    HIP_TRY(c, hipEventRecord(e0, c->stream));
+    for (int i = 0; i < steps; ++i) HIP_TRY(c, hipGraphLaunch(c->g_dev, c->stream));
+    HIP_TRY(c, hipEventRecord(e1, c->stream));
+    HIP_TRY(c, hipEventSynchronize(e1));
+    HIP_TRY(c, hipEventElapsedTime(ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return SRBD_OK;
+}
+
+extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, float* rng_us, float* reduce_us) {
+    if (!c || iters < 1) return SRBD_E_INVALID;
+    if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step once before timing");
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    std::vector<hipEvent_t> ev(4 * iters);
+    for (auto& e : ev) HIP_TRY(c, hipEventCreate(&e));
+    const ModelConst& mc = c->mc;
+    for (int i = 0; i < iters; ++i) {
+        HIP_TRY(c, hipEventRecord(ev[4 * i], c->stream));
+        launch_rng(mc, c->d_in, c->d_noise, c->stream);
+        HIP_TRY(c, hipEventRecord(ev[4 * i + 1], c->stream));
+        launch_rollout(mc, c->d_in, c->d_noise, c->d_costs, c->d_wrec, c->wrec_stride, c->threads, c->stream);
+        HIP_TRY(c, hipEventRecord(ev[4 * i + 2], c->stream));
+        launch_merge(mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, 0, c->d_noise, nullptr, c->d_out,
+                     c->stream);
+        HIP_TRY(c, hipEventRecord(ev[4 * i + 3], c->stream));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    double a = 0, b = 0, d = 0;
+    for (int i = 0; i < iters; ++i) {
+        float t0, t1, t2;
+        HIP_TRY(c, hipEventElapsedTime(&t0, ev[4 * i], ev[4 * i + 1]));
+        HIP_TRY(c, hipEventElapsedTime(&t1, ev[4 * i + 1], ev[4 * i + 2]));
+        HIP_TRY(c, hipEventElapsedTime(&t2, ev[4 * i + 2], ev[4 * i + 3]));
+        a += t0;
+        b += t1;
+        d += t2;
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    if (rng_us) *rng_us = (float)(a * 1000.0 / iters);
+    if (rollout_us) *rollout_us = (float)(b * 1000.0 / iters);
+    if (reduce_us) *reduce_us = (float)(d * 1000.0 / iters);
+    return SRBD_OK;
+}
+
+extern "C" int srbd_selftest_div(const float* a, const float* b, int32_t n, float* out_host, float* out_dev) {
+    if (!a || !b || n < 0) return SRBD_E_INVALID;
+    if (out_host)
+        for (int i = 0; i < n; ++i) out_host[i] = b[i] == 3.0f ? div3(a[i]) : div_by(a[i], b[i], 1.0f / b[i]);
+    if (out_dev) {
+        float *da = nullptr, *db = nullptr, *dout = nullptr;
+        const size_t bytes = sizeof(float) * (size_t)(n > 0 ? n : 1);
+        if (hipMalloc((void**)&da, bytes) != hipSuccess || hipMalloc((void**)&db, bytes) != hipSuccess ||
+            hipMalloc((void**)&dout, bytes) != hipSuccess)
+            return fail(nullptr, SRBD_E_NODEVICE, "device unavailable");
+        (void)hipMemcpy(da, a, bytes, hipMemcpyHostToDevice);
+        (void)hipMemcpy(db, b, bytes, hipMemcpyHostToDevice);
+        launch_div_selftest(da, db, n, dout, nullptr);
+        hipError_t e = hipMemcpy(out_dev, dout, bytes, hipMemcpyDeviceToHost);
+        (void)hipFree(da);
+        (void)hipFree(db);
+        (void)hipFree(dout);
+        if (e != hipSuccess) return fail(nullptr, SRBD_E_HIP, hipGetErrorString(e));
+    }
+    return SRBD_OK;
+}
+
+// ------------------------------------------------------------------ TAMOLS
+struct srbd_tamols_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    double* d_hm = nullptr;
+    double* d_out = nullptr;  // scores | footholds | boxes | seedh
+    int* d_valid = nullptr;
+    size_t cap_cand = 0;
+    std::string err;
+};
+
+extern "C" int srbd_tamols_create(int32_t device_id, srbd_tamols_ctx** out) {
+    if (!out) return SRBD_E_INVALID;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0 || device_id < 0 || device_id >= ndev)
+        return fail(nullptr, SRBD_E_NODEVICE, "no HIP device visible (this library has no CPU fallback)");
+    srbd_tamols_ctx* t = new srbd_tamols_ctx();
+    t->device = device_id;
+    if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc((void**)&t->d_valid, 4 * sizeof(int)) != hipSuccess) {
+        srbd_tamols_destroy(t);
+        return fail(nullptr, SRBD_E_HIP, "TAMOLS context allocation failed");
+    }
+    *out = t;
+    return SRBD_OK;
+}
+
+extern "C" void srbd_tamols_destroy(srbd_tamols_ctx* t) {
+    if (!t) return;
+    (void)hipSetDevice(t->device);
+    if (t->stream) (void)hipStreamSynchronize(t->stream);
+    (void)hipFree(t->d_hm);
+    (void)hipFree(t->d_out);
+    (void)hipFree(t->d_valid);
+    if (t->stream) (void)hipStreamDestroy(t->stream);
+    delete t;
+}
+
+extern "C" const char* srbd_tamols_last_error(const srbd_tamols_ctx* t) {
+    return t ? t->err.c_str() : g_last_error.c_str();
+}
+
+#define TAM_TRY(t, expr)                                                                            \
+    do {                                                                                            \
+        hipError_t _e = (expr);                                                                     \
+        if (_e != hipSuccess) {                                                                     \
+            (t)->err = std::string(#expr) + ": " + hipGetErrorString(_e);                          \
+            return SRBD_E_HIP;                                                                      \
+        }                                                                                           \
+    } while (0)
+
+extern "C" int srbd_tamols_run(srbd_tamols_ctx* t, const double* hm, int32_t rows, int32_t cols, const double* seeds,
+                               const double* hips, const double* vel, const double* base, const int32_t* contact,
+                               const double* feet, const srbd_tamols_params* p, double* out_fh, double* out_box,
+                               int32_t* out_valid, double* out_scores, double* out_seedh) {
+    if (!t || !hm || !seeds || !hips || !p || !out_fh || !out_box || !out_valid) return SRBD_E_INVALID;
+    const int nc = rows * cols;
+    if (rows < 1 || cols < 1 || nc > TAMOLS_MAXCAND) {
+        t->err = "patch must have 1..320 points";
+        return SRBD_E_INVALID;
+    }
+    TAM_TRY(t, hipSetDevice(t->device));
+    if (t->cap_cand < (size_t)nc) {
+        (void)hipFree(t->d_hm);
+        (void)hipFree(t->d_out);
+        t->d_hm = t->d_out = nullptr;
+        TAM_TRY(t, hipMalloc((void**)&t->d_hm, sizeof(double) * 4 * 3 * nc));
+        TAM_TRY(t, hipMalloc((void**)&t->d_out, sizeof(double) * (4 * (size_t)nc + 12 + 24 + 4)));
+        t->cap_cand = nc;
+    }
+    TamolsArgs a;
+    memset(&a, 0, sizeof(a));
+    a.rows = rows;
+    a.cols = cols;
+    a.ncand = nc;
+    a.has_vel = vel != nullptr;
+    a.has_base = base != nullptr;
+    a.has_feet = feet != nullptr;
+    for (int i = 0; i < 4; ++i) a.contact[i] = contact ? contact[i] : 0;
+    for (int i = 0; i < 3; ++i) {
+        a.vel[i] = vel ? vel[i] : 0.0;
+        a.base[i] = base ? base[i] : 0.0;
+    }
+    for (int i = 0; i < 12; ++i) {
+        a.feet[i] = feet ? feet[i] : 0.0;
+        a.seeds[i] = seeds[i];
+        a.hips[i] = hips[i];
+    }
+    a.p = *p;
+    double* d_scores = t->d_out;
+    double* d_fh = d_scores + 4 * (size_t)nc;
+    double* d_box = d_fh + 12;
+    double* d_seedh = d_box + 24;
+    TAM_TRY(t, hipMemcpyAsync(t->d_hm, hm, sizeof(double) * 12 * nc, hipMemcpyHostToDevice, t->stream));
+    launch_tamols(a, t->d_hm, d_scores, d_fh, d_box, t->d_valid, d_seedh, t->stream);
+    TAM_TRY(t, hipGetLastError());
+    TAM_TRY(t, hipMemcpyAsync(out_fh, d_fh, sizeof(double) * 12, hipMemcpyDeviceToHost, t->stream));
+    TAM_TRY(t, hipMemcpyAsync(out_box, d_box, sizeof(double) * 24, hipMemcpyDeviceToHost, t->stream));
+    TAM_TRY(t, hipMemcpyAsync(out_valid, t->d_valid, sizeof(int) * 4, hipMemcpyDeviceToHost, t->stream));
+    if (out_scores)
+        TAM_TRY(t, hipMemcpyAsync(out_scores, d_scores, sizeof(double) * 4 * nc, hipMemcpyDeviceToHost, t->stream));
+    if (out_seedh) TAM_TRY(t, hipMemcpyAsync(out_seedh, d_seedh, sizeof(double) * 4, hipMemcpyDeviceToHost, t->stream));
+    TAM_TRY(t, hipStreamSynchronize(t->stream));
+    return SRBD_OK;
+}

@@ -1,0 +1,264 @@
+// srbd_core.h -- float32 SRBD math shared by the CDNA4 kernels and the host-side
+// merge (compiled by hipcc for both).  Every function follows the reference's
+// float32 evaluation order (JAX, x64 off); the build uses -ffp-contract=off so
+// no multiply-add is fused unless written as an explicit fmaf.
+//
+// Reference (paths relative to the reference repository root):
+//   CMJ  = quadruped_pympc/controllers/sampling/centroidal_model_jax.py
+//   NMPC = quadruped_pympc/controllers/sampling/centroidal_nmpc_jax.py
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/srbd_mpc.h"
+
+#define SRBD_HD __host__ __device__ __forceinline__
+
+namespace srbd {
+
+constexpr int MAXH = SRBD_MAX_HORIZON;
+constexpr int MAXP = SRBD_MAX_PARAMS;
+constexpr int MAXK = SRBD_MAX_ELITE;
+constexpr int REC_HDR = 4;
+
+// Per-context constants, passed to every kernel by value (kernarg segment -> SGPRs).
+struct ModelConst {
+    int H, P, PL, kind, S, method, K;
+    int N, n_local, row0, ldn;
+    float inv_m, mg, grf_min, grf_max, mu, neg_mu;
+    float inertia[9], Iinv[9];
+    float Q[12];
+    float dts[MAXH];
+    // rollout spline coefficients at step n (horizon_leg = H), NMPC:181-257
+    int sidx[MAXH];
+    float sq[MAXH], somq[MAXH], sa[MAXH], sb[MAXH], sc[MAXH], sd[MAXH];
+    // final decode at step 0.0, horizon_leg 1 (NMPC:706-710)
+    int fidx;
+    float fq, fomq, fa, fb, fc, fd;
+    float sigma_mppi, sigma_rs[3];
+};
+
+// Per-step inputs: one pinned host copy -> one H2D per step.
+struct StepInput {
+    float state[24];
+    float ref[24];
+    float contact[4][MAXH];
+    float fzref[MAXH];  // float32(mass*9.81) / n_stance(n)   (NMPC:377-380)
+    float cost_feet;    // sum over feet of (e*0)*e: 0, or NaN when a foot error is not finite
+    uint32_t seed_lo, seed_hi, ctr_lo, ctr_hi;
+    float best[MAXP];
+    float sigma[MAXP];
+};
+
+struct StepOutput {
+    float best[MAXP];
+    float sigma[MAXP];
+    float grf[12];
+    float pred[24];
+    float best_cost;
+    int32_t best_index;
+    int32_t status;
+    int32_t pad;
+};
+
+SRBD_HD int rec_floats_wave(int P, int K) { return REC_HDR + P + 2 * K; }
+SRBD_HD int rec_floats_rank(int P, int K) { return REC_HDR + P + 2 * K + K * P; }
+SRBD_HD int num_elite(int method, int num_elite_cfg) { return method == SRBD_CEM_MPPI ? num_elite_cfg : 1; }
+
+SRBD_HD uint32_t f2u(float f) {
+    union { float f; uint32_t u; } x;
+    x.f = f;
+    return x.u;
+}
+SRBD_HD float u2f(uint32_t u) {
+    union { float f; uint32_t u; } x;
+    x.u = u;
+    return x.f;
+}
+// Sort key of a (saturated, non-negative) cost and its global row: ascending key order is
+// ascending cost, ties by ascending row == jnp.nanargmin / stable jnp.argsort order.
+SRBD_HD uint64_t cost_key(float c, uint32_t row) {
+    return ((uint64_t)f2u(c + 0.0f) << 32) | (uint64_t)row;
+}
+
+// Correctly rounded x / d given r = RN(1/d) (Markstein): q0 = RN(x r), rem = x - q0 d (exact,
+// fma), q = RN(q0 + rem r).  Equal to IEEE x / d for finite normal operands (tested in
+// tests/test_gpu_parity.py::test_division and test_host_logic.py).
+SRBD_HD float div_by(float x, float d, float r) {
+    float q0 = x * r;
+    float rem = fmaf(-q0, d, x);
+    return fmaf(rem, r, q0);
+}
+
+constexpr float THIRD = 0.3333333432674407958984375f;  // RN(1/3)
+SRBD_HD float div3(float x) { return div_by(x, 3.0f, THIRD); }
+
+// CMJ:67-91, entries divided by DET (IEEE reciprocal once, then Markstein per entry; falls back
+// to plain division when DET is not a comfortably normal number).
+SRBD_HD void inv3(const float A[9], float out[9]) {
+    const float a11 = A[0], a12 = A[1], a13 = A[2], a21 = A[3], a22 = A[4], a23 = A[5], a31 = A[6], a32 = A[7],
+                a33 = A[8];
+    const float DET = a11 * (a33 * a22 - a32 * a23) - a21 * (a33 * a12 - a32 * a13) + a31 * (a23 * a12 - a22 * a13);
+    const float M[9] = {(a33 * a22 - a32 * a23),  -(a33 * a12 - a32 * a13), (a23 * a12 - a22 * a13),
+                        -(a33 * a21 - a31 * a23), (a33 * a11 - a31 * a13),  -(a23 * a11 - a21 * a13),
+                        (a32 * a21 - a31 * a22),  -(a32 * a11 - a31 * a12), (a22 * a11 - a21 * a12)};
+    const float ad = fabsf(DET);
+    if (ad > 1e-30f && ad < 1e30f) {
+        const float r = 1.0f / DET;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) out[i] = div_by(M[i], DET, r);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) out[i] = M[i] / DET;
+    }
+}
+
+SRBD_HD void mv3(const float M[9], const float v[3], float o[3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) o[i] = M[3 * i] * v[0] + M[3 * i + 1] * v[1] + M[3 * i + 2] * v[2];
+}
+
+// jnp.dot(skew(v), f) (CMJ:100-101).  The reference's 0*f terms are dropped: f and v are finite
+// here (forces are clipped; rows of non-finite states saturate to 1e6 either way), so only the
+// sign of an exact zero can differ.
+SRBD_HD void skew_dot(const float v[3], const float f[3], float o[3]) {
+    o[0] = (-v[2]) * f[1] + v[1] * f[2];
+    o[1] = v[2] * f[0] + (-v[0]) * f[2];
+    o[2] = (-v[1]) * f[0] + v[0] * f[1];
+}
+
+SRBD_HD void sincos_(float x, float* s, float* c) {
+#ifdef __HIP_DEVICE_COMPILE__
+    sincosf(x, s, c);
+#else
+    *s = sinf(x);
+    *c = cosf(x);
+#endif
+}
+
+// Centroidal_Model_JAX.fd + integrate_jax (CMJ:93-174).  x: 12 evolving states, feet: 12
+// (constant over the rollout), F: 12 clipped foot forces, c: 4 contact flags.
+SRBD_HD void integrate(const ModelConst& mc, float x[12], const float feet[12], const float F[12], const float c[4],
+                       float dt) {
+    float temp[3], lin_acc[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) temp[k] = F[k] * c[0] + F[3 + k] * c[1] + F[6 + k] * c[2] + F[9 + k] * c[3];
+    lin_acc[0] = mc.inv_m * temp[0] + 0.0f;
+    lin_acc[1] = mc.inv_m * temp[1] + 0.0f;
+    lin_acc[2] = mc.inv_m * temp[2] + (-9.81f);
+
+    float sr, cr, sp, cp, sy, cy;
+    sincos_(x[6], &sr, &cr);
+    sincos_(x[7], &sp, &cp);
+    sincos_(x[8], &sy, &cy);
+
+    float temp2[3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float v[3] = {feet[3 * i] - x[0], feet[3 * i + 1] - x[1], feet[3 * i + 2] - x[2]};
+        float t[3];
+        skew_dot(v, F + 3 * i, t);
+        if (i == 0) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) temp2[k] = t[k] * c[0];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) temp2[k] = temp2[k] + t[k] * c[i];
+        }
+    }
+
+    const float conj[9] = {1.0f, 0.0f, -sp, 0.0f, cr, cp * sr, 0.0f, -sr, cp * cr};
+    float Cinv[9], er[3];
+    inv3(conj, Cinv);
+    mv3(Cinv, x + 9, er);
+
+    const float R[9] = {cp * cy, cp * sy, -sp,
+                        sr * sp * cy - cr * sy, sr * sp * sy + cr * cy, sr * cp,
+                        cr * sp * cy + sr * sy, cr * sp * sy - sr * cy, cr * cp};
+    float Iw[3], wxIw[3], a1[3], Rt[3], a2[3];
+    mv3(mc.inertia, x + 9, Iw);
+    skew_dot(x + 9, Iw, wxIw);
+    mv3(mc.Iinv, wxIw, a1);
+    mv3(R, temp2, Rt);
+    mv3(mc.Iinv, Rt, a2);
+
+    const float d[12] = {x[3],  x[4],  x[5],  lin_acc[0],    lin_acc[1],    lin_acc[2],
+                         er[0], er[1], er[2], -a1[0] + a2[0], -a1[1] + a2[1], -a1[2] + a2[2]};
+#pragma unroll
+    for (int k = 0; k < 12; ++k) x[k] = x[k] + d[k] * dt;
+}
+
+// NMPC:270-314: compare-select form, so a NaN fz becomes fz_min and a NaN fx/fy the cone bound.
+SRBD_HD void clip_leg(const ModelConst& mc, float& fx, float& fy, float& fz) {
+    fz = (fz > mc.grf_min) ? fz : mc.grf_min;
+    fz = (fz < mc.grf_max) ? fz : mc.grf_max;
+    const float lo = mc.neg_mu * fz, hi = mc.mu * fz;
+    fx = (fx > lo) ? fx : lo;
+    fx = (fx < hi) ? fx : hi;
+    fy = (fy > lo) ? fy : lo;
+    fy = (fy < hi) ? fy : hi;
+}
+
+// Gravity compensation + contact mask (NMPC:377-402), then clip.
+SRBD_HD void shape_leg(const ModelConst& mc, float fref, float c, float& fx, float& fy, float& fz) {
+    fz = fref + fz;
+    fx = div3(fx * c);
+    fy = div3(fy * c);
+    fz = fz * c;
+    clip_leg(mc, fx, fy, fz);
+}
+
+// Spline decode of one leg (NMPC:181-268) with precomputed per-step coefficients.
+// `p(j)` returns parameter j of this leg.
+template <class Acc>
+SRBD_HD void decode_leg(int kind, int H, int S, int idx, float q, float omq, float a, float b, float cc, float d,
+                        int n_zero_order, const Acc& p, float& fx, float& fy, float& fz) {
+    if (kind == SRBD_ZERO_ORDER) {
+        fx = p(n_zero_order);
+        fy = p(n_zero_order + H);
+        fz = p(n_zero_order + 2 * H);
+    } else if (kind == SRBD_LINEAR_SPLINE) {
+        const int sh = S + 1;
+        fx = omq * p(idx) + q * p(idx + 1);
+        fy = omq * p(idx + sh) + q * p(idx + sh + 1);
+        fz = omq * p(idx + 2 * sh) + q * p(idx + 2 * sh + 1);
+    } else {
+        const int s = 10 * idx;
+        float o[3];
+#pragma unroll
+        for (int ax = 0; ax < 3; ++ax) {
+            const float p0 = p(s + 4 * ax), p1 = p(s + 4 * ax + 1), p2 = p(s + 4 * ax + 2), p3 = p(s + 4 * ax + 3);
+            const float phi = 0.5f * ((p2 - p1) + (p1 - p0));
+            const float phin = 0.5f * ((p3 - p2) + (p2 - p1));
+            o[ax] = a * p1 + b * phi + cc * p2 + d * phin;
+        }
+        fx = o[0];
+        fy = o[1];
+        fz = o[2];
+    }
+}
+
+// Final GRF decode at step 0 and the predicted state (NMPC:695-784).
+SRBD_HD void final_grf_pred(const ModelConst& mc, const StepInput& in, const float* best, float grf[12],
+                            float pred[24]) {
+    const float c[4] = {in.contact[0][0], in.contact[1][0], in.contact[2][0], in.contact[3][0]};
+#pragma unroll
+    for (int leg = 0; leg < 4; ++leg) {
+        const float* pl = best + leg * mc.PL;
+        auto acc = [pl](int j) { return pl[j]; };
+        float fx, fy, fz;
+        decode_leg(mc.kind, mc.H, mc.S, mc.fidx, mc.fq, mc.fomq, mc.fa, mc.fb, mc.fc, mc.fd, 0, acc, fx, fy, fz);
+        shape_leg(mc, in.fzref[0], c[leg], fx, fy, fz);
+        grf[3 * leg] = fx;
+        grf[3 * leg + 1] = fy;
+        grf[3 * leg + 2] = fz;
+    }
+    float x[12];
+    for (int i = 0; i < 12; ++i) x[i] = in.state[i];
+    integrate(mc, x, in.state + 12, grf, c, mc.dts[0]);
+    for (int i = 0; i < 12; ++i) pred[i] = x[i];
+    for (int i = 12; i < 24; ++i) pred[i] = in.state[i];
+}
+
+}  // namespace srbd

@@ -1,0 +1,277 @@
+"""ctypes binding of ``libsrbd_hip.so`` (C-ABI declared in ``include/srbd_mpc.h``).
+
+The library is the only compute path: there is no CPU fallback.  Loading fails
+loudly (ImportError) when the shared object is missing, and creating a context
+fails loudly (RuntimeError) when no HIP device is visible.
+
+One HIP runtime per process: the PyTorch-ROCm wheel bundles its own
+``libamdhip64.so`` (SONAME ``libamdhip64.so.7``).  A process that uses both this
+library and ``torch.cuda`` (the sharded path over RCCL, the GPU tests) must import
+torch first; the loader then resolves our ``libamdhip64.so.7`` dependency to
+torch's copy.  Loading this library first would leave torch with a second runtime
+that finds no GPU.  Set ``SRBD_IMPORT_TORCH=1`` to have this module import torch
+before loading the library.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+MAX_HORIZON = 32
+MAX_PARAMS = 384
+MAX_ELITE = 16
+
+OK, E_INVALID, E_HIP, E_NODEVICE, E_STATE, E_NOMEM = 0, -1, -2, -3, -4, -5
+RANDOM_SAMPLING, MPPI, CEM_MPPI = 0, 1, 2
+ZERO_ORDER, LINEAR_SPLINE, CUBIC_SPLINE = 0, 1, 2
+METHOD_CODES = {"random_sampling": RANDOM_SAMPLING, "mppi": MPPI, "cem_mppi": CEM_MPPI}
+PARAM_CODES = {"zero_order": ZERO_ORDER, "linear_spline": LINEAR_SPLINE, "cubic_spline": CUBIC_SPLINE}
+
+_F = C.c_float
+_I = C.c_int32
+_D = C.c_double
+_P = C.c_void_p
+_FP = C.POINTER(C.c_float)
+_DP = C.POINTER(C.c_double)
+_IP = C.POINTER(C.c_int32)
+
+
+class SrbdConfig(C.Structure):
+    _fields_ = [
+        ("num_samples", _I), ("horizon", _I), ("method", _I), ("parametrization", _I), ("num_splines", _I),
+        ("num_elite", _I), ("device_id", _I), ("rank", _I), ("world_size", _I), ("use_graph", _I),
+        ("mass", _F), ("mg", _F), ("grf_min", _F), ("grf_max", _F), ("mu", _F),
+        ("inertia", _F * 9), ("dts", _F * MAX_HORIZON), ("q_diag", _F * 24),
+        ("sigma_mppi", _F), ("sigma_random_sampling", _F * 3),
+    ]
+
+
+class SrbdResult(C.Structure):
+    _fields_ = [("grf", _F * 12), ("predicted_state", _F * 24), ("best_cost", _F), ("best_index", _I),
+                ("status", _I), ("_pad", _I)]
+
+
+class TamolsParams(C.Structure):
+    _fields_ = [
+        ("gradient_delta", _D), ("slope_threshold", _D),
+        ("w_edge", _D), ("w_rough", _D), ("w_dev", _D), ("w_nominal", _D), ("w_tracking", _D), ("w_stability", _D),
+        ("stability_margin", _D), ("swing_time", _D), ("h_des", _D), ("l_min", _D), ("l_max", _D),
+        ("box_dx", _D), ("box_dy", _D), ("stance_duration", _D), ("alphas", _D * 5),
+    ]
+
+
+SIGNATURES = {
+    "srbd_num_params": (_I, [C.POINTER(SrbdConfig)]),
+    "srbd_device_count": (_I, [_IP]),
+    "srbd_abi_version": (_I, []),
+    "srbd_create": (_I, [C.POINTER(SrbdConfig), C.POINTER(_P)]),
+    "srbd_destroy": (None, [_P]),
+    "srbd_last_error": (C.c_char_p, [_P]),
+    "srbd_set_stream": (_I, [_P, _P]),
+    "srbd_step": (_I, [_P, _FP, _FP, _FP, _I, _FP, _FP, _FP, C.c_uint64, C.c_uint64, C.POINTER(SrbdResult), _FP]),
+    "srbd_record_floats": (_I, [_P]),
+    "srbd_step_local": (_I, [_P, _FP, _FP, _FP, _I, _FP, _FP, _FP, C.c_uint64, C.c_uint64, _P]),
+    "srbd_step_finish": (_I, [_P, _P, _I, _FP, _FP, C.POINTER(SrbdResult), _FP]),
+    "srbd_finish_host": (_I, [C.POINTER(SrbdConfig), _FP, _I, _FP, _FP, _I, _FP, _FP, C.POINTER(SrbdResult)]),
+    "srbd_make_record_host": (_I, [C.POINTER(SrbdConfig), _I, _I, _FP, _FP, _FP]),
+    "srbd_bench_device_steps": (_I, [_P, _I, _FP]),
+    "srbd_time_kernels": (_I, [_P, _I, _FP, _FP, _FP]),
+    "srbd_device_step_local": (_I, [_P, _P]),
+    "srbd_device_step_finish": (_I, [_P, _P, _I]),
+    "srbd_sync_result": (_I, [_P, _FP, _FP, C.POINTER(SrbdResult)]),
+    "srbd_copy_costs": (_I, [_P, _FP]),
+    "srbd_selftest_div": (_I, [_FP, _FP, _I, _FP, _FP]),
+    "srbd_tamols_create": (_I, [_I, C.POINTER(_P)]),
+    "srbd_tamols_destroy": (None, [_P]),
+    "srbd_tamols_last_error": (C.c_char_p, [_P]),
+    "srbd_tamols_run": (_I, [_P, _DP, _I, _I, _DP, _DP, _DP, _DP, _IP, _DP, C.POINTER(TamolsParams), _DP, _DP, _IP,
+                             _DP, _DP]),
+}
+
+LIB_NAME = "libsrbd_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+
+def _load():
+    if os.environ.get("SRBD_IMPORT_TORCH") == "1":
+        import torch  # noqa: F401  (one HIP runtime: torch's)
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is not built: run `make -C quadruped-pympc-tamols_amd` (or __graft_entry__.build()). "
+            "The sampling MPC has no CPU fallback."
+        )
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.srbd_abi_version() != 1:
+        raise ImportError("libsrbd_hip.so ABI mismatch")
+    return lib
+
+
+lib = _load()
+
+
+def fptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    assert a.dtype == np.float32 and a.flags["C_CONTIGUOUS"], (a.dtype, a.flags)
+    return a.ctypes.data_as(_FP)
+
+
+def dptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_DP)
+
+
+def iptr(a: np.ndarray | None):
+    if a is None:
+        return None
+    assert a.dtype == np.int32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_IP)
+
+
+def last_error(ctx=None) -> str:
+    msg = lib.srbd_last_error(ctx)
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, ctx=None, what: str = "srbd") -> None:
+    if rc != OK:
+        raise RuntimeError(f"{what} failed ({rc}): {last_error(ctx)}")
+
+
+def device_count() -> int:
+    n = _I(0)
+    lib.srbd_device_count(C.byref(n))
+    return int(n.value)
+
+
+def make_config(*, num_samples, horizon, method, parametrization, num_splines=2, num_elite=10, device_id=0, rank=0,
+                world_size=1, use_graph=True, mass, inertia, dts, grf_min=0.0, grf_max=None, mu=0.5, q_diag=None,
+                sigma_mppi=3.0, sigma_random_sampling=(0.2, 3.0, 10.0)) -> SrbdConfig:
+    cfg = SrbdConfig()
+    cfg.num_samples = int(num_samples)
+    cfg.horizon = int(horizon)
+    cfg.method = METHOD_CODES[method] if isinstance(method, str) else int(method)
+    cfg.parametrization = PARAM_CODES[parametrization] if isinstance(parametrization, str) else int(parametrization)
+    cfg.num_splines = int(num_splines)
+    cfg.num_elite = int(num_elite)
+    cfg.device_id = int(device_id)
+    cfg.rank = int(rank)
+    cfg.world_size = int(world_size)
+    cfg.use_graph = 1 if use_graph else 0
+    cfg.mass = float(np.float32(mass))
+    # (self.robot.mass * 9.81) is a Python float, rounded to f32 when divided by the f32 stance count
+    cfg.mg = float(np.float32(float(mass) * 9.81))
+    cfg.grf_min = float(np.float32(grf_min))
+    cfg.grf_max = float(np.float32(grf_max if grf_max is not None else float(mass) * 9.81))
+    cfg.mu = float(np.float32(mu))
+    inertia = np.asarray(inertia, dtype=np.float32).reshape(9)
+    for i in range(9):
+        cfg.inertia[i] = float(inertia[i])
+    dts = np.asarray(dts, dtype=np.float32).reshape(-1)
+    if dts.shape[0] != horizon:
+        raise ValueError("dts must have `horizon` entries")
+    for i in range(horizon):
+        cfg.dts[i] = float(dts[i])
+    if q_diag is None:
+        q_diag = np.zeros(24, dtype=np.float32)
+        q_diag[2] = 1500
+        q_diag[3:6] = 200
+        q_diag[6:8] = 500
+        q_diag[9:11] = 20
+        q_diag[11] = 50
+    q_diag = np.asarray(q_diag, dtype=np.float32)
+    for i in range(24):
+        cfg.q_diag[i] = float(q_diag[i])
+    cfg.sigma_mppi = float(np.float32(sigma_mppi))
+    for i in range(3):
+        cfg.sigma_random_sampling[i] = float(np.float32(sigma_random_sampling[i]))
+    return cfg
+
+
+def num_params(cfg: SrbdConfig) -> int:
+    P = lib.srbd_num_params(C.byref(cfg))
+    if P < 0:
+        raise ValueError("unsupported configuration")
+    return P
+
+
+class Context:
+    """Owns one ``srbd_ctx`` (device buffers, stream, graphs) for one configuration."""
+
+    def __init__(self, cfg: SrbdConfig):
+        self.cfg = cfg
+        self.P = num_params(cfg)
+        self.N = cfg.num_samples
+        ws = max(1, cfg.world_size)
+        self.row0 = cfg.rank * self.N // ws
+        self.n_local = (cfg.rank + 1) * self.N // ws - self.row0
+        h = _P()
+        rc = lib.srbd_create(C.byref(cfg), C.byref(h))
+        if rc != OK:
+            raise RuntimeError(f"srbd_create failed ({rc}): {last_error(None)}")
+        self.h = h
+        self.step_id = 0
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.srbd_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, rc, what):
+        check(rc, self.h, what)
+
+    def step(self, state, ref, contact, best, sigma=None, noise=None, seed=42, counter=0, want_costs=False):
+        state = np.ascontiguousarray(state, dtype=np.float32).reshape(24)
+        ref = np.ascontiguousarray(ref, dtype=np.float32).reshape(24)
+        contact = np.ascontiguousarray(contact, dtype=np.float32)
+        if contact.ndim != 2 or contact.shape[0] != 4 or contact.shape[1] < self.cfg.horizon:
+            raise ValueError("contact_sequence must be (4, >=H)")
+        best = np.array(best, dtype=np.float32).reshape(self.P).copy()
+        if sigma is not None:
+            sigma = np.array(np.broadcast_to(np.asarray(sigma, dtype=np.float32), (self.P,)), dtype=np.float32)
+        if noise is not None:
+            noise = np.ascontiguousarray(noise, dtype=np.float32)
+            if noise.shape != (self.n_local, self.P):
+                raise ValueError(f"noise must be ({self.n_local}, {self.P})")
+        res = SrbdResult()
+        costs = np.empty(self.n_local, dtype=np.float32) if want_costs else None
+        rc = lib.srbd_step(self.h, fptr(state), fptr(ref), fptr(contact), contact.shape[1], fptr(best), fptr(sigma),
+                           fptr(noise), C.c_uint64(int(seed)), C.c_uint64(int(counter)), C.byref(res), fptr(costs))
+        self.check(rc, "srbd_step")
+        self.step_id += 1
+        return best, sigma, res, costs
+
+    def copy_costs(self) -> np.ndarray:
+        out = np.empty(self.n_local, dtype=np.float32)
+        self.check(lib.srbd_copy_costs(self.h, fptr(out)), "srbd_copy_costs")
+        return out
+
+    def bench_device_steps(self, steps: int) -> float:
+        ms = _F(0)
+        self.check(lib.srbd_bench_device_steps(self.h, int(steps), C.byref(ms)), "srbd_bench_device_steps")
+        return float(ms.value)
+
+    def time_kernels(self, iters: int):
+        r, g, m = _F(0), _F(0), _F(0)
+        self.check(lib.srbd_time_kernels(self.h, int(iters), C.byref(r), C.byref(g), C.byref(m)), "srbd_time_kernels")
+        return {"rollout_us": r.value, "rng_us": g.value, "merge_us": m.value}
+
+    def set_stream(self, stream_handle: int | None):
+        self.check(lib.srbd_set_stream(self.h, C.c_void_p(stream_handle) if stream_handle else None), "srbd_set_stream")
+
+    def record_floats(self) -> int:
+        return int(lib.srbd_record_floats(self.h))

@@ -1,0 +1,277 @@
+"""MI355X sampling MPC with the reference's ``Sampling_MPC`` interface.
+
+Drop-in for ``quadruped_pympc/controllers/sampling/centroidal_nmpc_jax.py``
+(``Sampling_MPC``, :20-1097): same constructor (reads ``config.mpc_params``),
+attributes (``num_sampling_iterations``, ``sampling_method``,
+``best_control_parameters``, ``master_key``, ``sigma_cem_mppi`` ...), methods
+(``prepare_state_and_reference``, ``with_newkey``, ``with_newsigma``,
+``shift_solution``, ``reset``) and ``jitted_compute_control`` call shapes and
+return tuples, so ``SRBDControllerInterface.compute_control``
+(srbd_controller_interface.py:113-180) drives it unchanged.
+
+Every compute call goes through ``libsrbd_hip.so`` (hand-written CDNA4 kernels):
+device RNG, fused rollout + cost + block softmax partials, and one merge kernel
+that produces the GRFs, the predicted state and the updated parameters.  The
+HIP context is created on the first compute call (so construction is fork- and
+thread-safe, like the reference's lazy XLA compile); there is no CPU fallback.
+
+Differences from the reference, by design:
+
+* ``master_key`` is ``np.uint64[2] = (seed, counter)`` for the device Philox RNG
+  (JAX's threefry stream cannot be reproduced offline); ``with_newkey`` advances
+  the counter.  Pass ``noise=`` (the (N, P) ``additional_random_parameters``) to
+  any compute call to inject the sampled perturbations exactly.
+* ``costs`` (unused by every reference caller) is returned as a lazy array that
+  copies from the device on first access.
+"""
+from __future__ import annotations
+
+import copy
+import sys
+
+import numpy as np
+
+from ... import config as default_config
+from ... import _lib
+
+f32 = np.float32
+
+
+class LazyCosts:
+    """Saturated per-sample costs of one step, fetched from the device on first use."""
+
+    def __init__(self, ctx: "_lib.Context", step_id: int):
+        self._ctx, self._step_id, self._data = ctx, step_id, None
+
+    def _get(self) -> np.ndarray:
+        if self._data is None:
+            if self._ctx.step_id != self._step_id:
+                raise RuntimeError("costs of an older step: materialise them before the next compute call")
+            self._data = self._ctx.copy_costs()
+        return self._data
+
+    def __array__(self, dtype=None, copy=None):
+        a = self._get()
+        return a if dtype is None else a.astype(dtype)
+
+    def __len__(self):
+        return self._ctx.n_local
+
+    def __getitem__(self, i):
+        return self._get()[i]
+
+    @property
+    def shape(self):
+        return (self._ctx.n_local,)
+
+
+class Sampling_MPC:
+    """This is a small class that implements a sampling based control law (MI355X HIP backend)."""
+
+    def __init__(self, config_module=None):
+        cfg = config_module if config_module is not None else default_config
+        mp = cfg.mpc_params
+        self._cfg = cfg
+        device = mp["device"]
+        self.num_parallel_computations = mp["num_parallel_computations"]
+        self.sampling_method = mp["sampling_method"]
+        self.control_parametrization = mp["control_parametrization"]
+        self.num_sampling_iterations = mp["num_sampling_iterations"]
+        self.dt = mp["dt"]
+        self.horizon = mp["horizon"]
+        self.state_dim = 24
+        self.control_dim = 24
+        self.reference_dim = self.state_dim
+        self.max_sampling_forces_x = 10
+        self.max_sampling_forces_y = 10
+        self.max_sampling_forces_z = 30
+        if device != "gpu":
+            raise RuntimeError("Sampling_MPC (HIP) runs on the GPU only; mpc_params['device'] must be 'gpu'")
+        self.device_id = int(mp.get("device_id", 0))
+
+        # centroidal_nmpc_jax.py:52-93
+        if self.control_parametrization == "linear_spline":
+            self.num_spline = mp["num_splines"]
+            self.num_control_parameters_single_leg = (self.num_spline + 1) * 3
+        elif self.control_parametrization == "cubic_spline":
+            self.num_spline = mp["num_splines"]
+            self.num_control_parameters_single_leg = 4 * 3 * self.num_spline
+        else:
+            self.num_spline = mp.get("num_splines", 2)
+            self.num_control_parameters_single_leg = self.horizon * 3
+        self.num_control_parameters = self.num_control_parameters_single_leg * 4
+
+        # centroidal_nmpc_jax.py:96-110
+        if self.sampling_method == "random_sampling":
+            self.compute_control = self.compute_control_random_sampling
+            self.sigma_random_sampling = mp["sigma_random_sampling"]
+        elif self.sampling_method == "mppi":
+            self.compute_control = self.compute_control_mppi
+            self.sigma_mppi = mp["sigma_mppi"]
+        elif self.sampling_method == "cem_mppi":
+            self.compute_control = self.compute_control_cem_mppi
+            self.sigma_cem_mppi = np.ones(self.num_control_parameters, dtype=f32) * mp["sigma_cem_mppi"]
+        else:
+            print("Error: sampling method not recognized")
+            sys.exit(1)
+        self.jitted_compute_control = self.compute_control
+
+        # model constants (centroidal_model_jax.py:37-56)
+        self.mass = cfg.mass
+        self.inertia = np.asarray(cfg.inertia, dtype=f32)
+        if mp["use_nonuniform_discretization"]:
+            hf = mp["horizon_fine_grained"]
+            self.dts = np.concatenate([np.full(hf, mp["dt_fine_grained"], dtype=f32),
+                                       np.full(self.horizon - hf, self.dt, dtype=f32)])
+        else:
+            self.dts = np.full(self.horizon, self.dt, dtype=f32)
+
+        # centroidal_nmpc_jax.py:118-130
+        self.Q = np.zeros(self.state_dim, dtype=f32)
+        self.Q[2] = 1500
+        self.Q[3:6] = 200
+        self.Q[6:8] = 500
+        self.Q[9:11] = 20
+        self.Q[11] = 50
+        self.mu = mp["mu"]
+        self.f_z_max = mp["grf_max"]
+        self.f_z_min = mp["grf_min"]
+
+        self.best_control_parameters = np.zeros((self.num_control_parameters,), dtype=f32)
+        self.master_key = np.array([42, 0], dtype=np.uint64)
+        self._ctx = None
+
+    # ------------------------------------------------------------------ device
+    def _srbd_config(self) -> "_lib.SrbdConfig":
+        mp = self._cfg.mpc_params
+        return _lib.make_config(
+            num_samples=self.num_parallel_computations, horizon=self.horizon, method=self.sampling_method,
+            parametrization=self.control_parametrization, num_splines=self.num_spline,
+            num_elite=mp.get("num_elite", 10), device_id=self.device_id, use_graph=mp.get("use_hip_graph", True),
+            mass=self.mass, inertia=self.inertia, dts=self.dts, grf_min=self.f_z_min, grf_max=self.f_z_max,
+            mu=self.mu, q_diag=self.Q, sigma_mppi=mp["sigma_mppi"], sigma_random_sampling=mp["sigma_random_sampling"],
+        )
+
+    @property
+    def context(self) -> "_lib.Context":
+        if self._ctx is None:
+            self._ctx = _lib.Context(self._srbd_config())
+        return self._ctx
+
+    def _run(self, state, reference, contact_sequence, best_control_parameters, key, sigma, noise):
+        ctx = self.context
+        key = np.asarray(key, dtype=np.uint64).reshape(-1)
+        best, new_sigma, res, _ = ctx.step(state, reference, np.asarray(contact_sequence, dtype=f32),
+                                           best_control_parameters, sigma=sigma, noise=noise, seed=int(key[0]),
+                                           counter=int(key[1]) if key.shape[0] > 1 else 0)
+        grf = np.array(res.grf, dtype=f32)
+        pred = np.array(res.predicted_state, dtype=f32)
+        costs = LazyCosts(ctx, ctx.step_id)
+        return grf, np.zeros(12, dtype=np.int32), pred, best, f32(res.best_cost), new_sigma, costs, int(res.best_index)
+
+    # ------------------------------------------------------------------ controls
+    def compute_control_random_sampling(self, state, reference, contact_sequence, best_control_parameters, key,
+                                        timing=None, nominal_step_frequency=None, optimize_swing=None, *, noise=None):
+        """centroidal_nmpc_jax.py:629-787."""
+        grf, fh, pred, best, cost, _, costs, _ = self._run(state, reference, contact_sequence,
+                                                           best_control_parameters, key, None, noise)
+        return grf, fh, pred, best, cost, 1.4, costs
+
+    def compute_control_mppi(self, state, reference, contact_sequence, best_control_parameters, key, timing=None,
+                             nominal_step_frequency=None, optimize_swing=None, *, noise=None):
+        """centroidal_nmpc_jax.py:789-932."""
+        grf, fh, pred, best, cost, _, costs, _ = self._run(state, reference, contact_sequence,
+                                                           best_control_parameters, key, None, noise)
+        return grf, fh, pred, best, cost, 1.4, costs
+
+    def compute_control_cem_mppi(self, state, reference, contact_sequence, best_control_parameters, key, sigma,
+                                 timing=None, nominal_step_frequency=None, *, noise=None):
+        """centroidal_nmpc_jax.py:934-1094 (sigma: scalar or (P,))."""
+        grf, fh, pred, best, cost, new_sigma, costs, _ = self._run(state, reference, contact_sequence,
+                                                                   best_control_parameters, key, sigma, noise)
+        return grf, fh, pred, best, cost, 1.65, costs, new_sigma
+
+    # ------------------------------------------------------------------ keys / sigma (:498-511)
+    def with_newkey(self):
+        self.master_key = np.array([self.master_key[0], self.master_key[1] + np.uint64(1)], dtype=np.uint64)
+        return self
+
+    def get_key(self):
+        return self.master_key
+
+    def with_newsigma(self, sigma):
+        self.sigma_cem_mppi = sigma
+        return self
+
+    def get_sigma(self):
+        return self.sigma_cem_mppi
+
+    # ------------------------------------------------------------------ host-side helpers
+    def spline_host(self, parameters, step, horizon_leg):
+        """Host evaluation of the leg spline (centroidal_nmpc_jax.py:181-268), float32."""
+        p = np.asarray(parameters, dtype=f32)
+        if self.control_parametrization == "zero_order":
+            i = int(np.int16(step))
+            return p[i], p[i + self.horizon], p[i + 2 * self.horizon]
+        S = self.num_spline
+        cb = np.linspace(0, self.horizon, S + 1).astype(f32)
+        index = int(np.max(np.where(f32(step) >= cb, np.arange(S + 1), 0)))
+        q = f32(f32(f32(step) / f32(horizon_leg / S)) - f32(index))
+        if self.control_parametrization == "linear_spline":
+            sh = S + 1
+            return tuple((f32(1) - q) * p[index + a * sh] + q * p[index + a * sh + 1] for a in range(3))
+        s = 10 * index
+        a = f32(2) * q * q * q - f32(3) * q * q + f32(1)
+        b = q * q * q - f32(2) * q * q + q
+        c = f32(-2) * q * q * q + f32(3) * q * q
+        d = q * q * q - q * q
+        out = []
+        for o in (0, 4, 8):
+            p0, p1, p2, p3 = p[s + o], p[s + o + 1], p[s + o + 2], p[s + o + 3]
+            phi = f32(0.5) * ((p2 - p1) + (p1 - p0))
+            phin = f32(0.5) * ((p3 - p2) + (p2 - p1))
+            out.append(a * p1 + b * phi + c * p2 + d * phin)
+        return tuple(out)
+
+    def shift_solution(self, best_control_parameters, step):
+        """centroidal_nmpc_jax.py:513-561: leg-wise control[0], [2], [4] <- spline(control, step, H)."""
+        best = np.array(best_control_parameters, dtype=f32)
+        PL = self.num_control_parameters_single_leg
+        for leg in range(4):
+            ctrl = copy.deepcopy(best[leg * PL:(leg + 1) * PL])
+            fx, fy, fz = self.spline_host(ctrl, step, self.horizon)
+            ctrl[0], ctrl[2], ctrl[4] = fx, fy, fz
+            best[leg * PL:(leg + 1) * PL] = ctrl
+        return best
+
+    def prepare_state_and_reference(self, state_current, reference_state, current_contact, previous_contact,
+                                    mpc_frequency=100):
+        """centroidal_nmpc_jax.py:563-627."""
+        if self._cfg.mpc_params["shift_solution"]:
+            self.best_control_parameters = self.shift_solution(self.best_control_parameters, 1.0 / mpc_frequency)
+        state = np.concatenate(
+            (state_current["position"], state_current["linear_velocity"], state_current["orientation"],
+             state_current["angular_velocity"], state_current["foot_FL"], state_current["foot_FR"],
+             state_current["foot_RL"], state_current["foot_RR"])).reshape((24,))
+        legs = ("FL", "FR", "RL", "RR")
+        for leg, name in enumerate(legs):
+            if current_contact[leg] == 0.0:
+                state[12 + 3 * leg:15 + 3 * leg] = reference_state["ref_foot_" + name].reshape((3,))
+        ref = np.concatenate(
+            (reference_state["ref_position"], reference_state["ref_linear_velocity"],
+             reference_state["ref_orientation"], reference_state["ref_angular_velocity"])
+            + tuple(reference_state["ref_foot_" + n].reshape((3,)) for n in legs)).reshape((24,))
+        self.best_control_parameters = np.array(self.best_control_parameters, dtype=f32)
+        PL = self.num_control_parameters_single_leg
+        for leg in range(4):
+            if previous_contact[leg] == 1 and current_contact[leg] == 0:
+                self.best_control_parameters[leg * PL:(leg + 1) * PL] = 0.0
+        return state, ref
+
+    def reset(self):
+        print("Resetting the controller")
+
+    def close(self):
+        if self._ctx is not None:
+            self._ctx.close()
+            self._ctx = None

@@ -1,0 +1,184 @@
+"""Visual foothold adaptation with the TAMOLS local search on the GPU.
+
+Drop-in for ``quadruped_pympc/helpers/visual_foothold_adaptation.py``
+(``VisualFootholdAdaptation``, :38-231) for the strategies ``'height'`` and
+``'tamols'``.  The TAMOLS search (:153-229 and its cost helpers :261-714) runs as
+one HIP kernel launch over the four legs (``srbd_tamols_run``); the candidate set
+is every point of each leg's heightmap patch (:240-243), as in the reference.
+
+Fixes relative to the reference (behaviour otherwise unchanged):
+
+* ``compute_adaptation`` accepts and ignores extra keyword arguments such as the
+  ``phase_signal=`` that ``wb_interface.py:235-240`` passes (a TypeError in the
+  reference).
+
+``'vfa'`` needs the closed-source VFA module and raises ImportError, as the
+reference does when it is absent.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from .. import _lib
+from .. import config as default_config
+from .legs_attr import LegsAttr
+
+LEGS = ("FL", "FR", "RL", "RR")
+
+
+def tamols_params_struct(tamols_params: dict, robot_name: str) -> "_lib.TamolsParams":
+    """srbd_tamols_params from ``simulation_params['tamols_params']`` (config.py:209-243), with VFA's defaults."""
+    g = tamols_params.get
+    p = _lib.TamolsParams()
+    p.gradient_delta = g("gradient_delta", 0.04)
+    p.slope_threshold = g("slope_threshold", 0.7)
+    p.w_edge = g("weight_edge_avoidance", 15.0)
+    p.w_rough = g("weight_roughness", 10.0)
+    p.w_dev = g("weight_deviation", 1.0)
+    p.w_nominal = g("weight_nominal_kinematic", 20.0)
+    p.w_tracking = g("weight_reference_tracking", 2.0)
+    p.w_stability = g("weight_stability", 10.0)
+    p.stability_margin = g("stability_margin", 0.06)
+    p.swing_time = g("estimated_swing_time", 0.25)
+    p.h_des = g("h_des", 0.25)
+    p.l_min = g("l_min", {}).get(robot_name, 0.15)
+    p.l_max = g("l_max", {}).get(robot_name, 0.45)
+    p.box_dx = g("constraint_box_dx", 0.05)
+    p.box_dy = g("constraint_box_dy", 0.05)
+    p.stance_duration = 0.3
+    for i, a in enumerate(np.linspace(0.2, 0.8, 5)):
+        p.alphas[i] = float(a)
+    return p
+
+
+class TamolsSearch:
+    """Owns one ``srbd_tamols_ctx``; ``run`` evaluates all four legs in one kernel launch."""
+
+    def __init__(self, device_id: int = 0):
+        h = C.c_void_p()
+        rc = _lib.lib.srbd_tamols_create(int(device_id), C.byref(h))
+        if rc != _lib.OK:
+            raise RuntimeError(f"srbd_tamols_create failed ({rc}): {_lib.last_error(None)}")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.lib.srbd_tamols_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run(self, heightmaps, seeds, hips, params, forward_vel=None, base_position=None, current_contact=None,
+            current_feet_pos=None):
+        """heightmaps (4, rows, cols, 3) or (4, rows, cols, 1, 3); seeds/hips (4, 3).
+
+        Returns dict(footholds (4,3), boxes (4,2,3), valid (4,) bool, scores (4, rows*cols), seed_heights (4,))."""
+        hm = np.asarray(heightmaps, dtype=np.float64)
+        rows, cols = hm.shape[1], hm.shape[2]
+        hm = np.ascontiguousarray(hm.reshape(4, rows * cols, 3))
+        seeds = np.ascontiguousarray(seeds, dtype=np.float64).reshape(12)
+        hips = np.ascontiguousarray(hips, dtype=np.float64).reshape(12)
+        vel = None if forward_vel is None else np.ascontiguousarray(np.asarray(forward_vel, np.float64)[:3])
+        base = None if base_position is None else np.ascontiguousarray(np.asarray(base_position, np.float64)[:3])
+        contact = None if current_contact is None else np.ascontiguousarray(current_contact, dtype=np.int32)
+        feet = None if current_feet_pos is None else np.ascontiguousarray(current_feet_pos, dtype=np.float64).reshape(12)
+        fh = np.zeros(12)
+        boxes = np.zeros(24)
+        valid = np.zeros(4, dtype=np.int32)
+        scores = np.zeros(4 * rows * cols)
+        seedh = np.zeros(4)
+        rc = _lib.lib.srbd_tamols_run(self.h, _lib.dptr(hm), rows, cols, _lib.dptr(seeds), _lib.dptr(hips),
+                                      _lib.dptr(vel), _lib.dptr(base), _lib.iptr(contact), _lib.dptr(feet),
+                                      C.byref(params), _lib.dptr(fh), _lib.dptr(boxes), _lib.iptr(valid),
+                                      _lib.dptr(scores), _lib.dptr(seedh))
+        if rc != _lib.OK:
+            msg = _lib.lib.srbd_tamols_last_error(self.h)
+            raise RuntimeError(f"srbd_tamols_run failed ({rc}): {msg.decode() if msg else ''}")
+        return dict(footholds=fh.reshape(4, 3), boxes=boxes.reshape(4, 2, 3), valid=valid.astype(bool),
+                    scores=scores.reshape(4, rows * cols), seed_heights=seedh)
+
+
+class VisualFootholdAdaptation:
+    def __init__(self, legs_order, adaptation_strategy="height", config_module=None, device_id=None):
+        cfg = config_module if config_module is not None else default_config
+        self.footholds_adaptation = LegsAttr(FL=np.array([0, 0, 0]), FR=np.array([0, 0, 0]), RL=np.array([0, 0, 0]),
+                                             RR=np.array([0, 0, 0]))
+        self.footholds_constraints = LegsAttr(FL=None, FR=None, RL=None, RR=None)
+        self.initialized = False
+        self.adaptation_strategy = adaptation_strategy
+        self.legs_order = tuple(legs_order)
+        if adaptation_strategy == "vfa":
+            raise ImportError("VFA strategy requested but VFA module could not be imported.")
+        self._search = None
+        self._device_id = cfg.mpc_params.get("device_id", 0) if device_id is None else device_id
+        if adaptation_strategy == "tamols":
+            self.tamols_params = cfg.simulation_params.get("tamols_params", {})
+            self.robot_name = cfg.robot
+        self.last_scores = None
+
+    def update_footholds_adaptation(self, update_footholds_adaptation):
+        self.footholds_adaptation = update_footholds_adaptation
+        self.initialized = True
+
+    def reset(self):
+        self.initialized = False
+
+    def get_footholds_adapted(self, reference_footholds):
+        if not self.initialized:
+            self.footholds_adaptation = reference_footholds
+            return reference_footholds, self.footholds_constraints
+        return self.footholds_adaptation, self.footholds_constraints
+
+    @property
+    def search(self) -> TamolsSearch:
+        if self._search is None:
+            self._search = TamolsSearch(self._device_id)
+        return self._search
+
+    def compute_adaptation(self, legs_order, reference_footholds, hip_positions, heightmaps, forward_vel,
+                           base_orientation, base_orientation_rate, gait_phases=None, base_position=None,
+                           current_contact=None, current_feet_pos=None, **_ignored):
+        for leg_name in legs_order:
+            if heightmaps[leg_name].data is None:
+                return False
+
+        if self.adaptation_strategy == "tamols" and tuple(legs_order) != LEGS:
+            raise ValueError("TAMOLS expects legs_order FL, FR, RL, RR")
+
+        if self.adaptation_strategy == "height":
+            for leg_name in legs_order:
+                h = heightmaps[leg_name].get_height(reference_footholds[leg_name])
+                if h is not None:
+                    reference_footholds[leg_name][2] = h
+
+        elif self.adaptation_strategy == "tamols":
+            names = list(legs_order)
+            data = np.stack([np.asarray(heightmaps[n].data, dtype=np.float64)[:, :, 0, :] for n in names])
+            seeds = np.stack([np.asarray(reference_footholds[n], dtype=np.float64).copy() for n in names])
+            hips = np.stack([np.asarray(hip_positions[n], dtype=np.float64) for n in names])
+            contact = None if current_contact is None else np.asarray(current_contact).astype(np.int32)
+            feet = None
+            if current_feet_pos is not None and base_position is not None:
+                feet = np.stack([np.asarray(current_feet_pos[n], dtype=np.float64) for n in ("FL", "FR", "RL", "RR")])
+            out = self.search.run(data, seeds, hips, tamols_params_struct(self.tamols_params, self.robot_name),
+                                  forward_vel=forward_vel, base_position=base_position, current_contact=contact,
+                                  current_feet_pos=feet)
+            self.last_scores = out["scores"]
+            for i, n in enumerate(names):
+                if out["valid"][i]:
+                    reference_footholds[n] = out["footholds"][i].copy()
+                    self.footholds_constraints[n] = [out["boxes"][i, 0].copy(), out["boxes"][i, 1].copy()]
+                else:
+                    # VFA:223-228: the original heightmap's own lookup when it provides one
+                    get = getattr(heightmaps[n], "get_height", None)
+                    h = get(seeds[i]) if get is not None else out["seed_heights"][i]
+                    if h is not None:
+                        reference_footholds[n][2] = h
+        self.update_footholds_adaptation(reference_footholds)
+        return True

@@ -1,0 +1,99 @@
+"""Synthetic MPC workloads of the BASELINE.json configurations.
+
+No datasets or simulators exist offline, so every benchmark and parity case is
+fed from here: fixed-seed robot states, a forward-walking reference, and the
+contact sequence of the configured gait from the periodic gait generator,
+advanced 5 simulation steps (dt 0.002 s) per MPC step as in the reference loop
+(quadruped_pympc_wrapper.py:134, mpc_frequency 100).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .config import HIP_HEIGHTS, NOMINAL_FEET, ROBOTS
+from .helpers.periodic_gait_generator import BOUNDING, PACE, TROT, PeriodicGaitGenerator
+
+GAITS = {"trot": (TROT, 1.4, 0.65), "pace": (PACE, 1.4, 0.7), "bound": (BOUNDING, 1.8, 0.65)}
+
+
+@dataclass
+class Workload:
+    name: str
+    robot: str
+    gait: str
+    method: str
+    parametrization: str
+    num_samples: int
+    horizon: int
+    num_splines: int = 2
+    terrain: str = "flat"
+    sigma: float = 3.0
+    dt: float = 0.02
+
+    @property
+    def mass(self):
+        return ROBOTS[self.robot][0]
+
+    @property
+    def inertia(self):
+        return np.asarray(ROBOTS[self.robot][1], dtype=np.float32)
+
+    def num_params(self):
+        if self.parametrization == "linear_spline":
+            return 4 * 3 * (self.num_splines + 1)
+        if self.parametrization == "cubic_spline":
+            return 4 * 12 * self.num_splines
+        return 4 * 3 * self.horizon
+
+
+# BASELINE.json "configs", in order
+CONFIGS = {
+    "c1": Workload("go2_trot_flat_rs_n128_h10_zo", "go2", "trot", "random_sampling", "zero_order", 128, 10),
+    "c2": Workload("go2_trot_flat_mppi_n10000_h12_zo", "go2", "trot", "mppi", "zero_order", 10000, 12),
+    "c3": Workload("aliengo_pace_cem_n65536_h16_cubic2", "aliengo", "pace", "cem_mppi", "cubic_spline", 65536, 16),
+    "c4": Workload("go2_stones_tamols_mppi_n10000_h12_zo", "go2", "trot", "mppi", "zero_order", 10000, 12,
+                   terrain="stepping_stones_medium"),
+    "c5": Workload("hyqreal1_bound_mppi_n524288_h12_zo", "hyqreal1", "bound", "mppi", "zero_order", 524288, 12),
+}
+
+
+def robot_state(robot: str, k: int = 0) -> np.ndarray:
+    """24-vector [p, v, rpy, omega, feet FL FR RL RR] from default_rng(1234 + k)."""
+    rng = np.random.default_rng(1234 + k)
+    z = HIP_HEIGHTS[robot] + 0.05
+    fx, fy = NOMINAL_FEET[robot]
+    s = np.zeros(24)
+    s[0:3] = (0.0, 0.0, z)
+    s[3:6] = rng.uniform(-0.2, 0.2, 3)
+    s[6:9] = rng.uniform(-0.05, 0.05, 3)
+    s[9:12] = rng.uniform(-0.3, 0.3, 3)
+    s[12:24] = [fx, fy, 0.0, fx, -fy, 0.0, -fx, fy, 0.0, -fx, -fy, 0.0]
+    return s
+
+
+def reference(robot: str, state: np.ndarray) -> np.ndarray:
+    r = np.zeros(24)
+    r[2] = HIP_HEIGHTS[robot] + 0.05
+    r[3] = 0.5
+    r[12:24] = state[12:24]
+    return r
+
+
+def contact_sequences(gait: str, horizon: int, steps: int, mpc_dt: float = 0.02, sim_dt: float = 0.002,
+                      sim_per_mpc: int = 5) -> list:
+    gtype, freq, duty = GAITS[gait]
+    pgg = PeriodicGaitGenerator(duty, freq, gtype, horizon)
+    out = []
+    for _ in range(steps):
+        for _ in range(sim_per_mpc):
+            pgg.run(sim_dt, pgg.step_freq)
+        out.append(pgg.compute_contact_sequence([mpc_dt], [horizon]))
+    return out
+
+
+def inputs(w: Workload, k: int = 0):
+    """(state24, ref24, contact (4, H)) for MPC step k."""
+    s = robot_state(w.robot, k)
+    return s, reference(w.robot, s), contact_sequences(w.gait, w.horizon, k + 1)[-1]
