@@ -144,6 +144,9 @@ int srbd_sync_result(srbd_ctx* ctx, float* best_params, float* sigma, srbd_resul
 /* Saturated costs of this rank's rows from the last step (lazy materialisation). */
 int srbd_copy_costs(srbd_ctx* ctx, float* out_costs);
 
+/* Diagnostic: mean duration (us) of the merge kernel's 5 phases (s_memrealtime stamps). */
+int srbd_debug_merge_phases(srbd_ctx* ctx, int32_t iters, float* out_us);
+
 /* Self-test of the correctly rounded division used in the rollout (a/b; b == 3 uses the constant
  * path).  Host results always; device results when out_dev != NULL (needs a GPU). */
 int srbd_selftest_div(const float* a, const float* b, int32_t n, float* out_host, float* out_dev);

@@ -284,8 +284,9 @@ static void draw(uint64_t seed, uint64_t ctr, uint32_t d, uint32_t j, float* z, 
     uint32_t q = j & 3u, base = q & 2u;
     float ua = u01(o[base]), ub = u01(o[base + 1]);
     float r = sqrtf(-2.0f * logf(ua));
-    float th = 6.2831853071795864769f * ub;
-    *z = (q & 1u) ? r * sinf(th) : r * cosf(th);
+    /* sin/cos(pi * 2ub): the device uses sincospif(2ub); evaluated here in double, rounded once */
+    double th = 3.14159265358979323846 * (double)(2.0f * ub);
+    *z = (q & 1u) ? r * (float)sin(th) : r * (float)cos(th);
     *u = u01(o[q]);
 }
 

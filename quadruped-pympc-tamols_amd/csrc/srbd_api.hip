@@ -5,6 +5,7 @@
 // (ldn = rows rounded up to 256, padding zero), the per-block partial records, a StepOutput
 // (one D2H per step) and, optionally, a captured hipGraph of the whole step.
 #include <math.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -24,25 +25,43 @@ int rollout_threads(int n_local) {
     if (n_local <= 65536) return 128;
     return 256;
 }
-constexpr int MAX_RECORDS = 8192;
+// Four lanes per sample unless the samples alone fill the GPU (measured crossover: zero-order
+// N ~ 65536, splines beyond 262144; scripts/kernel_sweep.py).  Override with SRBD_ROLLOUT=thread|quad.
+int rollout_mode(int kind, int n_local) {
+    const char* e = getenv("SRBD_ROLLOUT");
+    if (e && !strcmp(e, "thread")) return ROLLOUT_THREAD;
+    if (e && !strcmp(e, "quad")) return ROLLOUT_QUAD;
+    const int quad_max = kind == SRBD_ZERO_ORDER ? 65536 : 524288;
+    return n_local <= quad_max ? ROLLOUT_QUAD : ROLLOUT_THREAD;
+}
+constexpr int MAX_RECORDS = 8192;  // merge_kernel holds 8 record minima per thread x 1024 threads
 }  // namespace
 
 struct srbd_ctx {
     srbd_config cfg;
     ModelConst mc;
-    int threads = 64, nblocks = 0, wrec_stride = 0, rrec_stride = 0;
+    int mode = 0, threads = 64, nblocks = 0, wrec_stride = 0, rrec_stride = 0;
     hipStream_t stream = nullptr;
     bool own_stream = true;
     StepInput* d_in = nullptr;
     StepInput* h_in = nullptr;
     StepOutput* d_out = nullptr;
     StepOutput* h_out = nullptr;
-    float* d_noise = nullptr;
+    // Noise matrices, double buffered: the rollout launch of a step reading d_noise[cur] also draws the
+    // predicted next step's noise (counter + 1) into the other buffer (MPPI / random sampling; CEM's
+    // draws depend on the sigma the step produces).
+    float* d_noise[2] = {nullptr, nullptr};
+    int cur = 0;
+    bool pref_valid = false;
+    int pref_buf = 0;
+    uint64_t pref_seed = 0, pref_ctr = 0;
+    bool chain_started = false;  // sharded device-resident chain
     float* d_noise_rm = nullptr;
     size_t noise_rm_cap = 0;
     float* d_costs = nullptr;
     float* d_wrec = nullptr;
-    hipGraphExec_t g_step = nullptr, g_dev = nullptr;
+    float* d_part = nullptr;  // first-level merge partials (rank-record format)
+    hipGraphExec_t g_step[2] = {nullptr, nullptr}, g_dev2 = nullptr, g_dev1 = nullptr;
     bool input_ready = false;
     std::string err;
 };
@@ -219,8 +238,10 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     srbd_ctx* c = new srbd_ctx();
     c->cfg = *cfg;
     c->mc = mc;
+    c->mode = rollout_mode(mc.kind, mc.n_local);
     c->threads = rollout_threads(mc.n_local);
-    c->nblocks = (mc.n_local + c->threads - 1) / c->threads;
+    const int spb = c->mode == ROLLOUT_QUAD ? 64 : c->threads;  // samples per rollout block
+    c->nblocks = (mc.n_local + spb - 1) / spb;
     if (c->nblocks > MAX_RECORDS) {
         delete c;
         return fail(nullptr, SRBD_E_INVALID, "too many samples per rank");
@@ -245,13 +266,20 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     const size_t noise_bytes = sizeof(float) * (size_t)mc.P * mc.ldn;
     if ((e = hipMalloc((void**)&c->d_in, sizeof(StepInput))) != hipSuccess) return cleanup_fail("hipMalloc", e);
     if ((e = hipMalloc((void**)&c->d_out, sizeof(StepOutput))) != hipSuccess) return cleanup_fail("hipMalloc", e);
-    if ((e = hipMalloc((void**)&c->d_noise, noise_bytes)) != hipSuccess) return cleanup_fail("hipMalloc", e);
+    for (int b = 0; b < 2; ++b)
+        if ((e = hipMalloc((void**)&c->d_noise[b], noise_bytes)) != hipSuccess) return cleanup_fail("hipMalloc", e);
     if ((e = hipMalloc((void**)&c->d_costs, sizeof(float) * mc.ldn)) != hipSuccess)
         return cleanup_fail("hipMalloc", e);
     if ((e = hipMalloc((void**)&c->d_wrec, sizeof(float) * (size_t)c->nblocks * c->wrec_stride)) != hipSuccess)
         return cleanup_fail("hipMalloc", e);
-    if ((e = hipMemsetAsync(c->d_noise, 0, noise_bytes, c->stream)) != hipSuccess)
-        return cleanup_fail("hipMemset", e);
+    {
+        const int m = merge_partials(c->nblocks);
+        if (m > 0 && (e = hipMalloc((void**)&c->d_part, sizeof(float) * (size_t)m * c->rrec_stride)) != hipSuccess)
+            return cleanup_fail("hipMalloc", e);
+    }
+    for (int b = 0; b < 2; ++b)
+        if ((e = hipMemsetAsync(c->d_noise[b], 0, noise_bytes, c->stream)) != hipSuccess)
+            return cleanup_fail("hipMemset", e);
     if ((e = hipMemsetAsync(c->d_in, 0, sizeof(StepInput), c->stream)) != hipSuccess)
         return cleanup_fail("hipMemset", e);
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return cleanup_fail("hipStreamSynchronize", e);
@@ -263,14 +291,17 @@ extern "C" void srbd_destroy(srbd_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device_id);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->g_step) (void)hipGraphExecDestroy(c->g_step);
-    if (c->g_dev) (void)hipGraphExecDestroy(c->g_dev);
+    for (int b = 0; b < 2; ++b)
+        if (c->g_step[b]) (void)hipGraphExecDestroy(c->g_step[b]);
+    if (c->g_dev2) (void)hipGraphExecDestroy(c->g_dev2);
+    if (c->g_dev1) (void)hipGraphExecDestroy(c->g_dev1);
+    for (int b = 0; b < 2; ++b) (void)hipFree(c->d_noise[b]);
     (void)hipFree(c->d_in);
     (void)hipFree(c->d_out);
-    (void)hipFree(c->d_noise);
     (void)hipFree(c->d_noise_rm);
     (void)hipFree(c->d_costs);
     (void)hipFree(c->d_wrec);
+    (void)hipFree(c->d_part);
     if (c->h_in) (void)hipHostFree(c->h_in);
     if (c->h_out) (void)hipHostFree(c->h_out);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -284,9 +315,13 @@ extern "C" int srbd_set_stream(srbd_ctx* c, void* s) {
     (void)hipSetDevice(c->cfg.device_id);
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->own_stream) HIP_TRY(c, hipStreamDestroy(c->stream));
-    if (c->g_step) (void)hipGraphExecDestroy(c->g_step);
-    if (c->g_dev) (void)hipGraphExecDestroy(c->g_dev);
-    c->g_step = c->g_dev = nullptr;
+    for (int b = 0; b < 2; ++b) {
+        if (c->g_step[b]) (void)hipGraphExecDestroy(c->g_step[b]);
+        c->g_step[b] = nullptr;
+    }
+    if (c->g_dev2) (void)hipGraphExecDestroy(c->g_dev2);
+    if (c->g_dev1) (void)hipGraphExecDestroy(c->g_dev1);
+    c->g_dev2 = c->g_dev1 = nullptr;
     if (s) {
         c->stream = (hipStream_t)s;
         c->own_stream = false;
@@ -298,7 +333,13 @@ extern "C" int srbd_set_stream(srbd_ctx* c, void* s) {
 }
 
 // ------------------------------------------------------------------ step
-static int upload_noise(srbd_ctx* c, const float* noise) {
+// Draw the next step's noise inside the rollout launch when the rollout leaves CUs idle (measured:
+// N <= 32768 with four lanes per sample) and the draws do not depend on this step (not CEM).
+static bool fusable(const srbd_ctx* c) {
+    return c->mc.method != SRBD_CEM_MPPI && c->mode == ROLLOUT_QUAD && c->mc.n_local <= 32768;
+}
+
+static int upload_noise(srbd_ctx* c, const float* noise, int buf) {
     const ModelConst& mc = c->mc;
     const size_t bytes = sizeof(float) * (size_t)mc.n_local * mc.P;
     if (c->noise_rm_cap < bytes) {
@@ -309,21 +350,40 @@ static int upload_noise(srbd_ctx* c, const float* noise) {
         c->noise_rm_cap = bytes;
     }
     HIP_TRY(c, hipMemcpyAsync(c->d_noise_rm, noise, bytes, hipMemcpyHostToDevice, c->stream));
-    launch_transpose(c->d_noise_rm, mc.n_local, mc.P, mc.ldn, c->d_noise, c->stream);
+    launch_transpose(c->d_noise_rm, mc.n_local, mc.P, mc.ldn, c->d_noise[buf], c->stream);
     return SRBD_OK;
 }
 
-// The device part of one step: [noise] -> rollout -> merge.
-static void enqueue_device_step(srbd_ctx* c, bool gen_noise, float* rank_out, StepOutput* out) {
-    const ModelConst& mc = c->mc;
-    if (gen_noise) launch_rng(mc, c->d_in, c->d_noise, c->stream);
-    launch_rollout(mc, c->d_in, c->d_noise, c->d_costs, c->d_wrec, c->wrec_stride, c->threads, c->stream);
-    launch_merge(mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, 0, c->d_noise, rank_out, out, c->stream);
+// Noise of a step: injected (noise != NULL), the draws the previous step's rollout launch made when
+// (seed, counter) match its prediction, else device draws generated now on the step's stream.
+// Returns in *buf the buffer holding them.  Everything is ordered on one stream.
+static int acquire_noise(srbd_ctx* c, const float* noise, uint64_t seed, uint64_t ctr, int* buf) {
+    int rc = SRBD_OK;
+    if (!noise && c->pref_valid && c->pref_seed == seed && c->pref_ctr == ctr) {
+        *buf = c->pref_buf;
+    } else {
+        *buf = c->cur;
+        if (noise) rc = upload_noise(c, noise, *buf);
+        else launch_rng(c->mc, c->d_in, seed, ctr, 0, 0, c->d_noise[*buf], c->stream);
+    }
+    c->pref_valid = false;
+    c->cur = *buf;
+    return rc;
 }
 
-static int enqueue_full_step(srbd_ctx* c, bool gen_noise) {
-    HIP_TRY(c, hipMemcpyAsync(c->d_in, c->h_in, sizeof(StepInput), hipMemcpyHostToDevice, c->stream));
-    enqueue_device_step(c, gen_noise, nullptr, c->d_out);
+// rollout (+ next draws, counter + 1 from the device StepInput) -> merge on noise buffer `buf`
+static void enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput* out, int chain = 0,
+                                int ctr_inc = 1, bool fuse_next = false) {
+    const ModelConst& mc = c->mc;
+    const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1};
+    launch_rollout(mc, c->d_in, c->d_noise[buf], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
+                   c->stream, fuse_next ? &next : nullptr);
+    launch_merge_tree(mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, c->d_noise[buf], c->d_part, rank_out, out,
+                      chain, c->stream, ctr_inc);
+}
+
+static int enqueue_full_step(srbd_ctx* c, int buf, bool fuse_next) {
+    enqueue_device_step(c, buf, nullptr, c->d_out, 0, 0, fuse_next);
     HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(StepOutput), hipMemcpyDeviceToHost, c->stream));
     return SRBD_OK;
 }
@@ -350,24 +410,32 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     int rc = fill_input(&c->cfg, c->mc, c->h_in, state, ref, contact, contact_stride, best, sigma, seed, counter);
     if (rc) return fail(c, rc, "invalid step arguments");
-    if (noise) {
-        if ((rc = upload_noise(c, noise))) return rc;
-        if ((rc = enqueue_full_step(c, false))) return rc;
-    } else if (c->cfg.use_graph && c->own_stream) {
-        if (!c->g_step) {
+    c->h_in->noise_scaled = noise ? 1 : 0;
+    HIP_TRY(c, hipMemcpyAsync(c->d_in, c->h_in, sizeof(StepInput), hipMemcpyHostToDevice, c->stream));
+    int buf = 0;
+    if ((rc = acquire_noise(c, noise, seed, counter, &buf))) return rc;
+    const bool fuse = !noise && fusable(c);
+    if (fuse && c->cfg.use_graph && c->own_stream) {
+        if (!c->g_step[buf]) {
             hipGraph_t g;
             HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-            rc = enqueue_full_step(c, true);
+            rc = enqueue_full_step(c, buf, true);
             hipError_t e = hipStreamEndCapture(c->stream, &g);
             if (rc) return rc;
             HIP_TRY(c, e);
-            e = hipGraphInstantiate(&c->g_step, g, nullptr, nullptr, 0);
+            e = hipGraphInstantiate(&c->g_step[buf], g, nullptr, nullptr, 0);
             (void)hipGraphDestroy(g);
             HIP_TRY(c, e);
         }
-        HIP_TRY(c, hipGraphLaunch(c->g_step, c->stream));
+        HIP_TRY(c, hipGraphLaunch(c->g_step[buf], c->stream));
     } else {
-        if ((rc = enqueue_full_step(c, true))) return rc;
+        if ((rc = enqueue_full_step(c, buf, fuse))) return rc;
+    }
+    if (fuse) {
+        c->pref_valid = true;
+        c->pref_buf = 1 - buf;
+        c->pref_seed = seed;
+        c->pref_ctr = counter + 1;
     }
     if (out_costs)
         HIP_TRY(c, hipMemcpyAsync(out_costs, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,
@@ -390,9 +458,19 @@ extern "C" int srbd_step_local(srbd_ctx* c, const float* state, const float* ref
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     int rc = fill_input(&c->cfg, c->mc, c->h_in, state, ref, contact, contact_stride, best, sigma, seed, counter);
     if (rc) return fail(c, rc, "invalid step arguments");
-    if (noise_local && (rc = upload_noise(c, noise_local))) return rc;
+    c->h_in->noise_scaled = noise_local ? 1 : 0;
     HIP_TRY(c, hipMemcpyAsync(c->d_in, c->h_in, sizeof(StepInput), hipMemcpyHostToDevice, c->stream));
-    enqueue_device_step(c, noise_local == nullptr, (float*)d_record, nullptr);
+    int buf = 0;
+    if ((rc = acquire_noise(c, noise_local, seed, counter, &buf))) return rc;
+    const bool fuse = !noise_local && fusable(c);
+    enqueue_device_step(c, buf, (float*)d_record, nullptr, 0, 0, fuse);
+    if (fuse) {
+        c->pref_valid = true;
+        c->pref_buf = 1 - buf;
+        c->pref_seed = seed;
+        c->pref_ctr = counter + 1;
+    }
+    c->chain_started = false;
     HIP_TRY(c, hipGetLastError());
     c->input_ready = true;
     return SRBD_OK;
@@ -403,7 +481,7 @@ extern "C" int srbd_step_finish(srbd_ctx* c, const void* d_records, int32_t nrec
     if (!c || !d_records || nrec < 1 || !best) return SRBD_E_INVALID;
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "srbd_step_finish before srbd_step_local");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
-    launch_merge(c->mc, c->d_in, (const float*)d_records, nrec, c->rrec_stride, 1, nullptr, nullptr, c->d_out,
+    launch_merge(c->mc, c->d_in, (const float*)d_records, nrec, c->rrec_stride, 1, nullptr, nullptr, c->d_out, 0,
                  c->stream);
     HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(StepOutput), hipMemcpyDeviceToHost, c->stream));
     if (out_costs_local)
@@ -414,11 +492,21 @@ extern "C" int srbd_step_finish(srbd_ctx* c, const void* d_records, int32_t nrec
     return copy_out(c, best, sigma, out);
 }
 
+// Device-resident sharded chain: draws keyed by the device counter, which srbd_device_step_finish
+// advances after the merge.
 extern "C" int srbd_device_step_local(srbd_ctx* c, void* d_record) {
     if (!c || !d_record) return SRBD_E_INVALID;
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step_local once first");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
-    enqueue_device_step(c, true, (float*)d_record, nullptr);
+    const bool fuse = fusable(c);
+    if (!c->chain_started || !fuse) {  // draws of this step (device counter); later ones come fused
+        c->cur = 0;
+        launch_rng(c->mc, c->d_in, 0, 0, 1, 0, c->d_noise[0], c->stream);
+    }
+    c->pref_valid = false;
+    enqueue_device_step(c, c->cur, (float*)d_record, nullptr, 0, 0, fuse);
+    if (fuse) c->cur = 1 - c->cur;
+    c->chain_started = true;
     HIP_TRY(c, hipGetLastError());
     return SRBD_OK;
 }
@@ -427,9 +515,8 @@ extern "C" int srbd_device_step_finish(srbd_ctx* c, const void* d_records, int32
     if (!c || !d_records || nrec < 1) return SRBD_E_INVALID;
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step_local once first");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
-    launch_merge(c->mc, c->d_in, (const float*)d_records, nrec, c->rrec_stride, 1, nullptr, nullptr, c->d_out,
-                 c->stream);
-    launch_advance(c->mc, c->d_in, c->d_out, c->stream);
+    launch_merge(c->mc, c->d_in, (const float*)d_records, nrec, c->rrec_stride, 1, nullptr, nullptr, c->d_out, 1,
+                 c->stream, nullptr, 1);
     HIP_TRY(c, hipGetLastError());
     return SRBD_OK;
 }
@@ -574,31 +661,53 @@ extern "C" int srbd_finish_host(const srbd_config* cfg, const float* recs, int32
 }
 
 // ------------------------------------------------------------------ measurement
+// Device-resident chain (benchmark): two steps per graph, each step's rollout launch also drawing
+// the next step's noise into the other buffer (device counter + 1), each merge writing the warm
+// start back and advancing the counter.  CEM (draws depend on the new sigma): draws inline.
+static int capture_dev_graphs(srbd_ctx* c) {
+    hipGraph_t g;
+    const bool fuse = fusable(c);
+    HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    for (int half = 0; half < 2; ++half) {
+        const int buf = fuse ? half : 0;
+        if (!fuse) launch_rng(c->mc, c->d_in, 0, 0, 1, 0, c->d_noise[0], c->stream);
+        enqueue_device_step(c, buf, nullptr, c->d_out, /*chain=*/1, /*ctr_inc=*/1, fuse);
+    }
+    HIP_TRY(c, hipStreamEndCapture(c->stream, &g));
+    hipError_t e = hipGraphInstantiate(&c->g_dev2, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    HIP_TRY(c, e);
+    HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    if (!fuse) launch_rng(c->mc, c->d_in, 0, 0, 1, 0, c->d_noise[0], c->stream);
+    enqueue_device_step(c, 0, nullptr, c->d_out, 1, 1, fuse);
+    HIP_TRY(c, hipStreamEndCapture(c->stream, &g));
+    e = hipGraphInstantiate(&c->g_dev1, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    HIP_TRY(c, e);
+    return SRBD_OK;
+}
+
 extern "C" int srbd_bench_device_steps(srbd_ctx* c, int32_t steps, float* ms) {
     if (!c || steps < 1 || !ms) return SRBD_E_INVALID;
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step once before benchmarking");
-    if (c->cfg.world_size > 1) return fail(c, SRBD_E_STATE, "sharded context");
+    if (c->cfg.world_size > 1 || !c->own_stream) return fail(c, SRBD_E_STATE, "needs an unsharded, own-stream context");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
-    if (!c->g_dev) {
-        hipGraph_t g;
-        HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-        enqueue_device_step(c, true, nullptr, c->d_out);
-        launch_advance(c->mc, c->d_in, c->d_out, c->stream);
-        HIP_TRY(c, hipStreamEndCapture(c->stream, &g));
-        hipError_t e = hipGraphInstantiate(&c->g_dev, g, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(g);
-        HIP_TRY(c, e);
-    }
+    c->pref_valid = false;
+    int rc;
+    if (!c->g_dev2 && (rc = capture_dev_graphs(c))) return rc;
     hipEvent_t e0, e1;
     HIP_TRY(c, hipEventCreate(&e0));
     HIP_TRY(c, hipEventCreate(&e1));
     HIP_TRY(c, hipEventRecord(e0, c->stream));
-    for (int i = 0; i < steps; ++i) HIP_TRY(c, hipGraphLaunch(c->g_dev, c->stream));
+    if (fusable(c)) launch_rng(c->mc, c->d_in, 0, 0, 1, 0, c->d_noise[0], c->stream);  // first step's draws
+    for (int i = 0; i < steps / 2; ++i) HIP_TRY(c, hipGraphLaunch(c->g_dev2, c->stream));
+    if (steps & 1) HIP_TRY(c, hipGraphLaunch(c->g_dev1, c->stream));
     HIP_TRY(c, hipEventRecord(e1, c->stream));
     HIP_TRY(c, hipEventSynchronize(e1));
     HIP_TRY(c, hipEventElapsedTime(ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    c->cur = 0;
     return SRBD_OK;
 }
 
@@ -606,17 +715,20 @@ extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, 
     if (!c || iters < 1) return SRBD_E_INVALID;
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step once before timing");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    c->pref_valid = false;
+    c->cur = 0;
     std::vector<hipEvent_t> ev(4 * iters);
     for (auto& e : ev) HIP_TRY(c, hipEventCreate(&e));
     const ModelConst& mc = c->mc;
     for (int i = 0; i < iters; ++i) {
         HIP_TRY(c, hipEventRecord(ev[4 * i], c->stream));
-        launch_rng(mc, c->d_in, c->d_noise, c->stream);
+        launch_rng(mc, c->d_in, 0, 0, 1, 0, c->d_noise[0], c->stream);
         HIP_TRY(c, hipEventRecord(ev[4 * i + 1], c->stream));
-        launch_rollout(mc, c->d_in, c->d_noise, c->d_costs, c->d_wrec, c->wrec_stride, c->threads, c->stream);
+        launch_rollout(mc, c->d_in, c->d_noise[0], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
+                       c->stream);
         HIP_TRY(c, hipEventRecord(ev[4 * i + 2], c->stream));
-        launch_merge(mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, 0, c->d_noise, nullptr, c->d_out,
-                     c->stream);
+        launch_merge_tree(mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, c->d_noise[0], c->d_part, nullptr,
+                          c->d_out, 0, c->stream);
         HIP_TRY(c, hipEventRecord(ev[4 * i + 3], c->stream));
     }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -634,6 +746,28 @@ extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, 
     if (rng_us) *rng_us = (float)(a * 1000.0 / iters);
     if (rollout_us) *rollout_us = (float)(b * 1000.0 / iters);
     if (reduce_us) *reduce_us = (float)(d * 1000.0 / iters);
+    return SRBD_OK;
+}
+
+// Diagnostic: average duration (us) of the merge kernel's phases from s_memrealtime stamps (100 MHz):
+// [min key, weighted sums, elite, outputs, tail].
+extern "C" int srbd_debug_merge_phases(srbd_ctx* c, int32_t iters, float* out_us) {
+    if (!c || iters < 1 || !out_us) return SRBD_E_INVALID;
+    if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step once first");
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    uint64_t* d = nullptr;
+    HIP_TRY(c, hipMalloc((void**)&d, 8 * sizeof(uint64_t)));
+    double acc[5] = {0, 0, 0, 0, 0};
+    for (int i = 0; i < iters; ++i) {
+        launch_merge(c->mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, 0, c->d_noise[c->cur], nullptr,
+                     c->d_out, 0, c->stream, d);
+        uint64_t h[8];
+        HIP_TRY(c, hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        for (int k = 0; k < 5; ++k) acc[k] += (double)(h[k + 1] - h[k]) * 0.01;  // 100 MHz ticks -> us
+    }
+    (void)hipFree(d);
+    for (int k = 0; k < 5; ++k) out_us[k] = (float)(acc[k] / iters);
     return SRBD_OK;
 }
 

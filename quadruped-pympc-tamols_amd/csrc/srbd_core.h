@@ -47,6 +47,8 @@ struct StepInput {
     float fzref[MAXH];  // float32(mass*9.81) / n_stance(n)   (NMPC:377-380)
     float cost_feet;    // sum over feet of (e*0)*e: 0, or NaN when a foot error is not finite
     uint32_t seed_lo, seed_hi, ctr_lo, ctr_hi;
+    int32_t noise_scaled;  // 0: noise holds unscaled CEM draws (device RNG), multiply by sigma on read
+    int32_t pad[3];
     float best[MAXP];
     float sigma[MAXP];
 };
@@ -137,6 +139,50 @@ SRBD_HD void sincos_(float x, float* s, float* c) {
 #endif
 }
 
+// Row c of calculate_inverse(conj) (CMJ:67-91 applied to CMJ:126-132) times omega.  conj has the
+// constant entries a11 = 1, a12 = a21 = a31 = 0, so the reference's cofactor expression reduces to
+//   DET = a33*a22 - a32*a23,  row0 = [1, a32*a13, -(a22*a13)]/DET,  row1 = [0, a33, -a23]/DET,
+//   row2 = [0, -a32, a22]/DET
+// with identical values (only the sign of an exact zero can differ, which cannot change a cost).
+SRBD_HD void euler_rate_coefs(int c, float sr, float cr, float sp, float cp, float& k1, float& k2) {
+    const float a13 = -sp, a22 = cr, a23 = cp * sr, a32 = -sr, a33 = cp * cr;
+    const float DET = a33 * a22 - a32 * a23;
+    const float n1 = c == 0 ? a32 * a13 : (c == 1 ? a33 : -a32);
+    const float n2 = c == 0 ? -(a22 * a13) : (c == 1 ? -a23 : a22);
+    const float ad = fabsf(DET);
+    if (ad > 1e-30f && ad < 1e30f) {
+        const float r = 1.0f / DET;
+        k1 = div_by(n1, DET, r);
+        k2 = div_by(n2, DET, r);
+    } else {
+        k1 = n1 / DET;
+        k2 = n2 / DET;
+    }
+}
+
+SRBD_HD float euler_rate_row(int c, float k1, float k2, float w0, float w1, float w2) {
+    return (c == 0 ? w0 + k1 * w1 : k1 * w1) + k2 * w2;
+}
+
+SRBD_HD void euler_rates(float sr, float cr, float sp, float cp, float w0, float w1, float w2, float er[3]) {
+    const float a13 = -sp, a22 = cr, a23 = cp * sr, a32 = -sr, a33 = cp * cr;
+    const float DET = a33 * a22 - a32 * a23;
+    const float n[6] = {a32 * a13, -(a22 * a13), a33, -a23, -a32, a22};
+    float k[6];
+    const float ad = fabsf(DET);
+    if (ad > 1e-30f && ad < 1e30f) {
+        const float r = 1.0f / DET;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) k[i] = div_by(n[i], DET, r);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) k[i] = n[i] / DET;
+    }
+    er[0] = euler_rate_row(0, k[0], k[1], w0, w1, w2);
+    er[1] = euler_rate_row(1, k[2], k[3], w0, w1, w2);
+    er[2] = euler_rate_row(2, k[4], k[5], w0, w1, w2);
+}
+
 // Centroidal_Model_JAX.fd + integrate_jax (CMJ:93-174).  x: 12 evolving states, feet: 12
 // (constant over the rollout), F: 12 clipped foot forces, c: 4 contact flags.
 SRBD_HD void integrate(const ModelConst& mc, float x[12], const float feet[12], const float F[12], const float c[4],
@@ -168,10 +214,8 @@ SRBD_HD void integrate(const ModelConst& mc, float x[12], const float feet[12], 
         }
     }
 
-    const float conj[9] = {1.0f, 0.0f, -sp, 0.0f, cr, cp * sr, 0.0f, -sr, cp * cr};
-    float Cinv[9], er[3];
-    inv3(conj, Cinv);
-    mv3(Cinv, x + 9, er);
+    float er[3];
+    euler_rates(sr, cr, sp, cp, x[9], x[10], x[11], er);
 
     const float R[9] = {cp * cy, cp * sy, -sp,
                         sr * sp * cy - cr * sy, sr * sp * sy + cr * cy, sr * cp,

@@ -10,18 +10,32 @@
 //   merge_kernel      merges block (or rank) records: global argmin, MPPI/CEM softmax-weighted
 //                     update, CEM sigma, final GRF decode + predicted state
 //   advance_kernel    device-resident warm start for back-to-back steps (benchmark chain)
+#include <utility>
+
 #include "srbd_launch.h"
 
 namespace srbd {
 
 // ------------------------------------------------------------------ helpers
+// 64-bit wave minimum with DPP (row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15/31, gfx9
+// family), result read from lane 63.  All 64 lanes must be active.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)(uint32_t)v, CTRL, ROWMASK, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)(uint32_t)(v >> 32), CTRL, ROWMASK, 0xF, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return b < a ? b : a; }
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t w = __shfl_xor(v, o);
-        v = w < v ? w : v;
-    }
-    return v;
+    v = umin64(v, dpp_u64<0x111, 0xF>(v));
+    v = umin64(v, dpp_u64<0x112, 0xF>(v));
+    v = umin64(v, dpp_u64<0x114, 0xF>(v));
+    v = umin64(v, dpp_u64<0x118, 0xF>(v));
+    v = umin64(v, dpp_u64<0x142, 0xA>(v));
+    v = umin64(v, dpp_u64<0x143, 0xC>(v));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+    return ((uint64_t)hi << 32) | lo;
 }
 
 // Block-wide min; every thread gets the result.  `red` holds blockDim/64 words.
@@ -59,11 +73,9 @@ __device__ __forceinline__ float u01(uint32_t x) { return ((float)(x >> 8) + 0.5
 // Noise row r (global), column j.  MPPI: sigma*Z(r-1, j); CEM: Z(r-1, j)*sigma_j; random sampling
 // (NMPC:647-677): rows 1..t sigma0*Z(r-1), rows t+1..2t sigma1*Z(r-1-t) (same draws: the reference
 // reuses one key, App. B #3), rows 2t+1..N-1 U(-s2, s2) from draw r-1-2t.  Row 0 is zero.
-__global__ void __launch_bounds__(256) rng_kernel(const ModelConst mc, const StepInput* __restrict__ in,
-                                                  float* __restrict__ noise) {
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    const int q = blockIdx.y;
-    if (k >= mc.n_local) return;
+// One item = (local row k, column quad q): one Philox4x32-10 call, two Box-Muller pairs.
+__device__ __forceinline__ void rng_item(const ModelConst& mc, const float* __restrict__ sigma, uint64_t seed,
+                                         uint64_t ctr, int k, int q, float* __restrict__ noise) {
     const int r = mc.row0 + k;
     float v[4] = {0.f, 0.f, 0.f, 0.f};
     if (r > 0) {
@@ -81,8 +93,8 @@ __global__ void __launch_bounds__(256) rng_kernel(const ModelConst mc, const Ste
                 d = (uint32_t)(r - 1 - 2 * t);
             }
         }
-        uint32_t c[4] = {d, (uint32_t)q, in->ctr_lo, in->ctr_hi};
-        philox4x32_10(c, in->seed_lo, in->seed_hi);
+        uint32_t c[4] = {d, (uint32_t)q, (uint32_t)ctr, (uint32_t)(ctr >> 32)};
+        philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
         if (mode == 2) {
             const float s2 = mc.sigma_rs[2];
 #pragma unroll
@@ -94,7 +106,7 @@ __global__ void __launch_bounds__(256) rng_kernel(const ModelConst mc, const Ste
                 const float ua = u01(c[2 * h]), ub = u01(c[2 * h + 1]);
                 const float rr = sqrtf(-2.0f * logf(ua));
                 float s, co;
-                sincosf(6.2831853071795864769f * ub, &s, &co);
+                sincospif(2.0f * ub, &s, &co);  // sin/cos(2 pi ub) without a large-argument reduction
                 z[2 * h] = rr * co;
                 z[2 * h + 1] = rr * s;
             }
@@ -104,7 +116,7 @@ __global__ void __launch_bounds__(256) rng_kernel(const ModelConst mc, const Ste
                 if (mode == 0) v[i] = mc.sigma_rs[0] * z[i];
                 else if (mode == 1) v[i] = mc.sigma_rs[1] * z[i];
                 else if (mode == 3) v[i] = mc.sigma_mppi * z[i];
-                else v[i] = z[i] * in->sigma[j < mc.P ? j : 0];
+                else v[i] = z[i] * sigma[j < mc.P ? j : 0];
             }
         }
     }
@@ -113,6 +125,27 @@ __global__ void __launch_bounds__(256) rng_kernel(const ModelConst mc, const Ste
         const int j = 4 * q + i;
         if (j < mc.P) noise[(size_t)j * mc.ldn + k] = v[i];
     }
+}
+
+// Items (k, q) enumerated k-fastest so consecutive lanes store consecutive floats.
+__device__ __forceinline__ void rng_items(const ModelConst& mc, const StepInput* __restrict__ in, const RngJob& job,
+                                          int first, int stride) {
+    uint64_t seed = job.seed, ctr = job.ctr;
+    if (job.dev_ctr) {
+        seed = ((uint64_t)in->seed_hi << 32) | in->seed_lo;
+        ctr = (((uint64_t)in->ctr_hi << 32) | in->ctr_lo) + (uint64_t)job.ctr_offset;
+    }
+    const int nq = (mc.P + 3) / 4;
+    const int total = mc.n_local * nq;
+    for (int it = first; it < total; it += stride) {
+        const int q = it / mc.n_local, k = it - q * mc.n_local;
+        rng_item(mc, in->sigma, seed, ctr, k, q, job.noise);
+    }
+}
+
+__global__ void __launch_bounds__(256) rng_kernel(const ModelConst mc, const StepInput* __restrict__ in,
+                                                  const RngJob job) {
+    rng_items(mc, in, job, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256);
 }
 
 // row-major (n x P) -> SoA [P][ldn]
@@ -137,10 +170,86 @@ __global__ void __launch_bounds__(256) transpose_kernel(const float* __restrict_
 // integer n, NMPC:187-189).
 __host__ __device__ constexpr int chunk_index(int n, int H, int S) { return (n * S) / H; }
 
+template <int N>
+struct IntC {
+    static constexpr int value = N;
+};
+template <class F, int... Ns>
+__device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, Ns...>) {
+    (f(IntC<Ns>{}), ...);
+}
+
+// Per-block record (see srbd_core.h REC_*): min key, sum_k e_k, sum_k e_k * noise_k[j], top-K keys,
+// e_k = exp(-(c_k - m_b)).  SPB samples per block (multiple of 4); the thread owning sample `sib`
+// passes it (others pass sib = -1).  All threads of the block must call this.
+__device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepInput* __restrict__ in, const int SPB,
+                                               int sib, bool valid, float cost, const float* __restrict__ noise,
+                                               float* __restrict__ recs, int rec_stride, float* e_sh, uint64_t* red,
+                                               uint64_t* elite_sh) {
+    const int tid = threadIdx.x, T = blockDim.x;
+    const int k0 = blockIdx.x * SPB;
+    const uint64_t key = (sib >= 0 && valid) ? cost_key(cost, (uint32_t)(mc.row0 + k0 + sib)) : ~0ull;
+    const uint64_t bkey = block_min_u64(key, red);
+    const float m = u2f((uint32_t)(bkey >> 32));
+    float* rec = recs + (size_t)blockIdx.x * rec_stride;
+    const int P = mc.P, K = mc.K;
+    if (tid == 0) elite_sh[0] = bkey;
+    uint64_t last = bkey;
+    for (int r = 1; r < K; ++r) {
+        const uint64_t cand = key > last ? key : ~0ull;
+        last = block_min_u64(cand, red);
+        if (tid == 0) elite_sh[r] = last;
+    }
+    if (mc.method != SRBD_RANDOM_SAMPLING) {
+        if (sib >= 0) e_sh[sib] = valid ? expf(-1.0f * (cost - m)) : 0.0f;
+        __syncthreads();
+        const size_t ldn = (size_t)mc.ldn;
+        const float* base = noise + k0;
+        for (int j = tid; j <= P; j += T) {
+            float a = 0.0f;
+            if (j < P) {
+                const float4* row = reinterpret_cast<const float4*>(base + (size_t)j * ldn);
+#pragma unroll 4
+                for (int i = 0; i < SPB / 4; ++i) {
+                    const float4 v = row[i];
+                    a = a + e_sh[4 * i] * v.x;
+                    a = a + e_sh[4 * i + 1] * v.y;
+                    a = a + e_sh[4 * i + 2] * v.z;
+                    a = a + e_sh[4 * i + 3] * v.w;
+                }
+                rec[REC_HDR + j] = a;
+            } else {
+                for (int i = 0; i < SPB; ++i) a = a + e_sh[i];
+                rec[1] = a;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        rec[0] = m;
+        rec[2] = u2f((uint32_t)bkey);
+        rec[3] = 0.0f;
+        if (mc.method == SRBD_RANDOM_SAMPLING) rec[1] = 1.0f;
+    }
+    if (tid < K) {
+        const uint64_t kk = elite_sh[tid];
+        rec[REC_HDR + P + 2 * tid] = u2f((uint32_t)kk);
+        rec[REC_HDR + P + 2 * tid + 1] = u2f((uint32_t)(kk >> 32));
+    }
+}
+
+// One thread per sample.  Best throughput when samples fill the GPU (>= ~1 wave per SIMD).
 template <int KIND, int HT, int ST>
 __global__ void __launch_bounds__(256) rollout_kernel(const ModelConst mc, const StepInput* __restrict__ in,
                                                       const float* __restrict__ noise, float* __restrict__ costs,
-                                                      float* __restrict__ recs, int rec_stride) {
+                                                      float* __restrict__ recs, int rec_stride,
+    const RngJob next_rng, int nroll) {
+    // blocks past the rollout grid generate the next step's noise on the CUs the rollout leaves idle
+    if ((int)blockIdx.x >= nroll) {
+        rng_items(mc, in, next_rng, ((int)blockIdx.x - nroll) * (int)blockDim.x + (int)threadIdx.x,
+                  ((int)gridDim.x - nroll) * (int)blockDim.x);
+        return;
+    }
     __shared__ float e_sh[256];
     __shared__ uint64_t red[4];
     __shared__ uint64_t elite_sh[MAXK];
@@ -165,7 +274,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(const ModelConst mc, const
     }
     float cost = 0.0f;
 
-    auto step = [&](const int n) {
+    auto step = [&](const int n) __attribute__((always_inline)) {
         const float c[4] = {in->contact[0][n], in->contact[1][n], in->contact[2][n], in->contact[3][n]};
         const float fref = in->fzref[n];
         const int idx = CT && KIND != SRBD_ZERO_ORDER ? chunk_index(n, HT, ST) : mc.sidx[n];
@@ -194,63 +303,184 @@ __global__ void __launch_bounds__(256) rollout_kernel(const ModelConst mc, const
         cost = cost + a;
     };
     if constexpr (CT) {
-#pragma unroll
-        for (int n = 0; n < HT; ++n) step(n);
+        unroll_seq([&](auto nc) { step(decltype(nc)::value); }, std::make_integer_sequence<int, (CT ? HT : 1)>{});
     } else {
         for (int n = 0; n < H; ++n) step(n);
     }
     // NMPC:686-687
     if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
     if (valid && costs) costs[k] = cost;
+    block_epilogue(mc, in, T, tid, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh);
+}
 
-    // ---- epilogue: block record
-    const uint32_t grow = (uint32_t)(mc.row0 + k);
-    const uint64_t key = valid ? cost_key(cost, grow) : ~0ull;
-    const uint64_t bkey = block_min_u64(key, red);
-    const float m = u2f((uint32_t)(bkey >> 32));
-    float* rec = recs + (size_t)blockIdx.x * rec_stride;
-    const int P = mc.P, K = mc.K;
-    if (tid == 0) elite_sh[0] = bkey;
-    uint64_t last = bkey;
-    for (int r = 1; r < K; ++r) {
-        const uint64_t cand = key > last ? key : ~0ull;
-        last = block_min_u64(cand, red);
-        if (tid == 0) elite_sh[r] = last;
+// ---- four lanes per sample: lane c in {0,1,2} owns component c (x, y, z) of every 3-vector of
+// the model (forces per leg, torques, p, v, rpy, omega); lane 3 mirrors lane 2.  Cross-lane data
+// moves are DPP quad permutations.  Every float operation is the one the thread-per-sample kernel
+// performs, in the same order, so both kernels give bitwise identical costs; the 4x wave count
+// and ~1.6x shorter per-lane instruction stream cut the latency when N is too small to fill
+// the GPU one sample per lane.
+constexpr int QP_B0 = 0x00, QP_B1 = 0x55, QP_B2 = 0xAA;  // quad_perm broadcast of lane 0/1/2
+constexpr int QP_NEXT = 0x09;   // lanes (0,1,2,3) <- (1,2,0,0): component c+1 (mod 3)
+constexpr int QP_NEXT2 = 0x52;  // lanes (0,1,2,3) <- (2,0,1,1): component c+2 (mod 3)
+
+template <int CTRL>
+__device__ __forceinline__ float qp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sel3(int c, float a0, float a1, float a2) { return c == 0 ? a0 : (c == 1 ? a1 : a2); }
+
+template <int KIND, int HT, int ST>
+__global__ void __launch_bounds__(256) rollout_quad_kernel(const ModelConst mc, const StepInput* __restrict__ in,
+                                                           const float* __restrict__ noise, float* __restrict__ costs,
+                                                           float* __restrict__ recs, int rec_stride,
+    const RngJob next_rng, int nroll) {
+    // blocks past the rollout grid generate the next step's noise on the CUs the rollout leaves idle
+    if ((int)blockIdx.x >= nroll) {
+        rng_items(mc, in, next_rng, ((int)blockIdx.x - nroll) * (int)blockDim.x + (int)threadIdx.x,
+                  ((int)gridDim.x - nroll) * (int)blockDim.x);
+        return;
     }
-    if (mc.method != SRBD_RANDOM_SAMPLING) {
-        e_sh[tid] = valid ? expf(-1.0f * (cost - m)) : 0.0f;
-        __syncthreads();
-        const float* base = noise + (size_t)blockIdx.x * T;
-        for (int j = tid; j <= P; j += T) {
-            float s = 0.0f;
-            if (j < P) {
-                const float4* row = reinterpret_cast<const float4*>(base + (size_t)j * ldn);
-                for (int i = 0; i < T / 4; ++i) {
-                    const float4 v = row[i];
-                    s = s + e_sh[4 * i] * v.x;
-                    s = s + e_sh[4 * i + 1] * v.y;
-                    s = s + e_sh[4 * i + 2] * v.z;
-                    s = s + e_sh[4 * i + 3] * v.w;
-                }
-                rec[REC_HDR + j] = s;
+    __shared__ float e_sh[64];
+    __shared__ uint64_t red[4];
+    __shared__ uint64_t elite_sh[MAXK];
+
+    constexpr bool CT = HT > 0 && (KIND == SRBD_ZERO_ORDER || ST > 0);
+    const int H = CT ? HT : mc.H;
+    const int S = CT ? ST : mc.S;
+    const int PL = CT ? (KIND == SRBD_ZERO_ORDER ? 3 * HT : (KIND == SRBD_LINEAR_SPLINE ? 3 * (ST + 1) : 12 * ST))
+                      : mc.PL;
+    const int tid = threadIdx.x;
+    const int q4 = tid & 3;
+    const int c = q4 < 3 ? q4 : 2;
+    const int sib = tid >> 2;
+    const int k = blockIdx.x * 64 + sib;
+    const bool valid = k < mc.n_local;
+    const size_t ldn = (size_t)mc.ldn;
+    const float* __restrict__ nz = noise + k;
+    const float* __restrict__ best = in->best;
+
+    // lane constants
+    const float Ir0 = sel3(c, mc.inertia[0], mc.inertia[3], mc.inertia[6]);
+    const float Ir1 = sel3(c, mc.inertia[1], mc.inertia[4], mc.inertia[7]);
+    const float Ir2 = sel3(c, mc.inertia[2], mc.inertia[5], mc.inertia[8]);
+    const float Ii0 = sel3(c, mc.Iinv[0], mc.Iinv[3], mc.Iinv[6]);
+    const float Ii1 = sel3(c, mc.Iinv[1], mc.Iinv[4], mc.Iinv[7]);
+    const float Ii2 = sel3(c, mc.Iinv[2], mc.Iinv[5], mc.Iinv[8]);
+    const float Qp = sel3(c, mc.Q[0], mc.Q[1], mc.Q[2]), Qv = sel3(c, mc.Q[3], mc.Q[4], mc.Q[5]);
+    const float Qr = sel3(c, mc.Q[6], mc.Q[7], mc.Q[8]), Qw = sel3(c, mc.Q[9], mc.Q[10], mc.Q[11]);
+    const float* st = in->state;
+    const float* rf = in->ref;
+    const float rp = sel3(c, rf[0], rf[1], rf[2]), rv = sel3(c, rf[3], rf[4], rf[5]);
+    const float rr = sel3(c, rf[6], rf[7], rf[8]), rw = sel3(c, rf[9], rf[10], rf[11]);
+    float feet[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) feet[l] = sel3(c, st[12 + 3 * l], st[13 + 3 * l], st[14 + 3 * l]);
+    const float g = c == 2 ? -9.81f : 0.0f;
+    float p = sel3(c, st[0], st[1], st[2]), v = sel3(c, st[3], st[4], st[5]);
+    float r = sel3(c, st[6], st[7], st[8]), w = sel3(c, st[9], st[10], st[11]);
+    float cost = 0.0f;
+
+    auto step = [&](const int n) __attribute__((always_inline)) {
+        const float cl[4] = {in->contact[0][n], in->contact[1][n], in->contact[2][n], in->contact[3][n]};
+        const float fref = in->fzref[n];
+        const int idx = CT && KIND != SRBD_ZERO_ORDER ? chunk_index(n, HT, ST) : mc.sidx[n];
+        float f[4];
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            const int base = l * PL;
+            auto P = [&](int j) { return best[base + j] + nz[(size_t)(base + j) * ldn]; };
+            float raw;
+            if (KIND == SRBD_ZERO_ORDER) {
+                raw = P(n + c * H);
+            } else if (KIND == SRBD_LINEAR_SPLINE) {
+                const int o = idx + c * (S + 1);
+                raw = mc.somq[n] * P(o) + mc.sq[n] * P(o + 1);
             } else {
-                for (int i = 0; i < T; ++i) s = s + e_sh[i];
-                rec[1] = s;
+                const int o = 10 * idx + 4 * c;
+                const float p0 = P(o), p1 = P(o + 1), p2 = P(o + 2), p3 = P(o + 3);
+                const float phi = 0.5f * ((p2 - p1) + (p1 - p0));
+                const float phin = 0.5f * ((p3 - p2) + (p2 - p1));
+                raw = mc.sa[n] * p1 + mc.sb[n] * phi + mc.sc[n] * p2 + mc.sd[n] * phin;
             }
+            // shape_leg / clip_leg, component-wise
+            float zp = (fref + raw) * cl[l];
+            zp = (zp > mc.grf_min) ? zp : mc.grf_min;
+            zp = (zp < mc.grf_max) ? zp : mc.grf_max;
+            float xy = div3(raw * cl[l]);
+            const float fz = qp<QP_B2>(c == 2 ? zp : xy);
+            const float lo = mc.neg_mu * fz, hi = mc.mu * fz;
+            xy = (xy > lo) ? xy : lo;
+            xy = (xy < hi) ? xy : hi;
+            f[l] = c == 2 ? fz : xy;
         }
+        const float temp = f[0] * cl[0] + f[1] * cl[1] + f[2] * cl[2] + f[3] * cl[3];
+        const float lin = mc.inv_m * temp + g;
+        float temp2 = 0.0f;
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            const float vl = feet[l] - p;
+            const float vn1 = qp<QP_NEXT>(vl), vn2 = qp<QP_NEXT2>(vl);
+            const float fn1 = qp<QP_NEXT>(f[l]), fn2 = qp<QP_NEXT2>(f[l]);
+            const float t = (-vn2) * fn1 + vn1 * fn2;
+            temp2 = l == 0 ? t * cl[0] : temp2 + t * cl[l];
+        }
+        float sn, cs;
+        sincosf(r, &sn, &cs);
+        const float sr = qp<QP_B0>(sn), cr = qp<QP_B0>(cs);
+        const float sp = qp<QP_B1>(sn), cp = qp<QP_B1>(cs);
+        const float sy = qp<QP_B2>(sn), cy = qp<QP_B2>(cs);
+        const float w0 = qp<QP_B0>(w), w1 = qp<QP_B1>(w), w2 = qp<QP_B2>(w);
+        float k1, k2;
+        euler_rate_coefs(c, sr, cr, sp, cp, k1, k2);
+        const float er = euler_rate_row(c, k1, k2, w0, w1, w2);
+        // row c of b_R_w (CMJ:136-150)
+        const float A = c == 1 ? sr : cr;
+        const float R0 = c == 0 ? cp * cy : (A * sp) * cy + (c == 1 ? -cr : sr) * sy;
+        const float R1 = c == 0 ? cp * sy : (A * sp) * sy + (c == 1 ? cr : -sr) * cy;
+        const float R2 = c == 0 ? -sp : A * cp;
+        const float Rt = R0 * qp<QP_B0>(temp2) + R1 * qp<QP_B1>(temp2) + R2 * qp<QP_B2>(temp2);
+        const float Iw = Ir0 * w0 + Ir1 * w1 + Ir2 * w2;
+        const float wx = (-qp<QP_NEXT2>(w)) * qp<QP_NEXT>(Iw) + qp<QP_NEXT>(w) * qp<QP_NEXT2>(Iw);
+        const float a1 = Ii0 * qp<QP_B0>(wx) + Ii1 * qp<QP_B1>(wx) + Ii2 * qp<QP_B2>(wx);
+        const float a2 = Ii0 * qp<QP_B0>(Rt) + Ii1 * qp<QP_B1>(Rt) + Ii2 * qp<QP_B2>(Rt);
+        const float aa = -a1 + a2;
+        const float dt = mc.dts[n];
+        const float pn = p + v * dt, vn = v + lin * dt, rn = r + er * dt, wn = w + aa * dt;
+        p = pn;
+        v = vn;
+        r = rn;
+        w = wn;
+        float e;
+        e = p - rp;
+        const float tp = (e * Qp) * e;
+        e = v - rv;
+        const float tv = (e * Qv) * e;
+        e = r - rr;
+        const float tr = (e * Qr) * e;
+        e = w - rw;
+        const float tw = (e * Qw) * e;
+        float a = qp<QP_B0>(tp) + qp<QP_B1>(tp);
+        a = a + qp<QP_B2>(tp);
+        a = a + qp<QP_B0>(tv);
+        a = a + qp<QP_B1>(tv);
+        a = a + qp<QP_B2>(tv);
+        a = a + qp<QP_B0>(tr);
+        a = a + qp<QP_B1>(tr);
+        a = a + qp<QP_B2>(tr);
+        a = a + qp<QP_B0>(tw);
+        a = a + qp<QP_B1>(tw);
+        a = a + qp<QP_B2>(tw);
+        a = a + in->cost_feet;
+        cost = cost + a;
+    };
+    if constexpr (CT) {
+        unroll_seq([&](auto nc) { step(decltype(nc)::value); }, std::make_integer_sequence<int, (CT ? HT : 1)>{});
+    } else {
+        for (int n = 0; n < H; ++n) step(n);
     }
-    __syncthreads();
-    if (tid == 0) {
-        rec[0] = m;
-        rec[2] = u2f((uint32_t)bkey);
-        rec[3] = 0.0f;
-        if (mc.method == SRBD_RANDOM_SAMPLING) rec[1] = 1.0f;
-    }
-    if (tid < K) {
-        const uint64_t kk = elite_sh[tid];
-        rec[REC_HDR + P + 2 * tid] = u2f((uint32_t)kk);
-        rec[REC_HDR + P + 2 * tid + 1] = u2f((uint32_t)(kk >> 32));
-    }
+    if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
+    if (valid && q4 == 0 && costs) costs[k] = cost;
+    block_epilogue(mc, in, 64, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh);
 }
 
 // ------------------------------------------------------------------ merge
@@ -258,104 +488,199 @@ __device__ __forceinline__ uint64_t rec_key(const float* R, int P, int q) {
     return ((uint64_t)f2u(R[REC_HDR + P + 2 * q + 1]) << 32) | (uint64_t)f2u(R[REC_HDR + P + 2 * q]);
 }
 
-__global__ void __launch_bounds__(1024) merge_kernel(const ModelConst mc, const StepInput* __restrict__ in,
-                                                     const float* __restrict__ recs, int nrec, int rec_stride,
-                                                     int rows_in_rec, const float* __restrict__ noise,
-                                                     float* __restrict__ rank_out, StepOutput* __restrict__ out) {
-    extern __shared__ float smem[];  // scale[nrec] | part[G*(P+1)]
-    __shared__ uint64_t red[16];
+constexpr int MERGE_THREADS = 1024;
+constexpr int MERGE_WAVES = MERGE_THREADS / 64;
+constexpr int MERGE_PREF = 24;  // record values of the weighted sums loaded per thread before beta is known
+constexpr int MERGE_RPT = 8;    // record headers per thread (nrec <= MERGE_RPT * MERGE_THREADS)
+constexpr uint64_t KEY_NONE = ~0ull;
+
+// Sorted (ascending) per-lane candidate list of at most MAXK keys; fully unrolled (registers only).
+__device__ __forceinline__ void lk_insert(uint64_t (&lk)[MAXK], uint64_t x) {
+#pragma unroll
+    for (int i = MAXK - 1; i >= 1; --i) lk[i] = (x < lk[i - 1]) ? lk[i - 1] : (x < lk[i] ? x : lk[i]);
+    lk[0] = x < lk[0] ? x : lk[0];
+}
+// K rounds of a wave-wide minimum over the lanes' list heads; the (unique) winning lane pops.
+__device__ __forceinline__ void wave_topk(uint64_t (&lk)[MAXK], int K, uint64_t* out) {
+    for (int e = 0; e < K; ++e) {
+        const uint64_t m = wave_min_u64(lk[0]);
+        const bool pop = lk[0] == m && m != KEY_NONE;
+#pragma unroll
+        for (int i = 0; i < MAXK - 1; ++i) lk[i] = pop ? lk[i + 1] : lk[i];
+        lk[MAXK - 1] = pop ? KEY_NONE : lk[MAXK - 1];
+        if ((threadIdx.x & 63) == 0) out[e] = m;
+    }
+}
+
+// One block merges `nrec` records (per-block records of one rank, or gathered rank records).
+//  L. one memory round trip: record headers (min cost, best row) and the first MERGE_PREF weighted-
+//     sum values of every (column j, record group g) thread;
+//  1. global (min cost, first row) key beta;  2. per-record rescale exp(-(m_r - beta)) -> LDS;
+//  3. sum_r scale_r * v_r[j] and sum_r scale_r * s_r in fixed order (groups, then columns);
+//  4. top-K keys: per-thread sorted lists -> per-wave K-round DPP minima -> one wave over the 16
+//     wave lists; 5. elite rows -> LDS;  6. outputs: rank record and/or final step outputs; with
+//     `chain` the new parameters, sigma and RNG counter are written back into `in` (warm start).
+__global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst mc, StepInput* __restrict__ in,
+                                                              const float* __restrict__ recs, int nrec,
+                                                              int rec_stride, int rows_in_rec,
+                                                              const float* __restrict__ noise,
+                                                              float* __restrict__ rank_out,
+                                                              StepOutput* __restrict__ out, int chain,
+                                                              int ctr_inc, uint64_t* __restrict__ dbg) {
+    extern __shared__ float smem[];  // scale[nrec_pad] | part[G*(P+1)] | erow[K*P]
+    __shared__ uint64_t red[MERGE_WAVES];
+    __shared__ uint64_t wlist[MERGE_WAVES][MAXK];
     __shared__ uint64_t elite[MAXK];
     __shared__ int elite_src[MAXK];
     __shared__ float Vs[MAXP + 1];
     __shared__ float nb[MAXP];
+    __shared__ float grf_sh[12];
+#define MERGE_STAMP(i) \
+    if (dbg && threadIdx.x == 0) dbg[i] = __builtin_amdgcn_s_memrealtime()
+    MERGE_STAMP(0);
 
-    const int tid = threadIdx.x, T = blockDim.x, P = mc.P, K = mc.K;
+    const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wv = tid >> 6;
+    const int P = mc.P, K = mc.K;
     const bool rs = mc.method == SRBD_RANDOM_SAMPLING;
-
-    // 1. global (min cost, first row)
-    uint64_t mine = ~0ull;
-    for (int r = tid; r < nrec; r += T) {
-        const float* R = recs + (size_t)r * rec_stride;
-        const uint64_t kk = ((uint64_t)f2u(R[0]) << 32) | (uint64_t)f2u(R[2]);
-        mine = kk < mine ? kk : mine;
-    }
-    const uint64_t bkey = block_min_u64(mine, red);
-    const float beta = u2f((uint32_t)(bkey >> 32));
-
-    // 2./3. softmax-weighted sums in a fixed order
-    float* scale = smem;
     const int cols = P + 1;
+    if (gridDim.x > 1) {  // first level of a two-level merge: block b reduces its slice into rank_out[b]
+        const int b0 = (int)((long)blockIdx.x * nrec / gridDim.x), b1 = (int)((long)(blockIdx.x + 1) * nrec / gridDim.x);
+        recs += (size_t)b0 * rec_stride;
+        nrec = b1 - b0;
+        rank_out += (size_t)blockIdx.x * rec_floats_rank(P, K);
+    }
+    int G = T / cols;
+    G = G < 1 ? 1 : (G > nrec ? nrec : G);
     const int nrec_pad = (nrec + 3) & ~3;
+    float* scale = smem;
     float* part = smem + nrec_pad;
+    float* erow = part + ((G * cols + 3) & ~3);
+
+    // ---- L: loads
+    float mr[MERGE_RPT];
+    uint64_t mine = KEY_NONE;
+#pragma unroll
+    for (int i = 0; i < MERGE_RPT; ++i) {
+        const int r = tid + i * T;
+        mr[i] = 0.0f;
+        if (r < nrec) {
+            const float* R = recs + (size_t)r * rec_stride;
+            mr[i] = R[0];
+            mine = umin64(mine, ((uint64_t)f2u(mr[i]) << 32) | (uint64_t)f2u(R[2]));
+        }
+    }
+    const int j = tid % cols, g = tid / cols;
+    const bool summer = !rs && tid < G * cols;
+    const int r0 = summer ? (int)((long)g * nrec / G) : 0, r1 = summer ? (int)((long)(g + 1) * nrec / G) : 0;
+    const int off = j < P ? REC_HDR + j : 1;
+    float pv[MERGE_PREF];
+#pragma unroll
+    for (int i = 0; i < MERGE_PREF; ++i) pv[i] = (r0 + i < r1) ? recs[(size_t)(r0 + i) * rec_stride + off] : 0.0f;
+
+    // ---- 1. beta
+    const uint64_t wmin = wave_min_u64(mine);
+    if (lane == 0) red[wv] = wmin;
+    __syncthreads();
+    uint64_t bkey = red[0];
+#pragma unroll
+    for (int i = 1; i < MERGE_WAVES; ++i) bkey = umin64(bkey, red[i]);
+    const float beta = u2f((uint32_t)(bkey >> 32));
+    MERGE_STAMP(1);
+
+    // ---- 2./3. softmax-weighted sums
     if (!rs) {
-        for (int r = tid; r < nrec; r += T) scale[r] = expf(-1.0f * (recs[(size_t)r * rec_stride] - beta));
+#pragma unroll
+        for (int i = 0; i < MERGE_RPT; ++i) {
+            const int r = tid + i * T;
+            if (r < nrec) scale[r] = expf(-1.0f * (mr[i] - beta));
+        }
         __syncthreads();
-        int G = T / cols;
-        G = G < 1 ? 1 : G;
-        if (G > nrec) G = nrec;
-        if (tid < G * cols) {
-            const int j = tid % cols, g = tid / cols;
-            const int r0 = (int)((long)g * nrec / G), r1 = (int)((long)(g + 1) * nrec / G);
+        if (summer) {
             float a = 0.0f;
-            for (int r = r0; r < r1; ++r) {
-                const float* R = recs + (size_t)r * rec_stride;
-                const float val = j < P ? R[REC_HDR + j] : R[1];
-                a = a + scale[r] * val;
+#pragma unroll
+            for (int i = 0; i < MERGE_PREF; ++i)
+                if (r0 + i < r1) a = a + scale[r0 + i] * pv[i];
+            for (int rb = r0 + MERGE_PREF; rb < r1; rb += MERGE_PREF) {
+#pragma unroll
+                for (int i = 0; i < MERGE_PREF; ++i)
+                    pv[i] = (rb + i < r1) ? recs[(size_t)(rb + i) * rec_stride + off] : 0.0f;
+#pragma unroll
+                for (int i = 0; i < MERGE_PREF; ++i)
+                    if (rb + i < r1) a = a + scale[rb + i] * pv[i];
             }
             part[g * cols + j] = a;
         }
         __syncthreads();
-        for (int j = tid; j < cols; j += T) {
+        for (int jj = tid; jj < cols; jj += T) {
             float a = 0.0f;
-            for (int g = 0; g < G; ++g) a = a + part[g * cols + j];
-            Vs[j] = a;
+            for (int gg = 0; gg < G; ++gg) a = a + part[gg * cols + jj];
+            Vs[jj] = a;
         }
     }
+    MERGE_STAMP(2);
 
-    // 4. elite keys in ascending order (keys are unique)
-    uint64_t last = 0;
-    for (int e = 0; e < K; ++e) {
-        uint64_t m2 = ~0ull;
-        int src = -1;
-        for (int t = tid; t < nrec * K; t += T) {
-            const int r = t / K, q = t % K;
-            const uint64_t kk = rec_key(recs + (size_t)r * rec_stride, P, q);
-            if ((e == 0 || kk > last) && kk < m2) {
-                m2 = kk;
-                src = t;
+    // ---- 4. top-K keys (ascending; keys are unique)
+    if (K == 1) {
+        if (tid == 0) elite[0] = bkey;
+    } else {
+        uint64_t lk[MAXK];
+#pragma unroll
+        for (int i = 0; i < MAXK; ++i) lk[i] = KEY_NONE;
+        for (int r = tid; r < nrec; r += T) {
+            const float* R = recs + (size_t)r * rec_stride;
+            for (int q = 0; q < K; ++q) {
+                const uint64_t x = rec_key(R, P, q);
+                if (x >= lk[K - 1]) break;  // the record's keys ascend
+                lk_insert(lk, x);
             }
         }
-        const uint64_t ch = block_min_u64(m2, red);
-        if (ch == m2 && src >= 0 && ch != ~0ull) elite_src[e] = src;
-        if (tid == 0) elite[e] = ch;
-        if (ch == ~0ull && tid == 0) elite_src[e] = -1;
-        last = ch;
+        wave_topk(lk, K, wlist[wv]);
         __syncthreads();
+        if (wv == 0) {
+#pragma unroll
+            for (int i = 0; i < MAXK; ++i) lk[i] = (lane < MERGE_WAVES && i < K) ? wlist[lane][i] : KEY_NONE;
+            wave_topk(lk, K, elite);
+        }
+    }
+    __syncthreads();
+    // record slot of every elite key (needed when rows travel inside the records)
+    if (rows_in_rec) {
+        for (int t = tid; t < nrec * K; t += T) {
+            const int r = t / K, q = t % K;
+            const uint64_t x = rec_key(recs + (size_t)r * rec_stride, P, q);
+            for (int e = 0; e < K; ++e)
+                if (x == elite[e] && x != KEY_NONE) elite_src[e] = t;
+        }
+        __syncthreads();
+    }
+    MERGE_STAMP(3);
+
+    // ---- 5. elite rows -> LDS
+    int Kv = 0;
+    for (int e = 0; e < K; ++e) Kv += elite[e] != KEY_NONE;
+    for (int t = tid; t < K * P; t += T) {
+        const int e = t / P, jj = t % P;
+        float v = 0.0f;
+        if (elite[e] != KEY_NONE) {
+            if (rows_in_rec) {
+                const int st = elite_src[e];
+                v = recs[(size_t)(st / K) * rec_stride + REC_HDR + P + 2 * K + (size_t)(st % K) * P + jj];
+            } else {
+                v = noise[(size_t)jj * mc.ldn + ((int)(uint32_t)elite[e] - mc.row0)];
+            }
+        }
+        erow[t] = v;
     }
     __syncthreads();
 
-    auto elite_row = [&](int e, int j) -> float {
-        const uint64_t kk = elite[e];
-        if (kk == ~0ull) return 0.0f;
-        if (rows_in_rec) {
-            const int t = elite_src[e];
-            const int r = t / K, q = t % K;
-            return recs[(size_t)r * rec_stride + REC_HDR + P + 2 * K + (size_t)q * P + j];
-        }
-        const int local = (int)(uint32_t)kk - mc.row0;
-        return noise[(size_t)j * mc.ldn + local];
-    };
-
+    // ---- 6. outputs
     if (rank_out) {
-        for (int j = tid; j < P; j += T) rank_out[REC_HDR + j] = rs ? 0.0f : Vs[j];
+        for (int jj = tid; jj < P; jj += T) rank_out[REC_HDR + jj] = rs ? 0.0f : Vs[jj];
         for (int e = tid; e < K; e += T) {
             rank_out[REC_HDR + P + 2 * e] = u2f((uint32_t)elite[e]);
             rank_out[REC_HDR + P + 2 * e + 1] = u2f((uint32_t)(elite[e] >> 32));
         }
-        for (int t = tid; t < K * P; t += T) {
-            const int e = t / P, j = t % P;
-            rank_out[REC_HDR + P + 2 * K + t] = elite_row(e, j);
-        }
+        for (int t = tid; t < K * P; t += T) rank_out[REC_HDR + P + 2 * K + t] = erow[t];
         if (tid == 0) {
             rank_out[0] = beta;
             rank_out[1] = rs ? 1.0f : Vs[P];
@@ -363,43 +688,69 @@ __global__ void __launch_bounds__(1024) merge_kernel(const ModelConst mc, const 
             rank_out[3] = 0.0f;
         }
     }
-
     if (out) {
-        int Kv = 0;
-        for (int e = 0; e < K; ++e) Kv += elite[e] != ~0ull;
-        for (int j = tid; j < P; j += T) {
-            float v;
-            if (rs) v = in->best[j] + elite_row(0, j);
-            else v = in->best[j] + Vs[j] / Vs[P];
-            nb[j] = v;
-            out->best[j] = v;
-            if (mc.method == SRBD_CEM_MPPI) {
+        for (int jj = tid; jj < P; jj += T) {
+            const float b0 = in->best[jj];
+            const float v = rs ? b0 + erow[jj] : b0 + Vs[jj] / Vs[P];
+            nb[jj] = v;
+            out->best[jj] = v;
+            if (mc.method == SRBD_CEM_MPPI) {  // NMPC:1075-1081
                 float s = 0.0f;
-                for (int e = 0; e < Kv; ++e) s = s + elite_row(e, j);
+                for (int e = 0; e < Kv; ++e) s = s + erow[e * P + jj];
                 const float mean = s / (float)Kv;
                 float var = 0.0f;
                 for (int e = 0; e < Kv; ++e) {
-                    const float d = elite_row(e, j) - mean;
+                    const float d = erow[e * P + jj] - mean;
                     var = var + d * d;
                 }
                 var = var / (float)(Kv - 1);
                 float sg = sqrtf(var + 1e-8f);
                 sg = sg > 5.0f ? 5.0f : sg;
                 sg = sg < 0.2f ? 0.2f : sg;
-                out->sigma[j] = sg;
+                out->sigma[jj] = sg;
+                if (chain) in->sigma[jj] = sg;
             }
         }
         __syncthreads();
-        if (tid == 0) {
-            float grf[12], pred[24];
-            final_grf_pred(mc, *in, nb, grf, pred);
-            for (int i = 0; i < 12; ++i) out->grf[i] = grf[i];
-            for (int i = 0; i < 24; ++i) out->pred[i] = pred[i];
+        MERGE_STAMP(4);
+        if (tid < 4) {  // final GRFs, one thread per leg (NMPC:695-750)
+            const int leg = tid;
+            const float* pl = nb + leg * mc.PL;
+            auto acc = [pl](int jj) { return pl[jj]; };
+            float fx, fy, fz;
+            decode_leg(mc.kind, mc.H, mc.S, mc.fidx, mc.fq, mc.fomq, mc.fa, mc.fb, mc.fc, mc.fd, 0, acc, fx, fy,
+                       fz);
+            shape_leg(mc, in->fzref[0], in->contact[leg][0], fx, fy, fz);
+            grf_sh[3 * leg] = fx;
+            grf_sh[3 * leg + 1] = fy;
+            grf_sh[3 * leg + 2] = fz;
+        }
+        __syncthreads();
+        if (tid < 12) out->grf[tid] = grf_sh[tid];
+        if (tid == 0) {  // predicted state (NMPC:752-784)
+            const float c[4] = {in->contact[0][0], in->contact[1][0], in->contact[2][0], in->contact[3][0]};
+            float x[12], F[12];
+            for (int i = 0; i < 12; ++i) {
+                x[i] = in->state[i];
+                F[i] = grf_sh[i];
+            }
+            integrate(mc, x, in->state + 12, F, c, mc.dts[0]);
+            for (int i = 0; i < 12; ++i) out->pred[i] = x[i];
+            for (int i = 12; i < 24; ++i) out->pred[i] = in->state[i];
             out->best_cost = beta;
             out->best_index = (int32_t)(uint32_t)bkey;
             out->status = 0;
+            if (chain && ctr_inc) {
+                const uint64_t cc = (((uint64_t)in->ctr_hi << 32) | in->ctr_lo) + (uint64_t)ctr_inc;
+                in->ctr_lo = (uint32_t)cc;
+                in->ctr_hi = (uint32_t)(cc >> 32);
+            }
         }
+        if (chain)
+            for (int jj = tid; jj < P; jj += T) in->best[jj] = nb[jj];
     }
+    MERGE_STAMP(5);
+#undef MERGE_STAMP
 }
 
 __global__ void advance_kernel(const ModelConst mc, StepInput* __restrict__ in, const StepOutput* __restrict__ out) {
@@ -429,10 +780,18 @@ __global__ void div_selftest_kernel(const float* a, const float* b, int n, float
 // ------------------------------------------------------------------ launchers
 template <int KIND, int HT, int ST>
 static void launch_rollout_t(const ModelConst& mc, const StepInput* in, const float* noise, float* costs,
-                             float* recs, int rec_stride, int threads, hipStream_t s) {
-    const int blocks = (mc.n_local + threads - 1) / threads;
-    hipLaunchKernelGGL((rollout_kernel<KIND, HT, ST>), dim3(blocks), dim3(threads), 0, s, mc, in, noise, costs,
-                       recs, rec_stride);
+                             float* recs, int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next) {
+    const RngJob job = next ? *next : RngJob{nullptr, 0, 0, 0, 0};
+    const int extra = next ? (rng_grid(mc) < 1024 ? rng_grid(mc) : 1024) : 0;
+    if (mode == ROLLOUT_QUAD) {
+        const int blocks = (mc.n_local + 63) / 64;
+        hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST>), dim3(blocks + extra), dim3(256), 0, s, mc, in, noise,
+                           costs, recs, rec_stride, job, blocks);
+    } else {
+        const int blocks = (mc.n_local + threads - 1) / threads;
+        hipLaunchKernelGGL((rollout_kernel<KIND, HT, ST>), dim3(blocks + extra * (256 / threads)), dim3(threads), 0, s,
+                           mc, in, noise, costs, recs, rec_stride, job, blocks);
+    }
 }
 
 bool rollout_specialised(int kind, int H, int S) {
@@ -441,28 +800,38 @@ bool rollout_specialised(int kind, int H, int S) {
 }
 
 void launch_rollout(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
-                    int rec_stride, int threads, hipStream_t s) {
+                    int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next) {
     const int H = mc.H, S = mc.S;
+#define SRBD_LR(K, HH, SS) \
+    return launch_rollout_t<K, HH, SS>(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next)
     switch (mc.kind) {
         case SRBD_ZERO_ORDER:
-            if (H == 10) return launch_rollout_t<SRBD_ZERO_ORDER, 10, 0>(mc, in, noise, costs, recs, rec_stride, threads, s);
-            if (H == 12) return launch_rollout_t<SRBD_ZERO_ORDER, 12, 0>(mc, in, noise, costs, recs, rec_stride, threads, s);
-            if (H == 16) return launch_rollout_t<SRBD_ZERO_ORDER, 16, 0>(mc, in, noise, costs, recs, rec_stride, threads, s);
-            return launch_rollout_t<SRBD_ZERO_ORDER, 0, 0>(mc, in, noise, costs, recs, rec_stride, threads, s);
+            if (H == 10) SRBD_LR(SRBD_ZERO_ORDER, 10, 0);
+            if (H == 12) SRBD_LR(SRBD_ZERO_ORDER, 12, 0);
+            if (H == 16) SRBD_LR(SRBD_ZERO_ORDER, 16, 0);
+            SRBD_LR(SRBD_ZERO_ORDER, 0, 0);
         case SRBD_LINEAR_SPLINE:
-            if (S == 2 && H == 12) return launch_rollout_t<SRBD_LINEAR_SPLINE, 12, 2>(mc, in, noise, costs, recs, rec_stride, threads, s);
-            if (S == 2 && H == 16) return launch_rollout_t<SRBD_LINEAR_SPLINE, 16, 2>(mc, in, noise, costs, recs, rec_stride, threads, s);
-            return launch_rollout_t<SRBD_LINEAR_SPLINE, 0, 0>(mc, in, noise, costs, recs, rec_stride, threads, s);
+            if (S == 2 && H == 12) SRBD_LR(SRBD_LINEAR_SPLINE, 12, 2);
+            if (S == 2 && H == 16) SRBD_LR(SRBD_LINEAR_SPLINE, 16, 2);
+            SRBD_LR(SRBD_LINEAR_SPLINE, 0, 0);
         default:
-            if (S == 2 && H == 12) return launch_rollout_t<SRBD_CUBIC_SPLINE, 12, 2>(mc, in, noise, costs, recs, rec_stride, threads, s);
-            if (S == 2 && H == 16) return launch_rollout_t<SRBD_CUBIC_SPLINE, 16, 2>(mc, in, noise, costs, recs, rec_stride, threads, s);
-            return launch_rollout_t<SRBD_CUBIC_SPLINE, 0, 0>(mc, in, noise, costs, recs, rec_stride, threads, s);
+            if (S == 2 && H == 12) SRBD_LR(SRBD_CUBIC_SPLINE, 12, 2);
+            if (S == 2 && H == 16) SRBD_LR(SRBD_CUBIC_SPLINE, 16, 2);
+            SRBD_LR(SRBD_CUBIC_SPLINE, 0, 0);
     }
+#undef SRBD_LR
 }
 
-void launch_rng(const ModelConst& mc, const StepInput* in, float* noise, hipStream_t s) {
-    dim3 grid((mc.n_local + 255) / 256, (mc.P + 3) / 4);
-    hipLaunchKernelGGL(rng_kernel, grid, dim3(256), 0, s, mc, in, noise);
+int rng_grid(const ModelConst& mc) {
+    const long items = (long)mc.n_local * ((mc.P + 3) / 4);
+    const long blocks = (items + 255) / 256;
+    return (int)(blocks < 2048 ? blocks : 2048);
+}
+
+void launch_rng(const ModelConst& mc, const StepInput* in, uint64_t seed, uint64_t ctr, int dev_ctr, int ctr_offset,
+                float* noise, hipStream_t s) {
+    const RngJob job{noise, seed, ctr, dev_ctr, ctr_offset};
+    hipLaunchKernelGGL(rng_kernel, dim3(rng_grid(mc)), dim3(256), 0, s, mc, in, job);
 }
 
 void launch_transpose(const float* src, int n, int P, int ldn, float* dst, hipStream_t s) {
@@ -470,15 +839,36 @@ void launch_transpose(const float* src, int n, int P, int ldn, float* dst, hipSt
     hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, s, src, n, P, ldn, dst);
 }
 
-size_t merge_smem_bytes(int nrec, int P) {
+size_t merge_smem_bytes(int nrec, int P, int K) {
     const int nrec_pad = (nrec + 3) & ~3;
-    return sizeof(float) * ((size_t)nrec_pad + 1024 + (size_t)P + 1);
+    return sizeof(float) * ((size_t)nrec_pad + MERGE_THREADS + 4 + (size_t)K * P);
 }
 
-void launch_merge(const ModelConst& mc, const StepInput* in, const float* recs, int nrec, int rec_stride,
-                  int rows_in_rec, const float* noise, float* rank_out, StepOutput* out, hipStream_t s) {
-    hipLaunchKernelGGL(merge_kernel, dim3(1), dim3(1024), merge_smem_bytes(nrec, mc.P), s, mc, in, recs, nrec,
-                       rec_stride, rows_in_rec, noise, rank_out, out);
+void launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
+                  int rows_in_rec, const float* noise, float* rank_out, StepOutput* out, int chain, hipStream_t s,
+                  uint64_t* dbg, int ctr_inc) {
+    hipLaunchKernelGGL(merge_kernel, dim3(1), dim3(MERGE_THREADS), merge_smem_bytes(nrec, mc.P, mc.K), s, mc, in, recs,
+                       nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, chain ? ctr_inc : 0, dbg);
+}
+
+int merge_partials(int nrec) {
+    if (nrec <= MERGE_DIRECT_MAX) return 0;
+    int m = (nrec + MERGE_PER_BLOCK - 1) / MERGE_PER_BLOCK;
+    return m > MERGE_MAX_PARTIALS ? MERGE_MAX_PARTIALS : m;
+}
+
+void launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
+                       const float* noise, float* partials, float* rank_out, StepOutput* out, int chain,
+                       hipStream_t s, int ctr_inc) {
+    const int m = merge_partials(nrec);
+    if (m == 0) {
+        launch_merge(mc, in, recs, nrec, rec_stride, 0, noise, rank_out, out, chain, s, nullptr, ctr_inc);
+        return;
+    }
+    const int per = (nrec + m - 1) / m;
+    hipLaunchKernelGGL(merge_kernel, dim3(m), dim3(MERGE_THREADS), merge_smem_bytes(per, mc.P, mc.K), s, mc, in, recs,
+                       nrec, rec_stride, 0, noise, partials, (StepOutput*)nullptr, 0, 0, (uint64_t*)nullptr);
+    launch_merge(mc, in, partials, m, rec_floats_rank(mc.P, mc.K), 1, noise, rank_out, out, chain, s, nullptr, ctr_inc);
 }
 
 void launch_advance(const ModelConst& mc, StepInput* in, const StepOutput* out, hipStream_t s) {

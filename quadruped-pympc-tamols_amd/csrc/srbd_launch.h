@@ -5,14 +5,42 @@
 
 namespace srbd {
 
+// One batch of noise draws: into `noise` (SoA), keyed by (seed, ctr) or, when dev_ctr != 0, by the
+// device StepInput's seed and counter + ctr_offset (device-resident chains).
+struct RngJob {
+    float* noise;
+    uint64_t seed, ctr;
+    int dev_ctr, ctr_offset;
+};
+int rng_grid(const ModelConst& mc);
+
+// rollout variants: one thread per sample (block = `threads` samples) or four lanes per sample
+// (block = 256 threads = 64 samples)
+enum { ROLLOUT_THREAD = 0, ROLLOUT_QUAD = 1 };
 bool rollout_specialised(int kind, int H, int S);
+// next != NULL: extra blocks of the same launch generate the next step's draws (RngJob) beside the
+// rollout, on the CUs it leaves idle.
 void launch_rollout(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
-                    int rec_stride, int threads, hipStream_t s);
-void launch_rng(const ModelConst& mc, const StepInput* in, float* noise, hipStream_t s);
+                    int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next = nullptr);
+// Counter: `ctr` (host-known), or in->ctr + ctr_offset when dev_ctr != 0 (device-resident chain).
+void launch_rng(const ModelConst& mc, const StepInput* in, uint64_t seed, uint64_t ctr, int dev_ctr, int ctr_offset,
+                float* noise, hipStream_t s);
 void launch_transpose(const float* src, int n, int P, int ldn, float* dst, hipStream_t s);
-size_t merge_smem_bytes(int nrec, int P);
-void launch_merge(const ModelConst& mc, const StepInput* in, const float* recs, int nrec, int rec_stride,
-                  int rows_in_rec, const float* noise, float* rank_out, StepOutput* out, hipStream_t s);
+size_t merge_smem_bytes(int nrec, int P, int K);
+// chain != 0: also write the new parameters / sigma / RNG counter back into `in` (device warm start)
+void launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
+                  int rows_in_rec, const float* noise, float* rank_out, StepOutput* out, int chain, hipStream_t s,
+                  uint64_t* dbg = nullptr, int ctr_inc = 1);
+// Two-level merge when there are many block records: merge_partials(nrec) first-level blocks each
+// reduce a slice of the records (spreading the record reads over CUs) into rank-format partials,
+// then one block merges the partials.
+constexpr int MERGE_DIRECT_MAX = 1024;
+constexpr int MERGE_PER_BLOCK = 16;
+constexpr int MERGE_MAX_PARTIALS = 64;
+int merge_partials(int nrec);
+void launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
+                       const float* noise, float* partials, float* rank_out, StepOutput* out, int chain,
+                       hipStream_t s, int ctr_inc = 1);
 void launch_advance(const ModelConst& mc, StepInput* in, const StepOutput* out, hipStream_t s);
 void launch_div_selftest(const float* a, const float* b, int n, float* o, hipStream_t s);
 

@@ -83,6 +83,7 @@ SIGNATURES = {
     "srbd_sync_result": (_I, [_P, _FP, _FP, C.POINTER(SrbdResult)]),
     "srbd_copy_costs": (_I, [_P, _FP]),
     "srbd_selftest_div": (_I, [_FP, _FP, _I, _FP, _FP]),
+    "srbd_debug_merge_phases": (_I, [_P, _I, _FP]),
     "srbd_tamols_create": (_I, [_I, C.POINTER(_P)]),
     "srbd_tamols_destroy": (None, [_P]),
     "srbd_tamols_last_error": (C.c_char_p, [_P]),
@@ -269,6 +270,11 @@ class Context:
         r, g, m = _F(0), _F(0), _F(0)
         self.check(lib.srbd_time_kernels(self.h, int(iters), C.byref(r), C.byref(g), C.byref(m)), "srbd_time_kernels")
         return {"rollout_us": r.value, "rng_us": g.value, "merge_us": m.value}
+
+    def merge_phases(self, iters: int = 50):
+        out = np.zeros(5, np.float32)
+        self.check(lib.srbd_debug_merge_phases(self.h, int(iters), fptr(out)), "srbd_debug_merge_phases")
+        return dict(zip(("min_key", "weighted_sums", "elite", "outputs", "tail"), (round(float(x), 3) for x in out)))
 
     def set_stream(self, stream_handle: int | None):
         self.check(lib.srbd_set_stream(self.h, C.c_void_p(stream_handle) if stream_handle else None), "srbd_set_stream")

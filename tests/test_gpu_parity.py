@@ -264,3 +264,15 @@ def test_sharded_records_on_one_gpu(lib):
         np.testing.assert_allclose(grf, full["grf"], rtol=1e-5, atol=1e-4)
     for cx in ctxs:
         cx.close()
+
+
+@pytest.mark.parametrize("wkey,method,par,H", CASES[:8])
+def test_rollout_variants_bitwise_identical(lib, monkeypatch, wkey, method, par, H):
+    """The four-lanes-per-sample kernel performs the thread kernel's float ops in the same order."""
+    case = make_case(wkey, N=3000, method=method, par=par, H=H, seed=11)
+    out = {}
+    for mode in ("thread", "quad"):
+        monkeypatch.setenv("SRBD_ROLLOUT", mode)
+        out[mode] = run_gpu(lib, case, noise=False, seed=9, counter=4)
+    for k in ("costs", "best", "grf", "pred"):
+        np.testing.assert_array_equal(out["thread"][k], out["quad"][k])
