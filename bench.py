@@ -42,13 +42,21 @@ def make_cfg(w: Workload, n_total: int, rank: int, world: int, device: int):
                             rank=rank, world_size=world, use_graph=True, sigma_mppi=w.sigma)
 
 
-def roofline(w: Workload, n_local: int, rollout_us: float, traffic):
+def roofline(w: Workload, n_local: int, kern: dict, traffic):
+    """Dominant kernel = the rollout launch as the timed chain runs it.
+
+    Algorithmic bytes (SURVEY 8(d)): each noise row read once and one cost written, N*(4P+4);
+    when the launch also draws the next step's noise (fused), + N*4P written.
+    """
     P = w.num_params()
-    algo = n_local * (4 * P + 4)  # read each noise row once, write one cost
-    achieved = algo / (rollout_us * 1e-6) / 1e9
+    fused = "fused_rollout_us" in kern
+    us = kern["fused_rollout_us"] if fused else kern["rollout_us"]
+    algo = n_local * (4 * P + 4) + (n_local * 4 * P if fused else 0)
+    achieved = algo / (us * 1e-6) / 1e9
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "rollout_kernel",
-            "kernel_us": round(rollout_us, 3), "algorithmic_bytes_per_launch": algo}
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "kernel": "rollout_quad_kernel" + (" (+ next-step Philox blocks)" if fused else ""),
+            "kernel_us": round(us, 3), "algorithmic_bytes_per_launch": algo}
 
 
 def pmc_traffic(workload_name: str):
@@ -108,67 +116,43 @@ def bench_single(w, args):
 
 
 def bench_multi(w, args, rank, world, local_rank):
-    import ctypes as C
-
     import torch
     import torch.distributed as dist
 
+    from quadruped_pympc_amd.sharded import ShardedSamplingMPC
+
     torch.cuda.set_device(local_rank)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    n_total = w.num_samples * world
-    ctx = _lib.Context(make_cfg(w, n_total, rank, world, local_rank))
-    stream = torch.cuda.current_stream()
-    ctx.set_stream(stream.cuda_stream)
-    recf = ctx.record_floats()
-    rec = torch.zeros(recf, dtype=torch.float32, device="cuda")
-    gathered = torch.zeros(world * recf, dtype=torch.float32, device="cuda")
+    n_total = w.num_samples * world  # weak scaling: N rows per GPU of one MPC problem
+    mpc = ShardedSamplingMPC(make_cfg(w, n_total, rank, world, local_rank), rank, world, local_rank)
     s, r, c = inputs(w, 0)
-    f = lambda a: _lib.fptr(np.ascontiguousarray(a, np.float32))  # noqa: E731
-    state, ref, contact = (np.ascontiguousarray(a, np.float32) for a in (s, r, c))
-    best = np.zeros(ctx.P, np.float32)
-    res = _lib.SrbdResult()
-
-    def host_step(counter):
-        nonlocal best
-        rc = _lib.lib.srbd_step_local(ctx.h, f(state), f(ref), f(contact), contact.shape[1], f(best), None, None,
-                                      42, counter, C.c_void_p(rec.data_ptr()))
-        ctx.check(rc, "srbd_step_local")
-        dist.all_gather_into_tensor(gathered, rec)
-        rc = _lib.lib.srbd_step_finish(ctx.h, C.c_void_p(gathered.data_ptr()), world, _lib.fptr(best), None,
-                                       C.byref(res), None)
-        ctx.check(rc, "srbd_step_finish")
-
-    def device_step():
-        ctx.check(_lib.lib.srbd_device_step_local(ctx.h, C.c_void_p(rec.data_ptr())), "device_step_local")
-        dist.all_gather_into_tensor(gathered, rec)
-        ctx.check(_lib.lib.srbd_device_step_finish(ctx.h, C.c_void_p(gathered.data_ptr()), world),
-                  "device_step_finish")
-
+    best = np.zeros(mpc.P, np.float32)
     for k in range(max(1, args.warmup)):
-        host_step(k)
+        best, _, _ = mpc.step(s, r, c, best, seed=42, counter=k)
     lat = []
     for k in range(args.latency_steps):
         dist.barrier()
         t0 = time.perf_counter()
-        host_step(1000 + k)
+        best, _, _ = mpc.step(s, r, c, best, seed=42, counter=1000 + k)
         lat.append(time.perf_counter() - t0)
     for _ in range(max(1, args.warmup)):
-        device_step()
+        mpc.device_step()
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        device_step()
+        mpc.device_step()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     t = torch.tensor([wall], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall = float(t.item())
-    ctx.set_stream(None)
-    kern = ctx.time_kernels(20)
-    ctx.close()
+    n_local = mpc.ctx.n_local
+    mpc.ctx.set_stream(None)
+    kern = mpc.ctx.time_kernels(20)
+    mpc.close()
     dist.destroy_process_group()
-    return dict(n_total=n_total, n_local=ctx.n_local, wall=wall, ms_dev=None, lat=lat, kern=kern)
+    return dict(n_total=n_total, n_local=n_local, wall=wall, ms_dev=None, lat=lat, kern=kern)
 
 
 def main():
@@ -213,7 +197,7 @@ def main():
                    "parametrization": w.parametrization, "robot": w.robot, "gait": w.gait,
                    "parallelism": f"rows sharded over {world} GPU(s)" if world > 1 else "single GPU"},
         "kernels_us": {k: round(v, 3) for k, v in out["kern"].items()},
-        "roofline": roofline(w, out["n_local"], out["kern"]["rollout_us"], pmc_traffic(w.name)),
+        "roofline": roofline(w, out["n_local"], out["kern"], pmc_traffic(w.name)),
     }
     if out["ms_dev"] is not None:
         line["device_ms_per_step"] = round(out["ms_dev"] / args.steps, 5)

@@ -130,8 +130,11 @@ int srbd_make_record_host(const srbd_config* cfg, int32_t rank, int32_t world_si
 /* Measurement: replay `steps` device-resident steps (RNG -> rollout -> reduction -> warm start
  * written back on device) back to back; returns elapsed ms (hipEvents on the context stream). */
 int srbd_bench_device_steps(srbd_ctx* ctx, int32_t steps, float* elapsed_ms);
-/* Average per-launch duration (us) of each kernel of one step, hipEvents around every launch. */
-int srbd_time_kernels(srbd_ctx* ctx, int32_t iters, float* rollout_us, float* rng_us, float* reduce_us);
+/* Average per-launch duration (us) of each kernel of one step, hipEvents around every launch.
+ * fused_rollout_us: the rollout launch that also draws the next step's noise (the form the step
+ * chain runs when fusion applies; 0 otherwise).  Any out pointer may be NULL. */
+int srbd_time_kernels(srbd_ctx* ctx, int32_t iters, float* rollout_us, float* rng_us, float* reduce_us,
+                      float* fused_rollout_us);
 
 /* Device-resident sharded chain (benchmark / pipelined callers): reuses the inputs of the last
  * srbd_step_local on the device.  srbd_device_step_local: RNG -> rollout -> rank record into d_record;

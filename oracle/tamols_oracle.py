@@ -25,7 +25,8 @@ from scipy.spatial import cKDTree
 
 LEGS = ("FL", "FR", "RL", "RR")
 
-# config.py:209-243 (tamols_params) -- values used when a key is absent follow VFA's .get defaults
+# config.py:209-243 (tamols_params) values; the tests always pass this dict explicitly, so VFA's own
+# .get() fallbacks (VFA:298-305, used by the product's tamols_params_struct) never apply here
 DEFAULT_PARAMS = {
     "gradient_delta": 0.04,
     "weight_edge_avoidance": 10.0,

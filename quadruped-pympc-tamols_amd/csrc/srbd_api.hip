@@ -165,8 +165,8 @@ static int build_model(const srbd_config* cfg, ModelConst* mc, std::string* why)
     mc->method = cfg->method;
     const int ne = cfg->num_elite > 0 ? cfg->num_elite : 10;
     mc->K = num_elite(cfg->method, ne);
-    if (mc->K > MAXK) {
-        *why = "num_elite too large";
+    if (mc->K > MAXK || (cfg->method == SRBD_CEM_MPPI && mc->K < 2)) {
+        *why = "num_elite must be in [2, SRBD_MAX_ELITE] (sample variance over the elite set)";
         return SRBD_E_INVALID;
     }
     mc->N = cfg->num_samples;
@@ -711,7 +711,8 @@ extern "C" int srbd_bench_device_steps(srbd_ctx* c, int32_t steps, float* ms) {
     return SRBD_OK;
 }
 
-extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, float* rng_us, float* reduce_us) {
+extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, float* rng_us, float* reduce_us,
+                                 float* fused_us) {
     if (!c || iters < 1) return SRBD_E_INVALID;
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step once before timing");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
@@ -742,7 +743,25 @@ extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, 
         b += t1;
         d += t2;
     }
+    // The launch the timed chain actually runs when fusion applies: rollout + next-step draws.
+    double f = 0;
+    if (fusable(c)) {
+        const RngJob next{c->d_noise[1], 0, 0, 1, 1};
+        for (int i = 0; i < iters; ++i) {
+            HIP_TRY(c, hipEventRecord(ev[4 * i], c->stream));
+            launch_rollout(mc, c->d_in, c->d_noise[0], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
+                           c->stream, &next);
+            HIP_TRY(c, hipEventRecord(ev[4 * i + 1], c->stream));
+        }
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        for (int i = 0; i < iters; ++i) {
+            float t;
+            HIP_TRY(c, hipEventElapsedTime(&t, ev[4 * i], ev[4 * i + 1]));
+            f += t;
+        }
+    }
     for (auto& e : ev) (void)hipEventDestroy(e);
+    if (fused_us) *fused_us = (float)(f * 1000.0 / iters);
     if (rng_us) *rng_us = (float)(a * 1000.0 / iters);
     if (rollout_us) *rollout_us = (float)(b * 1000.0 / iters);
     if (reduce_us) *reduce_us = (float)(d * 1000.0 / iters);

@@ -77,7 +77,7 @@ SIGNATURES = {
     "srbd_finish_host": (_I, [C.POINTER(SrbdConfig), _FP, _I, _FP, _FP, _I, _FP, _FP, C.POINTER(SrbdResult)]),
     "srbd_make_record_host": (_I, [C.POINTER(SrbdConfig), _I, _I, _FP, _FP, _FP]),
     "srbd_bench_device_steps": (_I, [_P, _I, _FP]),
-    "srbd_time_kernels": (_I, [_P, _I, _FP, _FP, _FP]),
+    "srbd_time_kernels": (_I, [_P, _I, _FP, _FP, _FP, _FP]),
     "srbd_device_step_local": (_I, [_P, _P]),
     "srbd_device_step_finish": (_I, [_P, _P, _I]),
     "srbd_sync_result": (_I, [_P, _FP, _FP, C.POINTER(SrbdResult)]),
@@ -204,6 +204,41 @@ def num_params(cfg: SrbdConfig) -> int:
     return P
 
 
+REC_HDR = 4  # srbd_core.h: [m, s, best row bits, pad]
+
+
+def record_floats_host(cfg: SrbdConfig) -> int:
+    """Floats per rank record (== srbd_record_floats of a context of this configuration)."""
+    K = cfg.num_elite if cfg.method == CEM_MPPI else 1
+    P = num_params(cfg)
+    return REC_HDR + P + 2 * K + K * P
+
+
+def make_record_host(cfg: SrbdConfig, rank: int, world: int, costs: np.ndarray, noise_rows: np.ndarray) -> np.ndarray:
+    """srbd_make_record_host: one rank's partial record from its saturated costs and noise rows."""
+    rec = np.zeros(record_floats_host(cfg), np.float32)
+    costs = np.ascontiguousarray(costs, np.float32)
+    noise_rows = np.ascontiguousarray(noise_rows, np.float32)
+    check(lib.srbd_make_record_host(C.byref(cfg), int(rank), int(world), fptr(costs), fptr(noise_rows), fptr(rec)),
+          None, "srbd_make_record_host")
+    return rec
+
+
+def finish_host(cfg: SrbdConfig, records: np.ndarray, state, contact, best, sigma=None):
+    """srbd_finish_host: merge gathered rank records (rank order) on the host."""
+    records = np.ascontiguousarray(records, np.float32)
+    nrec = records.size // record_floats_host(cfg)
+    state = np.ascontiguousarray(state, np.float32).reshape(24)
+    contact = np.ascontiguousarray(contact, np.float32)
+    best = np.array(best, np.float32).reshape(-1).copy()
+    if sigma is not None:
+        sigma = np.array(np.broadcast_to(np.asarray(sigma, np.float32), best.shape), np.float32)
+    res = SrbdResult()
+    check(lib.srbd_finish_host(C.byref(cfg), fptr(records), nrec, fptr(state), fptr(contact), contact.shape[1],
+                               fptr(best), fptr(sigma), C.byref(res)), None, "srbd_finish_host")
+    return best, sigma, res
+
+
 class Context:
     """Owns one ``srbd_ctx`` (device buffers, stream, graphs) for one configuration."""
 
@@ -267,9 +302,13 @@ class Context:
         return float(ms.value)
 
     def time_kernels(self, iters: int):
-        r, g, m = _F(0), _F(0), _F(0)
-        self.check(lib.srbd_time_kernels(self.h, int(iters), C.byref(r), C.byref(g), C.byref(m)), "srbd_time_kernels")
-        return {"rollout_us": r.value, "rng_us": g.value, "merge_us": m.value}
+        r, g, m, f = _F(0), _F(0), _F(0), _F(0)
+        self.check(lib.srbd_time_kernels(self.h, int(iters), C.byref(r), C.byref(g), C.byref(m), C.byref(f)),
+                   "srbd_time_kernels")
+        out = {"rollout_us": r.value, "rng_us": g.value, "merge_us": m.value}
+        if f.value > 0:  # rollout launch carrying the next step's draws (what the step chain runs)
+            out["fused_rollout_us"] = f.value
+        return out
 
     def merge_phases(self, iters: int = 50):
         out = np.zeros(5, np.float32)

@@ -1,0 +1,73 @@
+"""GPU path vs the committed golden fixtures (no oracle at run time).
+
+Tolerances as tests/test_gpu_parity.py: costs rtol 2e-5 atol 1e-3; GRFs rtol 1e-4 atol 5e-3;
+parameters rtol 1e-4 atol 1e-3; predicted state rtol 1e-5 atol 1e-4; TAMOLS scores atol 1e-9,
+footholds atol 1e-12.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+SRBD = sorted(glob.glob(os.path.join(GOLDEN, "srbd_*.npz")))
+f32 = np.float32
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from quadruped_pympc_amd import _lib
+
+    if _lib.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X")
+    return _lib
+
+
+@pytest.mark.parametrize("graph", [True, False])
+@pytest.mark.parametrize("path", SRBD, ids=os.path.basename)
+def test_gpu_step_matches_fixture(lib, path, graph):
+    g = dict(np.load(path, allow_pickle=False))
+    cfg = lib.make_config(num_samples=int(g["num_samples"]), horizon=int(g["horizon"]), method=str(g["method"]),
+                          parametrization=str(g["parametrization"]), num_splines=int(g["num_splines"]),
+                          mass=float(g["mass"]), inertia=g["inertia"], dts=g["dts"], use_graph=graph)
+    ctx = lib.Context(cfg)
+    try:
+        sigma = g["sigma_in"] if g["sigma_in"].size else None
+        best, ns, res, costs = ctx.step(g["state"], g["ref"], g["contact"], g["best_in"], sigma=sigma,
+                                        noise=g["noise"], want_costs=True)
+    finally:
+        ctx.close()
+    np.testing.assert_allclose(costs, g["costs"], rtol=2e-5, atol=1e-3)
+    assert res.best_index == int(g["best_index"])
+    np.testing.assert_allclose(np.array(res.grf), g["grf"], rtol=1e-4, atol=5e-3)
+    np.testing.assert_allclose(best, g["best"], rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(np.array(res.predicted_state), g["pred"], rtol=1e-5, atol=1e-4)
+    if sigma is not None:
+        np.testing.assert_allclose(ns, g["sigma"], rtol=1e-4, atol=1e-5)
+
+
+def test_gpu_tamols_matches_fixture(lib):
+    from quadruped_pympc_amd.config import HIP_HEIGHTS, simulation_params
+    from quadruped_pympc_amd.helpers.visual_foothold_adaptation import TamolsSearch, tamols_params_struct
+
+    g = dict(np.load(os.path.join(GOLDEN, "tamols_go2.npz"), allow_pickle=False))
+    params = dict(simulation_params["tamols_params"])
+    params["h_des"] = HIP_HEIGHTS["go2"]
+    s = TamolsSearch(0)
+    try:
+        for name in ("flat", "stepping_stones_medium"):
+            out = s.run(g[f"{name}_heightmaps"], g[f"{name}_seeds"], g[f"{name}_hips"],
+                        tamols_params_struct(params, "go2"), forward_vel=g[f"{name}_vel"],
+                        base_position=g[f"{name}_base"], current_contact=g[f"{name}_contact"],
+                        current_feet_pos=g[f"{name}_feet"])
+            sc = g[f"{name}_scores"]
+            np.testing.assert_array_equal(np.isinf(out["scores"]), np.isinf(sc))
+            fin = np.isfinite(sc)
+            np.testing.assert_allclose(out["scores"][fin], sc[fin], rtol=0, atol=1e-9)
+            np.testing.assert_array_equal(out["valid"], g[f"{name}_valid"])
+            np.testing.assert_allclose(out["footholds"], g[f"{name}_footholds"], rtol=0, atol=1e-12)
+    finally:
+        s.close()

@@ -1,0 +1,58 @@
+"""The sharded driver (quadruped_pympc_amd.sharded) over a real RCCL group on one GPU.
+
+World size 1 (the box has one GPU; RCCL refuses two ranks on one device): the rank record
+goes through all_gather_into_tensor on torch's stream and srbd_step_finish merges it.  The
+result must match the unsharded srbd_step on the same noise to reduction-order tolerance, and
+the device-resident chain must run.  Multi-rank merging is covered on CPU with gloo
+(tests/test_distributed_gloo.py) and on this GPU with several contexts
+(test_gpu_parity.py::test_sharded_records_on_one_gpu).
+"""
+import socket
+
+import numpy as np
+import pytest
+
+from helpers import make_case, product_cfg
+
+pytestmark = pytest.mark.gpu
+
+
+def test_sharded_driver_world1_matches_step():
+    import torch
+    import torch.distributed as dist
+
+    from quadruped_pympc_amd import _lib
+    from quadruped_pympc_amd.sharded import ShardedSamplingMPC
+
+    if _lib.device_count() < 1:
+        pytest.fail("no HIP device visible")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        for method in ("mppi", "cem_mppi", "random_sampling"):
+            case = make_case("c2", N=3000, method=method, seed=17)
+            ref = _lib.Context(product_cfg(case))
+            b0, s0, r0, _ = ref.step(case["state"], case["ref"], case["contact"], case["best"], sigma=case["sigma"],
+                                     noise=case["noise"])
+            ref.close()
+            mpc = ShardedSamplingMPC(product_cfg(case), 0, 1, 0)
+            b1, s1, r1 = mpc.step(case["state"], case["ref"], case["contact"], case["best"], sigma=case["sigma"],
+                                  noise_local=case["noise"])
+            assert r1.best_index == r0.best_index
+            np.testing.assert_allclose(b1, b0, rtol=1e-5, atol=1e-5)
+            np.testing.assert_allclose(np.array(r1.grf), np.array(r0.grf), rtol=1e-5, atol=1e-3)
+            if method == "cem_mppi":
+                np.testing.assert_allclose(s1, s0, rtol=1e-5, atol=1e-6)
+            # device-resident chain on the torch stream
+            b2, _, _ = mpc.step(case["state"], case["ref"], case["contact"], b1, sigma=s1, seed=42, counter=5)
+            for _ in range(4):
+                mpc.device_step()
+            torch.cuda.synchronize()
+            assert np.all(np.isfinite(b2))
+            mpc.close()
+    finally:
+        dist.destroy_process_group()
