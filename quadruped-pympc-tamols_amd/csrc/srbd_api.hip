@@ -46,7 +46,15 @@ struct srbd_ctx {
     StepInput* d_in = nullptr;
     StepInput* h_in = nullptr;
     StepOutput* d_out = nullptr;
+    // Host-driven steps: the merge writes StepOutput straight into mapped pinned host memory (h_out,
+    // device alias d_out_host) and then publishes a sequence number in h_flag; the host spins on it.
+    // (Measured on MI355X: launch + spin on a mapped flag 5.8 us vs launch + hipStreamSynchronize 11.3;
+    // a 2-kernel graph + sync 19.4: hipGraphs cost more than they save at this size.)
     StepOutput* h_out = nullptr;
+    StepOutput* d_out_host = nullptr;
+    uint32_t* h_flag = nullptr;
+    uint32_t* d_flag = nullptr;
+    uint32_t seq = 0;
     // Noise matrices, double buffered: the rollout launch of a step reading d_noise[cur] also draws the
     // predicted next step's noise (counter + 1) into the other buffer (MPPI / random sampling; CEM's
     // draws depend on the sigma the step produces).
@@ -61,7 +69,7 @@ struct srbd_ctx {
     float* d_costs = nullptr;
     float* d_wrec = nullptr;
     float* d_part = nullptr;  // first-level merge partials (rank-record format)
-    hipGraphExec_t g_step[2] = {nullptr, nullptr}, g_dev2 = nullptr, g_dev1 = nullptr;
+    hipGraphExec_t g_dev2 = nullptr, g_dev1 = nullptr;
     bool input_ready = false;
     std::string err;
 };
@@ -175,6 +183,10 @@ static int build_model(const srbd_config* cfg, ModelConst* mc, std::string* why)
     mc->ldn = (mc->n_local + 255) / 256 * 256;
     mc->inv_m = 1.0f / cfg->mass;
     mc->mg = cfg->mg;
+    if (!(cfg->grf_min >= 0.0f && cfg->grf_max >= cfg->grf_min && cfg->mu >= 0.0f)) {
+        *why = "need 0 <= grf_min <= grf_max and mu >= 0";
+        return SRBD_E_INVALID;
+    }
     mc->grf_min = cfg->grf_min;
     mc->grf_max = cfg->grf_max;
     mc->mu = cfg->mu;
@@ -239,6 +251,8 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     c->cfg = *cfg;
     c->mc = mc;
     c->mode = rollout_mode(mc.kind, mc.n_local);
+    // the four-lane kernel addresses noise through a buffer descriptor (31-bit byte offsets)
+    if ((long long)mc.P * mc.ldn * 4 >= (1LL << 31)) c->mode = ROLLOUT_THREAD;
     c->threads = rollout_threads(mc.n_local);
     const int spb = c->mode == ROLLOUT_QUAD ? 64 : c->threads;  // samples per rollout block
     c->nblocks = (mc.n_local + spb - 1) / spb;
@@ -259,8 +273,16 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
         return cleanup_fail("hipStreamCreate", e);
     if ((e = hipHostMalloc((void**)&c->h_in, sizeof(StepInput), hipHostMallocDefault)) != hipSuccess)
         return cleanup_fail("hipHostMalloc", e);
-    if ((e = hipHostMalloc((void**)&c->h_out, sizeof(StepOutput), hipHostMallocDefault)) != hipSuccess)
+    if ((e = hipHostMalloc((void**)&c->h_out, sizeof(StepOutput), hipHostMallocMapped | hipHostMallocCoherent)) !=
+        hipSuccess)
         return cleanup_fail("hipHostMalloc", e);
+    if ((e = hipHostGetDevicePointer((void**)&c->d_out_host, c->h_out, 0)) != hipSuccess)
+        return cleanup_fail("hipHostGetDevicePointer", e);
+    if ((e = hipHostMalloc((void**)&c->h_flag, 64, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+        return cleanup_fail("hipHostMalloc", e);
+    if ((e = hipHostGetDevicePointer((void**)&c->d_flag, c->h_flag, 0)) != hipSuccess)
+        return cleanup_fail("hipHostGetDevicePointer", e);
+    __atomic_store_n(c->h_flag, 0u, __ATOMIC_RELEASE);
     memset(c->h_in, 0, sizeof(StepInput));
     memset(c->h_out, 0, sizeof(StepOutput));
     const size_t noise_bytes = sizeof(float) * (size_t)mc.P * mc.ldn;
@@ -291,8 +313,6 @@ extern "C" void srbd_destroy(srbd_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device_id);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (int b = 0; b < 2; ++b)
-        if (c->g_step[b]) (void)hipGraphExecDestroy(c->g_step[b]);
     if (c->g_dev2) (void)hipGraphExecDestroy(c->g_dev2);
     if (c->g_dev1) (void)hipGraphExecDestroy(c->g_dev1);
     for (int b = 0; b < 2; ++b) (void)hipFree(c->d_noise[b]);
@@ -304,6 +324,7 @@ extern "C" void srbd_destroy(srbd_ctx* c) {
     (void)hipFree(c->d_part);
     if (c->h_in) (void)hipHostFree(c->h_in);
     if (c->h_out) (void)hipHostFree(c->h_out);
+    if (c->h_flag) (void)hipHostFree(c->h_flag);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -315,10 +336,6 @@ extern "C" int srbd_set_stream(srbd_ctx* c, void* s) {
     (void)hipSetDevice(c->cfg.device_id);
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->own_stream) HIP_TRY(c, hipStreamDestroy(c->stream));
-    for (int b = 0; b < 2; ++b) {
-        if (c->g_step[b]) (void)hipGraphExecDestroy(c->g_step[b]);
-        c->g_step[b] = nullptr;
-    }
     if (c->g_dev2) (void)hipGraphExecDestroy(c->g_dev2);
     if (c->g_dev1) (void)hipGraphExecDestroy(c->g_dev1);
     c->g_dev2 = c->g_dev1 = nullptr;
@@ -373,19 +390,30 @@ static int acquire_noise(srbd_ctx* c, const float* noise, uint64_t seed, uint64_
 
 // rollout (+ next draws, counter + 1 from the device StepInput) -> merge on noise buffer `buf`
 static void enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput* out, int chain = 0,
-                                int ctr_inc = 1, bool fuse_next = false) {
+                                int ctr_inc = 1, bool fuse_next = false, Publish pub = {nullptr, 0}) {
     const ModelConst& mc = c->mc;
     const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1};
     launch_rollout(mc, c->d_in, c->d_noise[buf], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
                    c->stream, fuse_next ? &next : nullptr);
     launch_merge_tree(mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, c->d_noise[buf], c->d_part, rank_out, out,
-                      chain, c->stream, ctr_inc);
+                      chain, c->stream, ctr_inc, pub);
 }
 
-static int enqueue_full_step(srbd_ctx* c, int buf, bool fuse_next) {
-    enqueue_device_step(c, buf, nullptr, c->d_out, 0, 0, fuse_next);
-    HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(StepOutput), hipMemcpyDeviceToHost, c->stream));
-    return SRBD_OK;
+// Wait for the merge to publish `seq`.  Polls the stream now and then so a device fault or a launch
+// failure surfaces as an error instead of a hang.
+static int wait_published(srbd_ctx* c, uint32_t seq) {
+    for (uint64_t it = 1;; ++it) {
+        if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == seq) return SRBD_OK;
+        if ((it & 4095) == 0) {
+            const hipError_t e = hipStreamQuery(c->stream);
+            if (e == hipSuccess) {  // drained: the flag store has completed
+                if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == seq) return SRBD_OK;
+                return fail(c, SRBD_E_HIP, "step completed without publishing its outputs");
+            }
+            if (e != hipErrorNotReady) HIP_TRY(c, e);
+        }
+        __builtin_ia32_pause();
+    }
 }
 
 static int copy_out(srbd_ctx* c, float* best, float* sigma, srbd_result* out) {
@@ -415,33 +443,21 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
     int buf = 0;
     if ((rc = acquire_noise(c, noise, seed, counter, &buf))) return rc;
     const bool fuse = !noise && fusable(c);
-    if (fuse && c->cfg.use_graph && c->own_stream) {
-        if (!c->g_step[buf]) {
-            hipGraph_t g;
-            HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-            rc = enqueue_full_step(c, buf, true);
-            hipError_t e = hipStreamEndCapture(c->stream, &g);
-            if (rc) return rc;
-            HIP_TRY(c, e);
-            e = hipGraphInstantiate(&c->g_step[buf], g, nullptr, nullptr, 0);
-            (void)hipGraphDestroy(g);
-            HIP_TRY(c, e);
-        }
-        HIP_TRY(c, hipGraphLaunch(c->g_step[buf], c->stream));
-    } else {
-        if ((rc = enqueue_full_step(c, buf, fuse))) return rc;
-    }
+    const Publish pub{c->d_flag, ++c->seq};
+    enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fuse, pub);
+    HIP_TRY(c, hipGetLastError());
     if (fuse) {
         c->pref_valid = true;
         c->pref_buf = 1 - buf;
         c->pref_seed = seed;
         c->pref_ctr = counter + 1;
     }
-    if (out_costs)
+    if ((rc = wait_published(c, pub.seq))) return rc;
+    if (out_costs) {
         HIP_TRY(c, hipMemcpyAsync(out_costs, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,
                                   c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
     c->input_ready = true;
     return copy_out(c, best, sigma, out);
 }
@@ -481,14 +497,17 @@ extern "C" int srbd_step_finish(srbd_ctx* c, const void* d_records, int32_t nrec
     if (!c || !d_records || nrec < 1 || !best) return SRBD_E_INVALID;
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "srbd_step_finish before srbd_step_local");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
-    launch_merge(c->mc, c->d_in, (const float*)d_records, nrec, c->rrec_stride, 1, nullptr, nullptr, c->d_out, 0,
-                 c->stream);
-    HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(StepOutput), hipMemcpyDeviceToHost, c->stream));
-    if (out_costs_local)
+    const Publish pub{c->d_flag, ++c->seq};
+    launch_merge(c->mc, c->d_in, (const float*)d_records, nrec, c->rrec_stride, 1, nullptr, nullptr, c->d_out_host,
+                 0, c->stream, nullptr, 1, pub);
+    HIP_TRY(c, hipGetLastError());
+    int rc = wait_published(c, pub.seq);
+    if (rc) return rc;
+    if (out_costs_local) {
         HIP_TRY(c, hipMemcpyAsync(out_costs_local, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,
                                   c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    HIP_TRY(c, hipGetLastError());
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
     return copy_out(c, best, sigma, out);
 }
 

@@ -233,15 +233,25 @@ SRBD_HD void integrate(const ModelConst& mc, float x[12], const float feet[12], 
     for (int k = 0; k < 12; ++k) x[k] = x[k] + d[k] * dt;
 }
 
-// NMPC:270-314: compare-select form, so a NaN fz becomes fz_min and a NaN fx/fy the cone bound.
+// NMPC:270-314: where(x > lo, x, lo) then where(x < hi, x, hi), so a NaN becomes the lower bound.
+// On the device this is one v_med3_f32: with lo <= hi it is the clamp, and with a NaN operand
+// gfx9's med3 returns min3(x, lo, hi) = lo, the reference's result.  Only the sign of an exact
+// zero can differ from the two compare-selects (no cost or force value does).  lo <= hi holds
+// because build_model requires 0 <= grf_min <= grf_max and mu >= 0.
+SRBD_HD float clamp_cs(float x, float lo, float hi) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_fmed3f(x, lo, hi);
+#else
+    x = (x > lo) ? x : lo;
+    return (x < hi) ? x : hi;
+#endif
+}
+
 SRBD_HD void clip_leg(const ModelConst& mc, float& fx, float& fy, float& fz) {
-    fz = (fz > mc.grf_min) ? fz : mc.grf_min;
-    fz = (fz < mc.grf_max) ? fz : mc.grf_max;
+    fz = clamp_cs(fz, mc.grf_min, mc.grf_max);
     const float lo = mc.neg_mu * fz, hi = mc.mu * fz;
-    fx = (fx > lo) ? fx : lo;
-    fx = (fx < hi) ? fx : hi;
-    fy = (fy > lo) ? fy : lo;
-    fy = (fy < hi) ? fy : hi;
+    fx = clamp_cs(fx, lo, hi);
+    fy = clamp_cs(fy, lo, hi);
 }
 
 // Gravity compensation + contact mask (NMPC:377-402), then clip.

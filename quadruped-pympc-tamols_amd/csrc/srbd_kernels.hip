@@ -209,7 +209,7 @@ __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepI
             float a = 0.0f;
             if (j < P) {
                 const float4* row = reinterpret_cast<const float4*>(base + (size_t)j * ldn);
-#pragma unroll 4
+#pragma unroll 16
                 for (int i = 0; i < SPB / 4; ++i) {
                     const float4 v = row[i];
                     a = a + e_sh[4 * i] * v.x;
@@ -240,7 +240,7 @@ __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepI
 
 // One thread per sample.  Best throughput when samples fill the GPU (>= ~1 wave per SIMD).
 template <int KIND, int HT, int ST>
-__global__ void __launch_bounds__(256) rollout_kernel(const ModelConst mc, const StepInput* __restrict__ in,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == SRBD_ZERO_ORDER ? 2 : 1))) rollout_kernel(const ModelConst mc, const StepInput* __restrict__ in,
                                                       const float* __restrict__ noise, float* __restrict__ costs,
                                                       float* __restrict__ recs, int rec_stride,
     const RngJob next_rng, int nroll) {
@@ -272,7 +272,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(const ModelConst mc, const
         x[i] = in->state[i];
         feet[i] = in->state[12 + i];
     }
-    float cost = 0.0f;
+    float cost3[3] = {0.0f, 0.0f, 0.0f};
 
     auto step = [&](const int n) __attribute__((always_inline)) {
         const float c[4] = {in->contact[0][n], in->contact[1][n], in->contact[2][n], in->contact[3][n]};
@@ -292,21 +292,23 @@ __global__ void __launch_bounds__(256) rollout_kernel(const ModelConst mc, const
             F[3 * leg + 2] = fz;
         }
         integrate(mc, x, feet, F, c, mc.dts[n]);
-        float a = 0.0f;
+        // tracking cost (NMPC:451) per component: cost_c += ((t_p + t_v) + t_rpy) + t_omega
+        float t[12];
 #pragma unroll
         for (int i = 0; i < 12; ++i) {
             const float e = x[i] - in->ref[i];
-            const float t = (e * mc.Q[i]) * e;
-            a = (i == 0) ? t : a + t;
+            t[i] = (e * mc.Q[i]) * e;
         }
-        a = a + in->cost_feet;
-        cost = cost + a;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) cost3[q] = cost3[q] + (((t[q] + t[3 + q]) + t[6 + q]) + t[9 + q]);
     };
     if constexpr (CT) {
         unroll_seq([&](auto nc) { step(decltype(nc)::value); }, std::make_integer_sequence<int, (CT ? HT : 1)>{});
     } else {
         for (int n = 0; n < H; ++n) step(n);
     }
+    float cost = (cost3[0] + cost3[1]) + cost3[2];
+    cost = cost + in->cost_feet;  // 0, or NaN when a foot term is non-finite (Q_feet = 0)
     // NMPC:686-687
     if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
     if (valid && costs) costs[k] = cost;
@@ -325,12 +327,12 @@ constexpr int QP_NEXT2 = 0x52;  // lanes (0,1,2,3) <- (2,0,1,1): component c+2 (
 
 template <int CTRL>
 __device__ __forceinline__ float qp(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 __device__ __forceinline__ float sel3(int c, float a0, float a1, float a2) { return c == 0 ? a0 : (c == 1 ? a1 : a2); }
 
 template <int KIND, int HT, int ST>
-__global__ void __launch_bounds__(256) rollout_quad_kernel(const ModelConst mc, const StepInput* __restrict__ in,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) rollout_quad_kernel(const ModelConst mc, const StepInput* __restrict__ in,
                                                            const float* __restrict__ noise, float* __restrict__ costs,
                                                            float* __restrict__ recs, int rec_stride,
     const RngJob next_rng, int nroll) {
@@ -380,6 +382,29 @@ __global__ void __launch_bounds__(256) rollout_quad_kernel(const ModelConst mc, 
     float r = sel3(c, st[6], st[7], st[8]), w = sel3(c, st[9], st[10], st[11]);
     float cost = 0.0f;
 
+    // Specialised shapes: every parameter this lane reads over the horizon (its component's block
+    // of each leg) is loaded before the first step, so the horizon chain pays one memory round trip
+    // instead of one per step (at N = 10 000 there is < 1 wave per SIMD to hide the latency).
+    // ZO: H values per leg; linear: S + 1; cubic: 4 per chunk (start 10 * chunk, NMPC:225).
+    constexpr int NPRE = !CT ? 1 : (KIND == SRBD_ZERO_ORDER ? HT : (KIND == SRBD_LINEAR_SPLINE ? ST + 1 : 4 * ST));
+    float pre[4][NPRE];
+    if constexpr (CT) {
+        // noise through a buffer descriptor: per-lane part (component block + sample) in voffset, the
+        // uniform row in soffset -> no per-load address arithmetic (launch_rollout checks P*ldn*4 < 2^31)
+        const int cblk = KIND == SRBD_ZERO_ORDER ? c * HT : (KIND == SRBD_LINEAR_SPLINE ? c * (ST + 1) : 4 * c);
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)noise, (short)0, mc.P * mc.ldn * 4, 0x00020000);
+        const int voff = (cblk * mc.ldn + k) * 4;
+        const float* __restrict__ bl = best + cblk;
+#pragma unroll
+        for (int l = 0; l < 4; ++l)
+#pragma unroll
+            for (int i = 0; i < NPRE; ++i) {
+                const int jr = l * PL + (KIND == SRBD_CUBIC_SPLINE ? 10 * (i >> 2) + (i & 3) : i);  // row - cblk
+                const float nzv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, jr * mc.ldn * 4, 0));
+                pre[l][i] = bl[jr] + nzv;
+            }
+    }
+
     auto step = [&](const int n) __attribute__((always_inline)) {
         const float cl[4] = {in->contact[0][n], in->contact[1][n], in->contact[2][n], in->contact[3][n]};
         const float fref = in->fzref[n];
@@ -388,30 +413,34 @@ __global__ void __launch_bounds__(256) rollout_quad_kernel(const ModelConst mc, 
 #pragma unroll
         for (int l = 0; l < 4; ++l) {
             const int base = l * PL;
-            auto P = [&](int j) { return best[base + j] + nz[(size_t)(base + j) * ldn]; };
+            // parameter j of this leg (i: its slot in the prefetched block when the shape is specialised;
+            // i is a compile-time constant there, so `pre` stays in registers)
+            auto P = [&](int i, int j) {
+                if constexpr (CT) {
+                    return pre[l][i];
+                } else {
+                    return best[base + j] + nz[(size_t)(base + j) * ldn];
+                }
+            };
             float raw;
             if (KIND == SRBD_ZERO_ORDER) {
-                raw = P(n + c * H);
+                raw = P(n, n + c * H);
             } else if (KIND == SRBD_LINEAR_SPLINE) {
                 const int o = idx + c * (S + 1);
-                raw = mc.somq[n] * P(o) + mc.sq[n] * P(o + 1);
+                raw = mc.somq[n] * P(idx, o) + mc.sq[n] * P(idx + 1, o + 1);
             } else {
                 const int o = 10 * idx + 4 * c;
-                const float p0 = P(o), p1 = P(o + 1), p2 = P(o + 2), p3 = P(o + 3);
+                const float p0 = P(4 * idx, o), p1 = P(4 * idx + 1, o + 1), p2 = P(4 * idx + 2, o + 2),
+                            p3 = P(4 * idx + 3, o + 3);
                 const float phi = 0.5f * ((p2 - p1) + (p1 - p0));
                 const float phin = 0.5f * ((p3 - p2) + (p2 - p1));
                 raw = mc.sa[n] * p1 + mc.sb[n] * phi + mc.sc[n] * p2 + mc.sd[n] * phin;
             }
             // shape_leg / clip_leg, component-wise
-            float zp = (fref + raw) * cl[l];
-            zp = (zp > mc.grf_min) ? zp : mc.grf_min;
-            zp = (zp < mc.grf_max) ? zp : mc.grf_max;
-            float xy = div3(raw * cl[l]);
+            float zp = clamp_cs((fref + raw) * cl[l], mc.grf_min, mc.grf_max);
+            const float xy = div3(raw * cl[l]);
             const float fz = qp<QP_B2>(c == 2 ? zp : xy);
-            const float lo = mc.neg_mu * fz, hi = mc.mu * fz;
-            xy = (xy > lo) ? xy : lo;
-            xy = (xy < hi) ? xy : hi;
-            f[l] = c == 2 ? fz : xy;
+            f[l] = c == 2 ? fz : clamp_cs(xy, mc.neg_mu * fz, mc.mu * fz);
         }
         const float temp = f[0] * cl[0] + f[1] * cl[1] + f[2] * cl[2] + f[3] * cl[3];
         const float lin = mc.inv_m * temp + g;
@@ -432,12 +461,21 @@ __global__ void __launch_bounds__(256) rollout_quad_kernel(const ModelConst mc, 
         const float w0 = qp<QP_B0>(w), w1 = qp<QP_B1>(w), w2 = qp<QP_B2>(w);
         float k1, k2;
         euler_rate_coefs(c, sr, cr, sp, cp, k1, k2);
-        const float er = euler_rate_row(c, k1, k2, w0, w1, w2);
+        // euler_rate_row, with both operands of every lane select computed first (straight-line code:
+        // selects, not divergent branches)
+        const float kw1 = k1 * w1;
+        const float er0 = w0 + kw1;
+        const float er = (c == 0 ? er0 : kw1) + k2 * w2;
         // row c of b_R_w (CMJ:136-150)
         const float A = c == 1 ? sr : cr;
-        const float R0 = c == 0 ? cp * cy : (A * sp) * cy + (c == 1 ? -cr : sr) * sy;
-        const float R1 = c == 0 ? cp * sy : (A * sp) * sy + (c == 1 ? cr : -sr) * cy;
-        const float R2 = c == 0 ? -sp : A * cp;
+        const float B0 = c == 1 ? -cr : sr, B1 = c == 1 ? cr : -sr;
+        const float Asp = A * sp;
+        const float r0a = cp * cy, r0b = Asp * cy + B0 * sy;
+        const float r1a = cp * sy, r1b = Asp * sy + B1 * cy;
+        const float r2b = A * cp;
+        const float R0 = c == 0 ? r0a : r0b;
+        const float R1 = c == 0 ? r1a : r1b;
+        const float R2 = c == 0 ? -sp : r2b;
         const float Rt = R0 * qp<QP_B0>(temp2) + R1 * qp<QP_B1>(temp2) + R2 * qp<QP_B2>(temp2);
         const float Iw = Ir0 * w0 + Ir1 * w1 + Ir2 * w2;
         const float wx = (-qp<QP_NEXT2>(w)) * qp<QP_NEXT>(Iw) + qp<QP_NEXT>(w) * qp<QP_NEXT2>(Iw);
@@ -450,34 +488,19 @@ __global__ void __launch_bounds__(256) rollout_quad_kernel(const ModelConst mc, 
         v = vn;
         r = rn;
         w = wn;
-        float e;
-        e = p - rp;
-        const float tp = (e * Qp) * e;
-        e = v - rv;
-        const float tv = (e * Qv) * e;
-        e = r - rr;
-        const float tr = (e * Qr) * e;
-        e = w - rw;
-        const float tw = (e * Qw) * e;
-        float a = qp<QP_B0>(tp) + qp<QP_B1>(tp);
-        a = a + qp<QP_B2>(tp);
-        a = a + qp<QP_B0>(tv);
-        a = a + qp<QP_B1>(tv);
-        a = a + qp<QP_B2>(tv);
-        a = a + qp<QP_B0>(tr);
-        a = a + qp<QP_B1>(tr);
-        a = a + qp<QP_B2>(tr);
-        a = a + qp<QP_B0>(tw);
-        a = a + qp<QP_B1>(tw);
-        a = a + qp<QP_B2>(tw);
-        a = a + in->cost_feet;
-        cost = cost + a;
+        // tracking cost (NMPC:451), accumulated per component lane: cost_c += ((tp + tv) + tr) + tw,
+        // the three lanes summed once after the horizon (see rollout_kernel for the same order)
+        const float ep = p - rp, ev = v - rv, er_ = r - rr, ew = w - rw;
+        const float tp = (ep * Qp) * ep, tv = (ev * Qv) * ev, tr = (er_ * Qr) * er_, tw = (ew * Qw) * ew;
+        cost = cost + (((tp + tv) + tr) + tw);
     };
     if constexpr (CT) {
         unroll_seq([&](auto nc) { step(decltype(nc)::value); }, std::make_integer_sequence<int, (CT ? HT : 1)>{});
     } else {
         for (int n = 0; n < H; ++n) step(n);
     }
+    cost = (qp<QP_B0>(cost) + qp<QP_B1>(cost)) + qp<QP_B2>(cost);
+    cost = cost + in->cost_feet;  // 0, or NaN when a foot term is non-finite (Q_feet = 0)
     if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
     if (valid && q4 == 0 && costs) costs[k] = cost;
     block_epilogue(mc, in, 64, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh);
@@ -526,7 +549,8 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst m
                                                               const float* __restrict__ noise,
                                                               float* __restrict__ rank_out,
                                                               StepOutput* __restrict__ out, int chain,
-                                                              int ctr_inc, uint64_t* __restrict__ dbg) {
+                                                              int ctr_inc, uint64_t* __restrict__ dbg,
+                                                              uint32_t* __restrict__ flag, uint32_t seq) {
     extern __shared__ float smem[];  // scale[nrec_pad] | part[G*(P+1)] | erow[K*P]
     __shared__ uint64_t red[MERGE_WAVES];
     __shared__ uint64_t wlist[MERGE_WAVES][MAXK];
@@ -751,6 +775,11 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst m
     }
     MERGE_STAMP(5);
 #undef MERGE_STAMP
+    if (flag) {  // every thread's output writes reach the system before thread 0 publishes `seq`
+        __threadfence_system();
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 __global__ void advance_kernel(const ModelConst mc, StepInput* __restrict__ in, const StepOutput* __restrict__ out) {
@@ -846,9 +875,10 @@ size_t merge_smem_bytes(int nrec, int P, int K) {
 
 void launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                   int rows_in_rec, const float* noise, float* rank_out, StepOutput* out, int chain, hipStream_t s,
-                  uint64_t* dbg, int ctr_inc) {
+                  uint64_t* dbg, int ctr_inc, Publish pub) {
     hipLaunchKernelGGL(merge_kernel, dim3(1), dim3(MERGE_THREADS), merge_smem_bytes(nrec, mc.P, mc.K), s, mc, in, recs,
-                       nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, chain ? ctr_inc : 0, dbg);
+                       nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, chain ? ctr_inc : 0, dbg, pub.flag,
+                       pub.seq);
 }
 
 int merge_partials(int nrec) {
@@ -859,16 +889,18 @@ int merge_partials(int nrec) {
 
 void launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                        const float* noise, float* partials, float* rank_out, StepOutput* out, int chain,
-                       hipStream_t s, int ctr_inc) {
+                       hipStream_t s, int ctr_inc, Publish pub) {
     const int m = merge_partials(nrec);
     if (m == 0) {
-        launch_merge(mc, in, recs, nrec, rec_stride, 0, noise, rank_out, out, chain, s, nullptr, ctr_inc);
+        launch_merge(mc, in, recs, nrec, rec_stride, 0, noise, rank_out, out, chain, s, nullptr, ctr_inc, pub);
         return;
     }
     const int per = (nrec + m - 1) / m;
     hipLaunchKernelGGL(merge_kernel, dim3(m), dim3(MERGE_THREADS), merge_smem_bytes(per, mc.P, mc.K), s, mc, in, recs,
-                       nrec, rec_stride, 0, noise, partials, (StepOutput*)nullptr, 0, 0, (uint64_t*)nullptr);
-    launch_merge(mc, in, partials, m, rec_floats_rank(mc.P, mc.K), 1, noise, rank_out, out, chain, s, nullptr, ctr_inc);
+                       nrec, rec_stride, 0, noise, partials, (StepOutput*)nullptr, 0, 0, (uint64_t*)nullptr,
+                       (uint32_t*)nullptr, 0u);
+    launch_merge(mc, in, partials, m, rec_floats_rank(mc.P, mc.K), 1, noise, rank_out, out, chain, s, nullptr, ctr_inc,
+                 pub);
 }
 
 void launch_advance(const ModelConst& mc, StepInput* in, const StepOutput* out, hipStream_t s) {

@@ -27,10 +27,16 @@ void launch_rng(const ModelConst& mc, const StepInput* in, uint64_t seed, uint64
                 float* noise, hipStream_t s);
 void launch_transpose(const float* src, int n, int P, int ldn, float* dst, hipStream_t s);
 size_t merge_smem_bytes(int nrec, int P, int K);
+// Completion published to the host: after every output write is visible system-wide, the merge
+// stores `seq` into `flag` (host-mapped pinned memory); the host spins on it instead of a stream sync.
+struct Publish {
+    uint32_t* flag;
+    uint32_t seq;
+};
 // chain != 0: also write the new parameters / sigma / RNG counter back into `in` (device warm start)
 void launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                   int rows_in_rec, const float* noise, float* rank_out, StepOutput* out, int chain, hipStream_t s,
-                  uint64_t* dbg = nullptr, int ctr_inc = 1);
+                  uint64_t* dbg = nullptr, int ctr_inc = 1, Publish pub = {nullptr, 0});
 // Two-level merge when there are many block records: merge_partials(nrec) first-level blocks each
 // reduce a slice of the records (spreading the record reads over CUs) into rank-format partials,
 // then one block merges the partials.
@@ -40,7 +46,7 @@ constexpr int MERGE_MAX_PARTIALS = 64;
 int merge_partials(int nrec);
 void launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                        const float* noise, float* partials, float* rank_out, StepOutput* out, int chain,
-                       hipStream_t s, int ctr_inc = 1);
+                       hipStream_t s, int ctr_inc = 1, Publish pub = {nullptr, 0});
 void launch_advance(const ModelConst& mc, StepInput* in, const StepOutput* out, hipStream_t s);
 void launch_div_selftest(const float* a, const float* b, int n, float* o, hipStream_t s);
 

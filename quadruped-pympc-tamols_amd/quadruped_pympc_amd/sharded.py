@@ -24,12 +24,13 @@ from . import _lib
 class RecordExchange:
     """The path's one collective: all-gather of equal-size float32 records in rank order."""
 
-    def __init__(self, record_floats: int, world: int, device, group=None):
+    def __init__(self, record_floats: int, world: int, device, group=None, stream=None):
         import torch
 
         self.torch = torch
         self.world = world
         self.group = group
+        self.stream = stream  # the stream the record producer and the merge run on (CUDA only)
         self.local = torch.zeros(record_floats, dtype=torch.float32, device=device)
         self.gathered = torch.zeros(world * record_floats, dtype=torch.float32, device=device)
         self._parts = list(self.gathered.view(world, record_floats).unbind(0))
@@ -38,7 +39,8 @@ class RecordExchange:
         import torch.distributed as dist
 
         if self.local.is_cuda:
-            dist.all_gather_into_tensor(self.gathered, self.local, group=self.group)
+            with self.torch.cuda.stream(self.stream):
+                dist.all_gather_into_tensor(self.gathered, self.local, group=self.group)
         else:  # gloo: list form, written straight into the views of `gathered`
             dist.all_gather(self._parts, self.local, group=self.group)
         return self.gathered
@@ -54,8 +56,9 @@ class ShardedSamplingMPC:
     """One rank of a row-sharded MPC problem on the current process's GPU.
 
     cfg: an _lib.SrbdConfig with the GLOBAL num_samples; rank / world_size / device_id are set here.
-    Launches on torch's current stream of `device`, so the RCCL gather is ordered after the
-    rollout and before the merge without host synchronisation.
+    The library and the RCCL gather share one dedicated (non-default) torch stream, so the gather
+    is ordered after the rollout and before the merge without host synchronisation.  (The legacy
+    null stream cannot be handed to srbd_set_stream: a NULL handle selects the context's own stream.)
     """
 
     def __init__(self, cfg: _lib.SrbdConfig, rank: int, world: int, device_index: int, group=None):
@@ -66,9 +69,10 @@ class ShardedSamplingMPC:
         self.ctx = _lib.Context(cfg)
         self.rank, self.world = rank, world
         self.device = torch.device("cuda", device_index)
-        self.stream = torch.cuda.current_stream(self.device)
+        self.stream = torch.cuda.Stream(self.device)
         self.ctx.set_stream(self.stream.cuda_stream)
-        self.exchange = RecordExchange(self.ctx.record_floats(), world, self.device, group)
+        with torch.cuda.stream(self.stream):
+            self.exchange = RecordExchange(self.ctx.record_floats(), world, self.device, group, self.stream)
         self.P = self.ctx.P
         self.result = _lib.SrbdResult()
 

@@ -1,0 +1,108 @@
+// Host-to-host latency floors of the HIP runtime on this box (measurement tool, not product code).
+// Build on the GPU box: hipcc --offload-arch=gfx950 -O2 -o /tmp/latency_probe scripts/latency_probe.hip
+// Prints p50 microseconds of:
+//   launch_sync        empty kernel + hipStreamSynchronize
+//   launch_flag        kernel writes a sequence number to host-mapped memory; host spins on it
+//   args3k_flag        same, with a 3 KB by-value kernel argument
+//   two_launch_flag    two dependent kernels, the second writes the flag
+//   h2d_launch_sync    4 KB pinned H2D + kernel + sync
+//   graph2_sync        graph of two kernels + sync
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <vector>
+
+struct Big {
+    float v[768];
+};
+
+__global__ void k_empty(int* d) {
+    if (threadIdx.x == 0 && d) d[0] += 1;
+}
+__global__ void k_flag(volatile unsigned* host_flag, unsigned seq) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        __threadfence_system();
+        *host_flag = seq;
+    }
+}
+__global__ void k_flag_args(volatile unsigned* host_flag, unsigned seq, Big b, float* sink) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        sink[0] = b.v[seq % 768];
+        __threadfence_system();
+        *host_flag = seq;
+    }
+}
+
+template <class F>
+static double p50(F f, int n = 3000) {
+    for (int i = 0; i < 100; ++i) f(i);
+    std::vector<double> t(n);
+    for (int i = 0; i < n; ++i) {
+        auto t0 = std::chrono::steady_clock::now();
+        f(i + 100);
+        t[i] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    }
+    std::nth_element(t.begin(), t.begin() + n / 2, t.end());
+    return t[n / 2];
+}
+
+int main() {
+    hipStream_t s;
+    hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    int* d;
+    hipMalloc(&d, 4096);
+    float* sink;
+    hipMalloc(&sink, 64);
+    unsigned* hflag;
+    hipHostMalloc((void**)&hflag, 64, hipHostMallocMapped | hipHostMallocCoherent);
+    unsigned* dflag;
+    hipHostGetDevicePointer((void**)&dflag, hflag, 0);
+    *hflag = 0;
+    float* hin;
+    hipHostMalloc((void**)&hin, 4096, hipHostMallocDefault);
+    Big b{};
+    auto spin = [&](unsigned seq) {
+        while (__atomic_load_n(hflag, __ATOMIC_ACQUIRE) != seq) {
+        }
+    };
+    double a = p50([&](int) {
+        k_empty<<<1, 64, 0, s>>>(d);
+        hipStreamSynchronize(s);
+    });
+    double bflag = p50([&](int i) {
+        k_flag<<<1, 64, 0, s>>>(dflag, (unsigned)i + 1);
+        spin((unsigned)i + 1);
+    });
+    double cargs = p50([&](int i) {
+        k_flag_args<<<1, 64, 0, s>>>(dflag, (unsigned)i + 1, b, sink);
+        spin((unsigned)i + 1);
+    });
+    double two = p50([&](int i) {
+        k_empty<<<1, 64, 0, s>>>(d);
+        k_flag<<<1, 64, 0, s>>>(dflag, (unsigned)i + 1);
+        spin((unsigned)i + 1);
+    });
+    double h2d = p50([&](int) {
+        hipMemcpyAsync(d, hin, 4096, hipMemcpyHostToDevice, s);
+        k_empty<<<1, 64, 0, s>>>(d);
+        hipStreamSynchronize(s);
+    });
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+    k_empty<<<1, 64, 0, s>>>(d);
+    k_empty<<<1, 64, 0, s>>>(d);
+    hipStreamEndCapture(s, &g);
+    hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    double gr = p50([&](int) {
+        hipGraphLaunch(ge, s);
+        hipStreamSynchronize(s);
+    });
+    hipStreamSynchronize(s);
+    printf("{\"launch_sync\": %.2f, \"launch_flag\": %.2f, \"args3k_flag\": %.2f, \"two_launch_flag\": %.2f, "
+           "\"h2d_launch_sync\": %.2f, \"graph2_sync\": %.2f}\n",
+           a, bflag, cargs, two, h2d, gr);
+    return 0;
+}
