@@ -149,15 +149,9 @@ SRBD_HD void euler_rate_coefs(int c, float sr, float cr, float sp, float cp, flo
     const float DET = a33 * a22 - a32 * a23;
     const float n1 = c == 0 ? a32 * a13 : (c == 1 ? a33 : -a32);
     const float n2 = c == 0 ? -(a22 * a13) : (c == 1 ? -a23 : a22);
-    const float ad = fabsf(DET);
-    if (ad > 1e-30f && ad < 1e30f) {
-        const float r = 1.0f / DET;
-        k1 = div_by(n1, DET, r);
-        k2 = div_by(n2, DET, r);
-    } else {
-        k1 = n1 / DET;
-        k2 = n2 / DET;
-    }
+    const float r = 1.0f / DET;  // |DET| >= |cos(pitch)| / 2 >= 8e-10: see euler_rates
+    k1 = div_by(n1, DET, r);
+    k2 = div_by(n2, DET, r);
 }
 
 SRBD_HD float euler_rate_row(int c, float k1, float k2, float w0, float w1, float w2) {
@@ -168,16 +162,14 @@ SRBD_HD void euler_rates(float sr, float cr, float sp, float cp, float w0, float
     const float a13 = -sp, a22 = cr, a23 = cp * sr, a32 = -sr, a33 = cp * cr;
     const float DET = a33 * a22 - a32 * a23;
     const float n[6] = {a32 * a13, -(a22 * a13), a33, -a23, -a32, a22};
+    // Correctly rounded n / DET via the IEEE reciprocal and one Markstein step.  That needs 1/DET and
+    // the quotients to stay normal: DET = cp (cr^2 + sr^2), so |DET| >= |cos(pitch)| / 2, and over
+    // every finite float32 pitch |cos| >= 1.6e-9 (exhaustive search, attained at 7.73e28); a
+    // non-finite angle makes DET NaN, and NaN propagates to the cost either way.
     float k[6];
-    const float ad = fabsf(DET);
-    if (ad > 1e-30f && ad < 1e30f) {
-        const float r = 1.0f / DET;
+    const float r = 1.0f / DET;
 #pragma unroll
-        for (int i = 0; i < 6; ++i) k[i] = div_by(n[i], DET, r);
-    } else {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) k[i] = n[i] / DET;
-    }
+    for (int i = 0; i < 6; ++i) k[i] = div_by(n[i], DET, r);
     er[0] = euler_rate_row(0, k[0], k[1], w0, w1, w2);
     er[1] = euler_rate_row(1, k[2], k[3], w0, w1, w2);
     er[2] = euler_rate_row(2, k[4], k[5], w0, w1, w2);

@@ -331,8 +331,78 @@ __device__ __forceinline__ float qp(float v) {
 }
 __device__ __forceinline__ float sel3(int c, float a0, float a1, float a2) { return c == 0 ? a0 : (c == 1 ? a1 : a2); }
 
+// Lane constants of the four-lane layout: lane c in {0,1,2} owns component c, lane 3 mirrors lane 2.
+struct QuadLane {
+    int c;
+    float g, Ir0, Ir1, Ir2, Ii0, Ii1, Ii2;
+};
+__device__ __forceinline__ QuadLane quad_lane(const ModelConst& mc, int c) {
+    QuadLane L;
+    L.c = c;
+    L.g = c == 2 ? -9.81f : 0.0f;
+    L.Ir0 = sel3(c, mc.inertia[0], mc.inertia[3], mc.inertia[6]);
+    L.Ir1 = sel3(c, mc.inertia[1], mc.inertia[4], mc.inertia[7]);
+    L.Ir2 = sel3(c, mc.inertia[2], mc.inertia[5], mc.inertia[8]);
+    L.Ii0 = sel3(c, mc.Iinv[0], mc.Iinv[3], mc.Iinv[6]);
+    L.Ii1 = sel3(c, mc.Iinv[1], mc.Iinv[4], mc.Iinv[7]);
+    L.Ii2 = sel3(c, mc.Iinv[2], mc.Iinv[5], mc.Iinv[8]);
+    return L;
+}
+
+// One explicit-Euler step of the single rigid body (Centroidal_Model_JAX.fd + integrate_jax,
+// CMJ:93-174) in the four-lane layout, from this lane's component of the contact-weighted force sum
+// `temp` = sum_i f_i c_i and torque sum `temp2` = sum_i (p_i - p_com) x f_i c_i.  The float ops and
+// their order are those of integrate() in srbd_core.h (rollout_kernel), so both layouts agree bit
+// for bit.  All four lanes of each quad must be active (DPP quad permutations).
+__device__ __forceinline__ void quad_rigid_body(const ModelConst& mc, const QuadLane& L, float temp, float temp2,
+                                                float dt, float& p, float& v, float& r, float& w) {
+    const int c = L.c;
+    const float lin = mc.inv_m * temp + L.g;
+    float sn, cs;
+    sincosf(r, &sn, &cs);
+    const float sr = qp<QP_B0>(sn), cr = qp<QP_B0>(cs);
+    const float sp = qp<QP_B1>(sn), cp = qp<QP_B1>(cs);
+    const float sy = qp<QP_B2>(sn), cy = qp<QP_B2>(cs);
+    const float w0 = qp<QP_B0>(w), w1 = qp<QP_B1>(w), w2 = qp<QP_B2>(w);
+    float k1, k2;
+    euler_rate_coefs(c, sr, cr, sp, cp, k1, k2);
+    // euler_rate_row, with both operands of every lane select computed first (straight-line code:
+    // selects, not divergent branches)
+    const float kw1 = k1 * w1;
+    const float er0 = w0 + kw1;
+    const float er = (c == 0 ? er0 : kw1) + k2 * w2;
+    // row c of b_R_w (CMJ:136-150)
+    const float A = c == 1 ? sr : cr;
+    const float B0 = c == 1 ? -cr : sr, B1 = c == 1 ? cr : -sr;
+    const float Asp = A * sp;
+    const float r0a = cp * cy, r0b = Asp * cy + B0 * sy;
+    const float r1a = cp * sy, r1b = Asp * sy + B1 * cy;
+    const float r2b = A * cp;
+    const float R0 = c == 0 ? r0a : r0b;
+    const float R1 = c == 0 ? r1a : r1b;
+    const float R2 = c == 0 ? -sp : r2b;
+    const float Rt = R0 * qp<QP_B0>(temp2) + R1 * qp<QP_B1>(temp2) + R2 * qp<QP_B2>(temp2);
+    const float Iw = L.Ir0 * w0 + L.Ir1 * w1 + L.Ir2 * w2;
+    const float wx = (-qp<QP_NEXT2>(w)) * qp<QP_NEXT>(Iw) + qp<QP_NEXT>(w) * qp<QP_NEXT2>(Iw);
+    const float a1 = L.Ii0 * qp<QP_B0>(wx) + L.Ii1 * qp<QP_B1>(wx) + L.Ii2 * qp<QP_B2>(wx);
+    const float a2 = L.Ii0 * qp<QP_B0>(Rt) + L.Ii1 * qp<QP_B1>(Rt) + L.Ii2 * qp<QP_B2>(Rt);
+    const float aa = -a1 + a2;
+    const float pn = p + v * dt, vn = v + lin * dt, rn = r + er * dt, wn = w + aa * dt;
+    p = pn;
+    v = vn;
+    r = rn;
+    w = wn;
+}
+
+// This lane's component of (p_i - p_com) x f_i (jnp.dot(skew(v), f), CMJ:100-101, zero terms dropped).
+__device__ __forceinline__ float quad_cross(float vl, float fl) {
+    const float vn1 = qp<QP_NEXT>(vl), vn2 = qp<QP_NEXT2>(vl);
+    const float fn1 = qp<QP_NEXT>(fl), fn2 = qp<QP_NEXT2>(fl);
+    return (-vn2) * fn1 + vn1 * fn2;
+}
+
 template <int KIND, int HT, int ST>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) rollout_quad_kernel(const ModelConst mc, const StepInput* __restrict__ in,
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) rollout_quad_kernel(const ModelConst mc, const StepInput* __restrict__ in,
                                                            const float* __restrict__ noise, float* __restrict__ costs,
                                                            float* __restrict__ recs, int rec_stride,
     const RngJob next_rng, int nroll) {
@@ -342,11 +412,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) r
                   ((int)gridDim.x - nroll) * (int)blockDim.x);
         return;
     }
-    __shared__ float e_sh[64];
-    __shared__ uint64_t red[4];
+    __shared__ float e_sh[128];
+    __shared__ uint64_t red[8];
     __shared__ uint64_t elite_sh[MAXK];
 
     constexpr bool CT = HT > 0 && (KIND == SRBD_ZERO_ORDER || ST > 0);
+    const int SPB = (int)blockDim.x >> 2;  // samples per block: 64 or 128
     const int H = CT ? HT : mc.H;
     const int S = CT ? ST : mc.S;
     const int PL = CT ? (KIND == SRBD_ZERO_ORDER ? 3 * HT : (KIND == SRBD_LINEAR_SPLINE ? 3 * (ST + 1) : 12 * ST))
@@ -355,19 +426,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) r
     const int q4 = tid & 3;
     const int c = q4 < 3 ? q4 : 2;
     const int sib = tid >> 2;
-    const int k = blockIdx.x * 64 + sib;
+    const int k = blockIdx.x * SPB + sib;
     const bool valid = k < mc.n_local;
     const size_t ldn = (size_t)mc.ldn;
     const float* __restrict__ nz = noise + k;
     const float* __restrict__ best = in->best;
 
     // lane constants
-    const float Ir0 = sel3(c, mc.inertia[0], mc.inertia[3], mc.inertia[6]);
-    const float Ir1 = sel3(c, mc.inertia[1], mc.inertia[4], mc.inertia[7]);
-    const float Ir2 = sel3(c, mc.inertia[2], mc.inertia[5], mc.inertia[8]);
-    const float Ii0 = sel3(c, mc.Iinv[0], mc.Iinv[3], mc.Iinv[6]);
-    const float Ii1 = sel3(c, mc.Iinv[1], mc.Iinv[4], mc.Iinv[7]);
-    const float Ii2 = sel3(c, mc.Iinv[2], mc.Iinv[5], mc.Iinv[8]);
+    const QuadLane L = quad_lane(mc, c);
     const float Qp = sel3(c, mc.Q[0], mc.Q[1], mc.Q[2]), Qv = sel3(c, mc.Q[3], mc.Q[4], mc.Q[5]);
     const float Qr = sel3(c, mc.Q[6], mc.Q[7], mc.Q[8]), Qw = sel3(c, mc.Q[9], mc.Q[10], mc.Q[11]);
     const float* st = in->state;
@@ -377,7 +443,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) r
     float feet[4];
 #pragma unroll
     for (int l = 0; l < 4; ++l) feet[l] = sel3(c, st[12 + 3 * l], st[13 + 3 * l], st[14 + 3 * l]);
-    const float g = c == 2 ? -9.81f : 0.0f;
     float p = sel3(c, st[0], st[1], st[2]), v = sel3(c, st[3], st[4], st[5]);
     float r = sel3(c, st[6], st[7], st[8]), w = sel3(c, st[9], st[10], st[11]);
     float cost = 0.0f;
@@ -409,7 +474,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) r
         const float cl[4] = {in->contact[0][n], in->contact[1][n], in->contact[2][n], in->contact[3][n]};
         const float fref = in->fzref[n];
         const int idx = CT && KIND != SRBD_ZERO_ORDER ? chunk_index(n, HT, ST) : mc.sidx[n];
-        float f[4];
+        // force and torque sums in leg order (integrate(): temp = sum_i f_i c_i, temp2 = sum_i t_i c_i;
+        // 0 + x == x).  No per-leg branch on the contact flags: the straight-line horizon schedules
+        // better than it saves (measured 15.9 -> 17.1 us at C2 with the branches)
+        float temp = 0.0f, temp2 = 0.0f;
 #pragma unroll
         for (int l = 0; l < 4; ++l) {
             const int base = l * PL;
@@ -440,54 +508,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) r
             float zp = clamp_cs((fref + raw) * cl[l], mc.grf_min, mc.grf_max);
             const float xy = div3(raw * cl[l]);
             const float fz = qp<QP_B2>(c == 2 ? zp : xy);
-            f[l] = c == 2 ? fz : clamp_cs(xy, mc.neg_mu * fz, mc.mu * fz);
+            const float f = c == 2 ? fz : clamp_cs(xy, mc.neg_mu * fz, mc.mu * fz);
+            temp = temp + f * cl[l];
+            temp2 = temp2 + quad_cross(feet[l] - p, f) * cl[l];
         }
-        const float temp = f[0] * cl[0] + f[1] * cl[1] + f[2] * cl[2] + f[3] * cl[3];
-        const float lin = mc.inv_m * temp + g;
-        float temp2 = 0.0f;
-#pragma unroll
-        for (int l = 0; l < 4; ++l) {
-            const float vl = feet[l] - p;
-            const float vn1 = qp<QP_NEXT>(vl), vn2 = qp<QP_NEXT2>(vl);
-            const float fn1 = qp<QP_NEXT>(f[l]), fn2 = qp<QP_NEXT2>(f[l]);
-            const float t = (-vn2) * fn1 + vn1 * fn2;
-            temp2 = l == 0 ? t * cl[0] : temp2 + t * cl[l];
-        }
-        float sn, cs;
-        sincosf(r, &sn, &cs);
-        const float sr = qp<QP_B0>(sn), cr = qp<QP_B0>(cs);
-        const float sp = qp<QP_B1>(sn), cp = qp<QP_B1>(cs);
-        const float sy = qp<QP_B2>(sn), cy = qp<QP_B2>(cs);
-        const float w0 = qp<QP_B0>(w), w1 = qp<QP_B1>(w), w2 = qp<QP_B2>(w);
-        float k1, k2;
-        euler_rate_coefs(c, sr, cr, sp, cp, k1, k2);
-        // euler_rate_row, with both operands of every lane select computed first (straight-line code:
-        // selects, not divergent branches)
-        const float kw1 = k1 * w1;
-        const float er0 = w0 + kw1;
-        const float er = (c == 0 ? er0 : kw1) + k2 * w2;
-        // row c of b_R_w (CMJ:136-150)
-        const float A = c == 1 ? sr : cr;
-        const float B0 = c == 1 ? -cr : sr, B1 = c == 1 ? cr : -sr;
-        const float Asp = A * sp;
-        const float r0a = cp * cy, r0b = Asp * cy + B0 * sy;
-        const float r1a = cp * sy, r1b = Asp * sy + B1 * cy;
-        const float r2b = A * cp;
-        const float R0 = c == 0 ? r0a : r0b;
-        const float R1 = c == 0 ? r1a : r1b;
-        const float R2 = c == 0 ? -sp : r2b;
-        const float Rt = R0 * qp<QP_B0>(temp2) + R1 * qp<QP_B1>(temp2) + R2 * qp<QP_B2>(temp2);
-        const float Iw = Ir0 * w0 + Ir1 * w1 + Ir2 * w2;
-        const float wx = (-qp<QP_NEXT2>(w)) * qp<QP_NEXT>(Iw) + qp<QP_NEXT>(w) * qp<QP_NEXT2>(Iw);
-        const float a1 = Ii0 * qp<QP_B0>(wx) + Ii1 * qp<QP_B1>(wx) + Ii2 * qp<QP_B2>(wx);
-        const float a2 = Ii0 * qp<QP_B0>(Rt) + Ii1 * qp<QP_B1>(Rt) + Ii2 * qp<QP_B2>(Rt);
-        const float aa = -a1 + a2;
-        const float dt = mc.dts[n];
-        const float pn = p + v * dt, vn = v + lin * dt, rn = r + er * dt, wn = w + aa * dt;
-        p = pn;
-        v = vn;
-        r = rn;
-        w = wn;
+        quad_rigid_body(mc, L, temp, temp2, mc.dts[n], p, v, r, w);
         // tracking cost (NMPC:451), accumulated per component lane: cost_c += ((tp + tv) + tr) + tw,
         // the three lanes summed once after the horizon (see rollout_kernel for the same order)
         const float ep = p - rp, ev = v - rv, er_ = r - rr, ew = w - rw;
@@ -503,7 +528,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) r
     cost = cost + in->cost_feet;  // 0, or NaN when a foot term is non-finite (Q_feet = 0)
     if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
     if (valid && q4 == 0 && costs) costs[k] = cost;
-    block_epilogue(mc, in, 64, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh);
+    block_epilogue(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh);
 }
 
 // ------------------------------------------------------------------ merge
@@ -580,7 +605,21 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst m
     float* part = smem + nrec_pad;
     float* erow = part + ((G * cols + 3) & ~3);
 
-    // ---- L: loads
+    // ---- L: loads.  The StepInput fields the output phases need are fetched here too, so their
+    // latency hides under the record loads instead of stalling the tail.
+    const float best_pre = (out && tid < P) ? in->best[tid] : 0.0f;
+    const int qc = tid < 3 ? tid : 2;  // tail lanes 0..3: component of the four-lane layout
+    float tail_pre[13];
+    if (out && tid < 4) {
+        tail_pre[0] = in->fzref[0];
+#pragma unroll
+        for (int l = 0; l < 4; ++l) tail_pre[1 + l] = in->contact[l][0];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tail_pre[5 + q] = in->state[3 * q + qc];  // p, v, rpy, omega
+#pragma unroll
+        for (int l = 0; l < 4; ++l) tail_pre[9 + l] = in->state[12 + 3 * l + qc];  // feet
+    }
+    const float state_hi = (out && tid >= 12 && tid < 24) ? in->state[tid] : 0.0f;
     float mr[MERGE_RPT];
     uint64_t mine = KEY_NONE;
 #pragma unroll
@@ -714,7 +753,7 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst m
     }
     if (out) {
         for (int jj = tid; jj < P; jj += T) {
-            const float b0 = in->best[jj];
+            const float b0 = jj == tid ? best_pre : in->best[jj];
             const float v = rs ? b0 + erow[jj] : b0 + Vs[jj] / Vs[P];
             nb[jj] = v;
             out->best[jj] = v;
@@ -744,23 +783,34 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst m
             float fx, fy, fz;
             decode_leg(mc.kind, mc.H, mc.S, mc.fidx, mc.fq, mc.fomq, mc.fa, mc.fb, mc.fc, mc.fd, 0, acc, fx, fy,
                        fz);
-            shape_leg(mc, in->fzref[0], in->contact[leg][0], fx, fy, fz);
+            shape_leg(mc, tail_pre[0], tail_pre[1 + leg], fx, fy, fz);
             grf_sh[3 * leg] = fx;
             grf_sh[3 * leg + 1] = fy;
             grf_sh[3 * leg + 2] = fz;
         }
         __syncthreads();
         if (tid < 12) out->grf[tid] = grf_sh[tid];
-        if (tid == 0) {  // predicted state (NMPC:752-784)
-            const float c[4] = {in->contact[0][0], in->contact[1][0], in->contact[2][0], in->contact[3][0]};
-            float x[12], F[12];
-            for (int i = 0; i < 12; ++i) {
-                x[i] = in->state[i];
-                F[i] = grf_sh[i];
+        if (tid < 4) {  // predicted state (NMPC:752-784): one Euler step in the four-lane layout
+            const int c = qc;
+            const QuadLane L = quad_lane(mc, c);
+            float p = tail_pre[5], v = tail_pre[6], r = tail_pre[7], w = tail_pre[8];
+            const float c0 = tail_pre[1], c1 = tail_pre[2], c2 = tail_pre[3], c3 = tail_pre[4];
+            const float f0 = grf_sh[c], f1 = grf_sh[3 + c], f2 = grf_sh[6 + c], f3 = grf_sh[9 + c];
+            const float temp = f0 * c0 + f1 * c1 + f2 * c2 + f3 * c3;  // integrate()'s order
+            float temp2 = quad_cross(tail_pre[9] - p, f0) * c0;
+            temp2 = temp2 + quad_cross(tail_pre[10] - p, f1) * c1;
+            temp2 = temp2 + quad_cross(tail_pre[11] - p, f2) * c2;
+            temp2 = temp2 + quad_cross(tail_pre[12] - p, f3) * c3;
+            quad_rigid_body(mc, L, temp, temp2, mc.dts[0], p, v, r, w);
+            if (tid < 3) {
+                out->pred[c] = p;
+                out->pred[3 + c] = v;
+                out->pred[6 + c] = r;
+                out->pred[9 + c] = w;
             }
-            integrate(mc, x, in->state + 12, F, c, mc.dts[0]);
-            for (int i = 0; i < 12; ++i) out->pred[i] = x[i];
-            for (int i = 12; i < 24; ++i) out->pred[i] = in->state[i];
+        }
+        if (tid >= 12 && tid < 24) out->pred[tid] = state_hi;
+        if (tid == 0) {
             out->best_cost = beta;
             out->best_index = (int32_t)(uint32_t)bkey;
             out->status = 0;
@@ -812,10 +862,11 @@ static void launch_rollout_t(const ModelConst& mc, const StepInput* in, const fl
                              float* recs, int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next) {
     const RngJob job = next ? *next : RngJob{nullptr, 0, 0, 0, 0};
     const int extra = next ? (rng_grid(mc) < 1024 ? rng_grid(mc) : 1024) : 0;
-    if (mode == ROLLOUT_QUAD) {
-        const int blocks = (mc.n_local + 63) / 64;
-        hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST>), dim3(blocks + extra), dim3(256), 0, s, mc, in, noise,
-                           costs, recs, rec_stride, job, blocks);
+    if (mode == ROLLOUT_QUAD) {  // `threads` = 4 lanes x samples per block (256 or 512)
+        const int spb = threads / 4;
+        const int blocks = (mc.n_local + spb - 1) / spb;
+        hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST>), dim3(blocks + extra * 256 / threads), dim3(threads), 0,
+                           s, mc, in, noise, costs, recs, rec_stride, job, blocks);
     } else {
         const int blocks = (mc.n_local + threads - 1) / threads;
         hipLaunchKernelGGL((rollout_kernel<KIND, HT, ST>), dim3(blocks + extra * (256 / threads)), dim3(threads), 0, s,
