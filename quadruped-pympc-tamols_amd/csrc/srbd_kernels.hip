@@ -14,6 +14,8 @@
 
 #include "srbd_launch.h"
 
+#include <cstdlib>
+
 namespace srbd {
 
 // ------------------------------------------------------------------ helpers
@@ -57,13 +59,13 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
             k0 += 0x9E3779B9u;
             k1 += 0xBB67AE85u;
         }
-        const uint32_t lo0 = 0xD2511F53u * c[0], hi0 = __umulhi(0xD2511F53u, c[0]);
-        const uint32_t lo1 = 0xCD9E8D57u * c[2], hi1 = __umulhi(0xCD9E8D57u, c[2]);
-        const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        // one 32x32->64 multiply each (v_mad_u64_u32) instead of separate lo / hi multiplies
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
         c[0] = n0;
-        c[1] = lo1;
+        c[1] = (uint32_t)p1;
         c[2] = n2;
-        c[3] = lo0;
+        c[3] = (uint32_t)p0;
     }
 }
 
@@ -74,60 +76,61 @@ __device__ __forceinline__ float u01(uint32_t x) { return ((float)(x >> 8) + 0.5
 // (NMPC:647-677): rows 1..t sigma0*Z(r-1), rows t+1..2t sigma1*Z(r-1-t) (same draws: the reference
 // reuses one key, App. B #3), rows 2t+1..N-1 U(-s2, s2) from draw r-1-2t.  Row 0 is zero.
 // One item = (local row k, column quad q): one Philox4x32-10 call, two Box-Muller pairs.
-__device__ __forceinline__ void rng_item(const ModelConst& mc, const float* __restrict__ sigma, uint64_t seed,
-                                         uint64_t ctr, int k, int q, float* __restrict__ noise) {
-    const int r = mc.row0 + k;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (r > 0) {
-        const int t = mc.N / 3;
-        uint32_t d = (uint32_t)(r - 1);
-        int mode = mc.method == SRBD_MPPI ? 3 : (mc.method == SRBD_CEM_MPPI ? 4 : 0);
-        if (mc.method == SRBD_RANDOM_SAMPLING) {
-            if (r <= t) {
-                mode = 0;
-            } else if (r <= 2 * t) {
-                mode = 1;
-                d = (uint32_t)(r - 1 - t);
-            } else {
-                mode = 2;
-                d = (uint32_t)(r - 1 - 2 * t);
-            }
-        }
-        uint32_t c[4] = {d, (uint32_t)q, (uint32_t)ctr, (uint32_t)(ctr >> 32)};
-        philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-        if (mode == 2) {
-            const float s2 = mc.sigma_rs[2];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = u01(c[i]) * (2.0f * s2) - s2;
-        } else {
-            float z[4];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const float ua = u01(c[2 * h]), ub = u01(c[2 * h + 1]);
-                const float rr = sqrtf(-2.0f * logf(ua));
-                float s, co;
-                sincospif(2.0f * ub, &s, &co);  // sin/cos(2 pi ub) without a large-argument reduction
-                z[2 * h] = rr * co;
-                z[2 * h + 1] = rr * s;
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int j = 4 * q + i;
-                if (mode == 0) v[i] = mc.sigma_rs[0] * z[i];
-                else if (mode == 1) v[i] = mc.sigma_rs[1] * z[i];
-                else if (mode == 3) v[i] = mc.sigma_mppi * z[i];
-                else v[i] = z[i] * sigma[j < mc.P ? j : 0];
-            }
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int j = 4 * q + i;
-        if (j < mc.P) noise[(size_t)j * mc.ldn + k] = v[i];
-    }
+// Box-Muller on the hardware transcendentals: v_log_f32 (log2), v_sqrt_f32, and v_sin/v_cos_f32,
+// which take revolutions, i.e. sin/cos(2 pi ub) directly with no range reduction (ub in (0, 1)).
+// They differ from libm by a few ulp (the host oracle's draws agree to ~1e-6 relative).
+__device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
+    const float ua = u01(a), ub = u01(b);
+    const float rr = __builtin_amdgcn_sqrtf(-1.38629436112f * __builtin_amdgcn_logf(ua));  // -2 ln ua
+    z0 = rr * __builtin_amdgcn_cosf(ub);
+    z1 = rr * __builtin_amdgcn_sinf(ub);
 }
 
-// Items (k, q) enumerated k-fastest so consecutive lanes store consecutive floats.
+__device__ __forceinline__ void rng_item(const ModelConst& mc, const float* __restrict__ sigma, uint32_t key0,
+                                         uint32_t key1, uint32_t c2, uint32_t c3, int k, int q,
+                                         float* __restrict__ noise) {
+    const int r = mc.row0 + k;
+    uint32_t d = (uint32_t)(r - 1);
+    float scale = mc.sigma_mppi;  // MPPI
+    bool uniform = false;
+    if (mc.method == SRBD_RANDOM_SAMPLING) {
+        const int t = mc.N / 3;
+        if (r <= t) {
+            scale = mc.sigma_rs[0];
+        } else if (r <= 2 * t) {
+            scale = mc.sigma_rs[1];
+            d = (uint32_t)(r - 1 - t);
+        } else {
+            uniform = true;
+            d = (uint32_t)(r - 1 - 2 * t);
+        }
+    }
+    uint32_t c[4] = {d, (uint32_t)q, c2, c3};
+    philox4x32_10(c, key0, key1);
+    float v[4];
+    if (uniform) {
+        const float s2 = mc.sigma_rs[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = u01(c[i]) * (2.0f * s2) - s2;
+    } else {
+        box_muller(c[0], c[1], v[0], v[1]);
+        box_muller(c[2], c[3], v[2], v[3]);
+        if (mc.method == SRBD_CEM_MPPI) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = v[i] * sigma[4 * q + i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = scale * v[i];
+        }
+    }
+    const size_t ldn = (size_t)mc.ldn;
+    float* __restrict__ o = noise + (size_t)(4 * q) * ldn + k;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i * ldn] = r > 0 ? v[i] : 0.0f;  // row 0: the warm start itself
+}
+
+// Items (k, q) enumerated k-fastest so consecutive lanes store consecutive floats; the item index is
+// advanced incrementally (no per-item division).  P is a multiple of 12, so quads are whole.
 __device__ __forceinline__ void rng_items(const ModelConst& mc, const StepInput* __restrict__ in, const RngJob& job,
                                           int first, int stride) {
     uint64_t seed = job.seed, ctr = job.ctr;
@@ -135,11 +138,18 @@ __device__ __forceinline__ void rng_items(const ModelConst& mc, const StepInput*
         seed = ((uint64_t)in->seed_hi << 32) | in->seed_lo;
         ctr = (((uint64_t)in->ctr_hi << 32) | in->ctr_lo) + (uint64_t)job.ctr_offset;
     }
-    const int nq = (mc.P + 3) / 4;
-    const int total = mc.n_local * nq;
-    for (int it = first; it < total; it += stride) {
-        const int q = it / mc.n_local, k = it - q * mc.n_local;
-        rng_item(mc, in->sigma, seed, ctr, k, q, job.noise);
+    const int n = mc.n_local, nq = mc.P / 4;
+    int q = first / n, k = first - q * n;
+    const int sq = stride / n, sk = stride - sq * n;
+    while (q < nq) {
+        rng_item(mc, in->sigma, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ctr, (uint32_t)(ctr >> 32), k, q,
+                 job.noise);
+        k += sk;
+        q += sq;
+        if (k >= n) {
+            k -= n;
+            ++q;
+        }
     }
 }
 
@@ -542,21 +552,56 @@ constexpr int MERGE_PREF = 24;  // record values of the weighted sums loaded per
 constexpr int MERGE_RPT = 8;    // record headers per thread (nrec <= MERGE_RPT * MERGE_THREADS)
 constexpr uint64_t KEY_NONE = ~0ull;
 
-// Sorted (ascending) per-lane candidate list of at most MAXK keys; fully unrolled (registers only).
-__device__ __forceinline__ void lk_insert(uint64_t (&lk)[MAXK], uint64_t x) {
+// Sorted (ascending) per-lane candidate list of at most KM keys; fully unrolled (registers only).
+template <int KM>
+__device__ __forceinline__ void lk_insert(uint64_t (&lk)[KM], uint64_t x) {
 #pragma unroll
-    for (int i = MAXK - 1; i >= 1; --i) lk[i] = (x < lk[i - 1]) ? lk[i - 1] : (x < lk[i] ? x : lk[i]);
+    for (int i = KM - 1; i >= 1; --i) lk[i] = (x < lk[i - 1]) ? lk[i - 1] : (x < lk[i] ? x : lk[i]);
     lk[0] = x < lk[0] ? x : lk[0];
 }
 // K rounds of a wave-wide minimum over the lanes' list heads; the (unique) winning lane pops.
-__device__ __forceinline__ void wave_topk(uint64_t (&lk)[MAXK], int K, uint64_t* out) {
+template <int KM>
+__device__ __forceinline__ void wave_topk(uint64_t (&lk)[KM], int K, uint64_t* out) {
     for (int e = 0; e < K; ++e) {
         const uint64_t m = wave_min_u64(lk[0]);
         const bool pop = lk[0] == m && m != KEY_NONE;
 #pragma unroll
-        for (int i = 0; i < MAXK - 1; ++i) lk[i] = pop ? lk[i + 1] : lk[i];
-        lk[MAXK - 1] = pop ? KEY_NONE : lk[MAXK - 1];
+        for (int i = 0; i < KM - 1; ++i) lk[i] = pop ? lk[i + 1] : lk[i];
+        lk[KM - 1] = pop ? KEY_NONE : lk[KM - 1];
         if ((threadIdx.x & 63) == 0) out[e] = m;
+    }
+}
+
+// Block-wide K smallest record keys (ascending) into `elite`, K <= KM: every thread's list starts as
+// its first record's keys (a record's keys ascend already), later records insert; per-wave K-round
+// minima; then one wave over the MERGE_WAVES wave lists.  Caller syncs afterwards.
+template <int KM>
+__device__ __forceinline__ void block_topk(const float* __restrict__ recs, int nrec, int rec_stride, int P, int K,
+                                           uint64_t (*wlist)[MAXK], uint64_t* elite) {
+    const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wv = tid >> 6;
+    uint64_t lk[KM];
+#pragma unroll
+    for (int i = 0; i < KM; ++i) lk[i] = KEY_NONE;
+    for (int r = tid; r < nrec; r += T) {
+        const float* R = recs + (size_t)r * rec_stride;
+        uint64_t keys[KM];  // all of the record's keys in one memory round trip
+#pragma unroll
+        for (int q = 0; q < KM; ++q) keys[q] = q < K ? rec_key(R, P, q) : KEY_NONE;
+        if (r == tid) {
+#pragma unroll
+            for (int q = 0; q < KM; ++q) lk[q] = keys[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < KM; ++q)
+                if (keys[q] < lk[K - 1]) lk_insert(lk, keys[q]);  // later keys fail too
+        }
+    }
+    wave_topk(lk, K, wlist[wv]);
+    __syncthreads();
+    if (wv == 0) {
+#pragma unroll
+        for (int i = 0; i < KM; ++i) lk[i] = (lane < MERGE_WAVES && i < K) ? wlist[lane][i] : KEY_NONE;
+        wave_topk(lk, K, elite);
     }
 }
 
@@ -686,24 +731,10 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst m
     if (K == 1) {
         if (tid == 0) elite[0] = bkey;
     } else {
-        uint64_t lk[MAXK];
-#pragma unroll
-        for (int i = 0; i < MAXK; ++i) lk[i] = KEY_NONE;
-        for (int r = tid; r < nrec; r += T) {
-            const float* R = recs + (size_t)r * rec_stride;
-            for (int q = 0; q < K; ++q) {
-                const uint64_t x = rec_key(R, P, q);
-                if (x >= lk[K - 1]) break;  // the record's keys ascend
-                lk_insert(lk, x);
-            }
-        }
-        wave_topk(lk, K, wlist[wv]);
-        __syncthreads();
-        if (wv == 0) {
-#pragma unroll
-            for (int i = 0; i < MAXK; ++i) lk[i] = (lane < MERGE_WAVES && i < K) ? wlist[lane][i] : KEY_NONE;
-            wave_topk(lk, K, elite);
-        }
+        if (K <= 10)
+            block_topk<10>(recs, nrec, rec_stride, P, K, wlist, elite);
+        else
+            block_topk<MAXK>(recs, nrec, rec_stride, P, K, wlist, elite);
     }
     __syncthreads();
     // record slot of every elite key (needed when rows travel inside the records)
@@ -932,9 +963,16 @@ void launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nr
                        pub.seq);
 }
 
+int tune_knob(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return (e && atoi(e) > 0) ? atoi(e) : dflt;
+}
+
 int merge_partials(int nrec) {
-    if (nrec <= MERGE_DIRECT_MAX) return 0;
-    int m = (nrec + MERGE_PER_BLOCK - 1) / MERGE_PER_BLOCK;
+    static const int direct_max = tune_knob("SRBD_MERGE_DIRECT_MAX", MERGE_DIRECT_MAX);
+    static const int per_block = tune_knob("SRBD_MERGE_PER_BLOCK", MERGE_PER_BLOCK);
+    if (nrec <= direct_max) return 0;
+    int m = (nrec + per_block - 1) / per_block;
     return m > MERGE_MAX_PARTIALS ? MERGE_MAX_PARTIALS : m;
 }
 

@@ -40,10 +40,13 @@ void launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nr
 // Two-level merge when there are many block records: merge_partials(nrec) first-level blocks each
 // reduce a slice of the records (spreading the record reads over CUs) into rank-format partials,
 // then one block merges the partials.
-constexpr int MERGE_DIRECT_MAX = 1024;
-constexpr int MERGE_PER_BLOCK = 16;
+// Defaults (measured, scripts/kernel_sweep.py); SRBD_MERGE_DIRECT_MAX / SRBD_MERGE_PER_BLOCK override.
+constexpr int MERGE_DIRECT_MAX = 256;
+constexpr int MERGE_PER_BLOCK = 32;
 constexpr int MERGE_MAX_PARTIALS = 64;
 int merge_partials(int nrec);
+// Integer tuning knob from the environment (read once), else `dflt`.
+int tune_knob(const char* name, int dflt);
 void launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                        const float* noise, float* partials, float* rank_out, StepOutput* out, int chain,
                        hipStream_t s, int ctr_inc = 1, Publish pub = {nullptr, 0});
