@@ -358,12 +358,20 @@ extern "C" int srbd_set_stream(srbd_ctx* c, void* s) {
 }
 
 // ------------------------------------------------------------------ step
-// Draw the next step's noise inside the rollout launch (extra blocks beside the rollout) when the
-// draws do not depend on this step (not CEM).  Measured: N = 65 536 MPPI 64.2 -> 53.9 us per step;
-// SRBD_FUSE_MAX overrides the row limit.
+// Draw the next step's noise inside the rollout launch (extra blocks beside the rollout).  The draws
+// never depend on the step (CEM stores unscaled normals, scaled by sigma on read).  Measured per
+// step: N = 65 536 MPPI 64.2 -> 53.9 us, CEM cubic H16 98.4 -> 89.9 us, CEM N = 10 000 52.4 ->
+// 48.3 us; SRBD_FUSE_MAX overrides the row limit.
 static bool fusable(const srbd_ctx* c) {
     static const int fuse_max = tune_knob("SRBD_FUSE_MAX", 65536);
-    return c->mc.method != SRBD_CEM_MPPI && c->mc.n_local <= fuse_max;
+    return c->mc.n_local <= fuse_max;
+}
+
+// Device-chain steps draw on the device: CEM draws are then unscaled (StepInput::noise_scaled = 0)
+// whatever the last host step injected.
+static int reset_noise_scaled(srbd_ctx* c) {
+    HIP_TRY(c, hipMemsetAsync(&c->d_in->noise_scaled, 0, sizeof(int32_t), c->stream));
+    return SRBD_OK;
 }
 
 static int upload_noise(srbd_ctx* c, const float* noise, int buf) {
@@ -528,6 +536,10 @@ extern "C" int srbd_device_step_local(srbd_ctx* c, void* d_record) {
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step_local once first");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     const bool fuse = fusable(c);
+    if (!c->chain_started) {
+        const int rc = reset_noise_scaled(c);
+        if (rc) return rc;
+    }
     if (!c->chain_started || !fuse) {  // draws of this step (device counter); later ones come fused
         c->cur = 0;
         launch_rng(c->mc, c->d_in, 0, 0, 1, 0, c->d_noise[0], c->stream);
@@ -724,6 +736,7 @@ extern "C" int srbd_bench_device_steps(srbd_ctx* c, int32_t steps, float* ms) {
     c->pref_valid = false;
     int rc;
     if (!c->g_dev2 && (rc = capture_dev_graphs(c))) return rc;
+    if ((rc = reset_noise_scaled(c))) return rc;
     hipEvent_t e0, e1;
     HIP_TRY(c, hipEventCreate(&e0));
     HIP_TRY(c, hipEventCreate(&e1));
@@ -747,6 +760,7 @@ extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, 
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     c->pref_valid = false;
     c->cur = 0;
+    if (int rc = reset_noise_scaled(c)) return rc;
     std::vector<hipEvent_t> ev(4 * iters);
     for (auto& e : ev) HIP_TRY(c, hipEventCreate(&e));
     const ModelConst& mc = c->mc;

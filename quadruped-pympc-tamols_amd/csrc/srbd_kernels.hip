@@ -71,6 +71,12 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
 
 __device__ __forceinline__ float u01(uint32_t x) { return ((float)(x >> 8) + 0.5f) * 5.9604644775390625e-08f; }
 
+// Noise buffers hold unscaled CEM draws Z when they come from the device RNG (StepInput::noise_scaled
+// == 0): readers form the noise value Z * sigma_j.  Injected noise is stored as given.
+__device__ __forceinline__ bool zs_scaled(const ModelConst& mc, const StepInput* in) {
+    return mc.method == SRBD_CEM_MPPI && in->noise_scaled == 0;
+}
+
 // ------------------------------------------------------------------ RNG
 // Noise row r (global), column j.  MPPI: sigma*Z(r-1, j); CEM: Z(r-1, j)*sigma_j; random sampling
 // (NMPC:647-677): rows 1..t sigma0*Z(r-1), rows t+1..2t sigma1*Z(r-1-t) (same draws: the reference
@@ -115,10 +121,10 @@ __device__ __forceinline__ void rng_item(const ModelConst& mc, const float* __re
     } else {
         box_muller(c[0], c[1], v[0], v[1]);
         box_muller(c[2], c[3], v[2], v[3]);
-        if (mc.method == SRBD_CEM_MPPI) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = v[i] * sigma[4 * q + i];
-        } else {
+        // CEM: the standard normals themselves (they do not depend on the step's sigma, so the next
+        // step's draws can be made early); every reader multiplies by sigma_j (zs_scale), the same
+        // float product Z * sigma the reference forms (NMPC:951-958)
+        if (mc.method != SRBD_CEM_MPPI) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) v[i] = scale * v[i];
         }
@@ -195,7 +201,7 @@ __device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, Ns.
 __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepInput* __restrict__ in, const int SPB,
                                                int sib, bool valid, float cost, const float* __restrict__ noise,
                                                float* __restrict__ recs, int rec_stride, float* e_sh, uint64_t* red,
-                                               uint64_t* elite_sh) {
+                                               uint64_t* elite_sh, bool cemt) {
     const int tid = threadIdx.x, T = blockDim.x;
     const int k0 = blockIdx.x * SPB;
     const uint64_t key = (sib >= 0 && valid) ? cost_key(cost, (uint32_t)(mc.row0 + k0 + sib)) : ~0ull;
@@ -215,17 +221,19 @@ __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepI
         __syncthreads();
         const size_t ldn = (size_t)mc.ldn;
         const float* base = noise + k0;
+        const bool zs = cemt && zs_scaled(mc, in);
         for (int j = tid; j <= P; j += T) {
             float a = 0.0f;
             if (j < P) {
                 const float4* row = reinterpret_cast<const float4*>(base + (size_t)j * ldn);
+                const float sj = zs ? in->sigma[j] : 1.0f;  // x * 1 == x
 #pragma unroll 16
                 for (int i = 0; i < SPB / 4; ++i) {
                     const float4 v = row[i];
-                    a = a + e_sh[4 * i] * v.x;
-                    a = a + e_sh[4 * i + 1] * v.y;
-                    a = a + e_sh[4 * i + 2] * v.z;
-                    a = a + e_sh[4 * i + 3] * v.w;
+                    a = a + e_sh[4 * i] * (v.x * sj);
+                    a = a + e_sh[4 * i + 1] * (v.y * sj);
+                    a = a + e_sh[4 * i + 2] * (v.z * sj);
+                    a = a + e_sh[4 * i + 3] * (v.w * sj);
                 }
                 rec[REC_HDR + j] = a;
             } else {
@@ -249,7 +257,7 @@ __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepI
 }
 
 // One thread per sample.  Best throughput when samples fill the GPU (>= ~1 wave per SIMD).
-template <int KIND, int HT, int ST>
+template <int KIND, int HT, int ST, bool CEMT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == SRBD_ZERO_ORDER ? 2 : 1))) rollout_kernel(const ModelConst mc, const StepInput* __restrict__ in,
                                                       const float* __restrict__ noise, float* __restrict__ costs,
                                                       float* __restrict__ recs, int rec_stride,
@@ -275,6 +283,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
     const size_t ldn = (size_t)mc.ldn;
     const float* __restrict__ nz = noise + k;
     const float* __restrict__ best = in->best;
+    const bool zs = CEMT && zs_scaled(mc, in);  // CEMT: CEM kernels only carry the scaling code
 
     float x[12], feet[12];
 #pragma unroll
@@ -292,7 +301,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
 #pragma unroll
         for (int leg = 0; leg < 4; ++leg) {
             const int base = leg * PL;
-            auto acc = [&](int j) { return best[base + j] + nz[(size_t)(base + j) * ldn]; };
+            auto acc = [&](int j) {
+                const float z = nz[(size_t)(base + j) * ldn];
+                return best[base + j] + (zs ? z * in->sigma[base + j] : z);
+            };
             float fx, fy, fz;
             decode_leg(KIND, H, S, idx, mc.sq[n], mc.somq[n], mc.sa[n], mc.sb[n], mc.sc[n], mc.sd[n], n, acc, fx,
                        fy, fz);
@@ -322,7 +334,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
     // NMPC:686-687
     if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
     if (valid && costs) costs[k] = cost;
-    block_epilogue(mc, in, T, tid, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh);
+    block_epilogue(mc, in, T, tid, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh, CEMT);
 }
 
 // ---- four lanes per sample: lane c in {0,1,2} owns component c (x, y, z) of every 3-vector of
@@ -411,7 +423,7 @@ __device__ __forceinline__ float quad_cross(float vl, float fl) {
     return (-vn2) * fn1 + vn1 * fn2;
 }
 
-template <int KIND, int HT, int ST>
+template <int KIND, int HT, int ST, bool CEMT>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) rollout_quad_kernel(const ModelConst mc, const StepInput* __restrict__ in,
                                                            const float* __restrict__ noise, float* __restrict__ costs,
                                                            float* __restrict__ recs, int rec_stride,
@@ -441,6 +453,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
     const size_t ldn = (size_t)mc.ldn;
     const float* __restrict__ nz = noise + k;
     const float* __restrict__ best = in->best;
+    const bool zs = CEMT && zs_scaled(mc, in);  // CEMT: CEM kernels only carry the scaling code
 
     // lane constants
     const QuadLane L = quad_lane(mc, c);
@@ -470,13 +483,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
         const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)noise, (short)0, mc.P * mc.ldn * 4, 0x00020000);
         const int voff = (cblk * mc.ldn + k) * 4;
         const float* __restrict__ bl = best + cblk;
+        const float* __restrict__ sl = in->sigma + cblk;
 #pragma unroll
         for (int l = 0; l < 4; ++l)
 #pragma unroll
             for (int i = 0; i < NPRE; ++i) {
                 const int jr = l * PL + (KIND == SRBD_CUBIC_SPLINE ? 10 * (i >> 2) + (i & 3) : i);  // row - cblk
                 const float nzv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, jr * mc.ldn * 4, 0));
-                pre[l][i] = bl[jr] + nzv;
+                pre[l][i] = bl[jr] + (zs ? nzv * sl[jr] : nzv);
             }
     }
 
@@ -497,7 +511,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
                 if constexpr (CT) {
                     return pre[l][i];
                 } else {
-                    return best[base + j] + nz[(size_t)(base + j) * ldn];
+                    const float z = nz[(size_t)(base + j) * ldn];
+                    return best[base + j] + (zs ? z * in->sigma[base + j] : z);
                 }
             };
             float raw;
@@ -538,7 +553,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
     cost = cost + in->cost_feet;  // 0, or NaN when a foot term is non-finite (Q_feet = 0)
     if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
     if (valid && q4 == 0 && costs) costs[k] = cost;
-    block_epilogue(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh);
+    block_epilogue(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh,
+                   CEMT);
 }
 
 // ------------------------------------------------------------------ merge
@@ -761,6 +777,7 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst m
                 v = recs[(size_t)(st / K) * rec_stride + REC_HDR + P + 2 * K + (size_t)(st % K) * P + jj];
             } else {
                 v = noise[(size_t)jj * mc.ldn + ((int)(uint32_t)elite[e] - mc.row0)];
+                if (zs_scaled(mc, in)) v = v * in->sigma[jj];
             }
         }
         erow[t] = v;
@@ -845,6 +862,7 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst m
             out->best_cost = beta;
             out->best_index = (int32_t)(uint32_t)bkey;
             out->status = 0;
+            if (chain) in->noise_scaled = 0;  // the chain's next draws come from the device RNG
             if (chain && ctr_inc) {
                 const uint64_t cc = (((uint64_t)in->ctr_hi << 32) | in->ctr_lo) + (uint64_t)ctr_inc;
                 in->ctr_lo = (uint32_t)cc;
@@ -893,15 +911,26 @@ static void launch_rollout_t(const ModelConst& mc, const StepInput* in, const fl
                              float* recs, int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next) {
     const RngJob job = next ? *next : RngJob{nullptr, 0, 0, 0, 0};
     const int extra = next ? (rng_grid(mc) < 1024 ? rng_grid(mc) : 1024) : 0;
+    const bool cem = mc.method == SRBD_CEM_MPPI;
     if (mode == ROLLOUT_QUAD) {  // `threads` = 4 lanes x samples per block (256 or 512)
         const int spb = threads / 4;
         const int blocks = (mc.n_local + spb - 1) / spb;
-        hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST>), dim3(blocks + extra * 256 / threads), dim3(threads), 0,
-                           s, mc, in, noise, costs, recs, rec_stride, job, blocks);
+        const dim3 grid(blocks + extra * 256 / threads);
+        if (cem)
+            hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, true>), grid, dim3(threads), 0, s, mc, in, noise,
+                               costs, recs, rec_stride, job, blocks);
+        else
+            hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false>), grid, dim3(threads), 0, s, mc, in, noise,
+                               costs, recs, rec_stride, job, blocks);
     } else {
         const int blocks = (mc.n_local + threads - 1) / threads;
-        hipLaunchKernelGGL((rollout_kernel<KIND, HT, ST>), dim3(blocks + extra * (256 / threads)), dim3(threads), 0, s,
-                           mc, in, noise, costs, recs, rec_stride, job, blocks);
+        const dim3 grid(blocks + extra * (256 / threads));
+        if (cem)
+            hipLaunchKernelGGL((rollout_kernel<KIND, HT, ST, true>), grid, dim3(threads), 0, s, mc, in, noise, costs,
+                               recs, rec_stride, job, blocks);
+        else
+            hipLaunchKernelGGL((rollout_kernel<KIND, HT, ST, false>), grid, dim3(threads), 0, s, mc, in, noise, costs,
+                               recs, rec_stride, job, blocks);
     }
 }
 
