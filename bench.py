@@ -11,7 +11,9 @@ HBM when the timed region starts; `value` = rollouts of all ranks / max-over-ran
 reference, contact and parameters in; GRFs, predicted state, parameters out; PCIe included).
 
 N>1 GPUs (torchrun, one rank per GPU): weak scaling, N = 10 000 rows per GPU of ONE MPC problem;
-each step ends in one RCCL all-gather of the per-rank partial records (the path's only exchange).
+each step ends in one RCCL all-gather of the per-rank partial records (the path's only exchange),
+issued by the library on its own stream between the rollout and the merge (torch.distributed only
+carries the RCCL unique id and the timing barrier / max-over-ranks).
 """
 from __future__ import annotations
 
@@ -25,7 +27,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "quadruped-pympc-tamols_amd"))
-if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+if int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--force-sharded" in sys.argv:
     import torch  # noqa: F401  -- before libsrbd_hip.so: one HIP runtime per process (see _lib.py)
 
 from quadruped_pympc_amd import _lib  # noqa: E402
@@ -135,20 +137,17 @@ def bench_multi(w, args, rank, world, local_rank):
         t0 = time.perf_counter()
         best, _, _ = mpc.step(s, r, c, best, seed=42, counter=1000 + k)
         lat.append(time.perf_counter() - t0)
-    for _ in range(max(1, args.warmup)):
-        mpc.device_step()
+    mpc.device_steps(max(1, args.warmup))
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        mpc.device_step()
+    mpc.device_steps(args.steps)  # rollout -> ncclAllGather -> merge per step, driven from C++
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     t = torch.tensor([wall], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall = float(t.item())
     n_local = mpc.ctx.n_local
-    mpc.ctx.set_stream(None)
     kern = mpc.ctx.time_kernels(20)
     mpc.close()
     dist.destroy_process_group()
@@ -164,12 +163,13 @@ def main():
     ap.add_argument("--latency-steps", type=int, default=500)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-sharded", action="store_true", help=argparse.SUPPRESS)  # 1-GPU rehearsal
     args = ap.parse_args()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     w = CONFIGS[args.config]
-    if world > 1:
+    if world > 1 or args.force_sharded:
         out = bench_multi(w, args, rank, world, local_rank)
     else:
         out = bench_single(w, args)

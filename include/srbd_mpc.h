@@ -147,6 +147,21 @@ int srbd_sync_result(srbd_ctx* ctx, float* best_params, float* sigma, srbd_resul
 /* Saturated costs of this rank's rows from the last step (lazy materialisation). */
 int srbd_copy_costs(srbd_ctx* ctx, float* out_costs);
 
+/*
+ * Sharded transport owned by the library (one process per GPU).  RCCL is loaded at run time from
+ * `rccl_path` (the copy the process already uses, e.g. torch/lib/librccl.so) or /opt/rocm/lib.
+ *   srbd_comm_get_unique_id : rank 0 makes the id (128 bytes); the caller broadcasts it
+ *   srbd_comm_init          : every rank joins (rank / world_size from the context's config)
+ *   srbd_step_sharded       : srbd_step_local + ncclAllGather of the rank records + srbd_step_finish
+ *   srbd_sharded_device_steps: `steps` device-resident sharded steps, elapsed ms (hipEvents)
+ */
+int srbd_comm_get_unique_id(const char* rccl_path, uint8_t* id_out);
+int srbd_comm_init(srbd_ctx* ctx, const char* rccl_path, const uint8_t* id_in);
+int srbd_step_sharded(srbd_ctx* ctx, const float* state, const float* ref, const float* contact,
+                      int32_t contact_stride, float* best_params, float* sigma, const float* noise_local,
+                      uint64_t seed, uint64_t counter, srbd_result* out, float* out_costs_local);
+int srbd_sharded_device_steps(srbd_ctx* ctx, int32_t steps, float* elapsed_ms);
+
 /* Diagnostic: mean duration (us) of the merge kernel's 5 phases (s_memrealtime stamps). */
 int srbd_debug_merge_phases(srbd_ctx* ctx, int32_t iters, float* out_us);
 

@@ -4,6 +4,7 @@
 // buffer and its device copy (one H2D per step), the noise matrix in SoA layout [P][ldn]
 // (ldn = rows rounded up to 256, padding zero), the per-block partial records, a StepOutput
 // (one D2H per step) and, optionally, a captured hipGraph of the whole step.
+#include <dlfcn.h>
 #include <math.h>
 #include <stdlib.h>
 #include <stdio.h>
@@ -12,6 +13,8 @@
 #include <algorithm>
 #include <string>
 #include <vector>
+
+#include <rccl/rccl.h>  // types only: RCCL is dlopen'ed (the caller's copy, e.g. torch's)
 
 #include "srbd_launch.h"
 
@@ -63,6 +66,12 @@ struct srbd_ctx {
     uint32_t* h_flag = nullptr;
     uint32_t* d_flag = nullptr;
     uint32_t seq = 0;
+    // Sharded transport owned by the library: an RCCL communicator (srbd_comm_init) and the rank
+    // record / gathered records it exchanges with ncclAllGather on the context stream.
+    ncclComm_t comm = nullptr;
+    int comm_world = 0;
+    float* d_myrec = nullptr;
+    float* d_gath = nullptr;
     // Noise matrices, double buffered: the rollout launch of a step reading d_noise[cur] also draws the
     // predicted next step's noise (counter + 1) into the other buffer (MPPI / random sampling; CEM's
     // draws depend on the sigma the step produces).
@@ -317,10 +326,13 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     return SRBD_OK;
 }
 
+static void comm_release(srbd_ctx* c);
+
 extern "C" void srbd_destroy(srbd_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device_id);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    comm_release(c);
     if (c->g_dev2) (void)hipGraphExecDestroy(c->g_dev2);
     if (c->g_dev1) (void)hipGraphExecDestroy(c->g_dev1);
     for (int b = 0; b < 2; ++b) (void)hipFree(c->d_noise[b]);
@@ -699,6 +711,132 @@ extern "C" int srbd_finish_host(const srbd_config* cfg, const float* recs, int32
     }
     delete in;
     return SRBD_OK;
+}
+
+// ------------------------------------------------------------------ sharded transport (RCCL)
+// One process per GPU; torch.distributed (or any launcher) only carries rank 0's ncclUniqueId.
+// Every step then runs from C++: rollout -> rank record -> ncclAllGather over xGMI -> merge, all on
+// the context stream, so a Python loop never sits between the kernels and the collective.
+namespace {
+struct RcclApi {
+    void* h = nullptr;
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+RcclApi g_rccl;
+std::string g_rccl_err;
+
+// Resolve RCCL from `path` (the copy the process already uses, e.g. torch/lib/librccl.so), else the
+// system one.  dlopen of an already loaded path returns that same object.
+bool rccl_load(const char* path) {
+    if (g_rccl.h) return true;
+    const char* cands[3] = {path, "/opt/rocm/lib/librccl.so.1", "librccl.so.1"};
+    for (const char* p : cands) {
+        if (!p || !*p) continue;
+        void* h = dlopen(p, RTLD_NOW | RTLD_LOCAL);
+        if (!h) continue;
+        RcclApi a;
+        a.h = h;
+        a.get_unique_id = (decltype(a.get_unique_id))dlsym(h, "ncclGetUniqueId");
+        a.comm_init_rank = (decltype(a.comm_init_rank))dlsym(h, "ncclCommInitRank");
+        a.comm_destroy = (decltype(a.comm_destroy))dlsym(h, "ncclCommDestroy");
+        a.all_gather = (decltype(a.all_gather))dlsym(h, "ncclAllGather");
+        a.error_string = (decltype(a.error_string))dlsym(h, "ncclGetErrorString");
+        if (a.get_unique_id && a.comm_init_rank && a.comm_destroy && a.all_gather && a.error_string) {
+            g_rccl = a;
+            return true;
+        }
+        dlclose(h);
+    }
+    g_rccl_err = "RCCL not found (tried the given path and /opt/rocm/lib/librccl.so.1)";
+    return false;
+}
+}  // namespace
+
+#define RCCL_TRY(ctx, expr)                                                                   \
+    do {                                                                                      \
+        const ncclResult_t r_ = (expr);                                                       \
+        if (r_ != ncclSuccess) return fail((ctx), SRBD_E_HIP, std::string(#expr ": ") + g_rccl.error_string(r_)); \
+    } while (0)
+
+static void comm_release(srbd_ctx* c) {
+    if (c->comm && g_rccl.comm_destroy) (void)g_rccl.comm_destroy(c->comm);
+    c->comm = nullptr;
+    (void)hipFree(c->d_myrec);
+    (void)hipFree(c->d_gath);
+    c->d_myrec = c->d_gath = nullptr;
+}
+
+extern "C" int srbd_comm_get_unique_id(const char* rccl_path, uint8_t* id_out) {
+    if (!id_out) return SRBD_E_INVALID;
+    if (!rccl_load(rccl_path)) return fail(nullptr, SRBD_E_STATE, g_rccl_err);
+    ncclUniqueId id;
+    const ncclResult_t r = g_rccl.get_unique_id(&id);
+    if (r != ncclSuccess) return fail(nullptr, SRBD_E_HIP, std::string("ncclGetUniqueId: ") + g_rccl.error_string(r));
+    memcpy(id_out, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return SRBD_OK;
+}
+
+extern "C" int srbd_comm_init(srbd_ctx* c, const char* rccl_path, const uint8_t* id_in) {
+    if (!c || !id_in) return SRBD_E_INVALID;
+    if (!rccl_load(rccl_path)) return fail(c, SRBD_E_STATE, g_rccl_err);
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    comm_release(c);
+    ncclUniqueId id;
+    memcpy(id.internal, id_in, NCCL_UNIQUE_ID_BYTES);
+    const int world = c->cfg.world_size > 0 ? c->cfg.world_size : 1;
+    RCCL_TRY(c, g_rccl.comm_init_rank(&c->comm, world, id, c->cfg.rank));
+    c->comm_world = world;
+    HIP_TRY(c, hipMalloc((void**)&c->d_myrec, sizeof(float) * c->rrec_stride));
+    HIP_TRY(c, hipMalloc((void**)&c->d_gath, sizeof(float) * (size_t)c->rrec_stride * world));
+    return SRBD_OK;
+}
+
+static int gather_records(srbd_ctx* c) {
+    if (!c->comm) return fail(c, SRBD_E_STATE, "srbd_comm_init first");
+    RCCL_TRY(c, g_rccl.all_gather(c->d_myrec, c->d_gath, (size_t)c->rrec_stride, ncclFloat32, c->comm, c->stream));
+    return SRBD_OK;
+}
+
+// One host-driven sharded step (Sampling_MPC call) with the exchange inside: the rank's rows,
+// ncclAllGather of the rank records, the merge; outputs identical on every rank.
+extern "C" int srbd_step_sharded(srbd_ctx* c, const float* state, const float* ref, const float* contact,
+                                 int32_t contact_stride, float* best, float* sigma, const float* noise_local,
+                                 uint64_t seed, uint64_t counter, srbd_result* out, float* out_costs_local) {
+    if (!c || !best) return SRBD_E_INVALID;
+    if (!c->comm) return fail(c, SRBD_E_STATE, "srbd_comm_init first");
+    int rc = srbd_step_local(c, state, ref, contact, contact_stride, best, sigma, noise_local, seed, counter,
+                             c->d_myrec);
+    if (rc) return rc;
+    if ((rc = gather_records(c))) return rc;
+    return srbd_step_finish(c, c->d_gath, c->comm_world, best, sigma, out, out_costs_local);
+}
+
+// `steps` device-resident sharded steps (warm start kept on the device), elapsed ms by hipEvents.
+extern "C" int srbd_sharded_device_steps(srbd_ctx* c, int32_t steps, float* elapsed_ms) {
+    if (!c || steps < 1) return SRBD_E_INVALID;
+    if (!c->comm) return fail(c, SRBD_E_STATE, "srbd_comm_init first");
+    hipEvent_t e0, e1;
+    HIP_TRY(c, hipEventCreate(&e0));
+    HIP_TRY(c, hipEventCreate(&e1));
+    HIP_TRY(c, hipEventRecord(e0, c->stream));
+    int rc = SRBD_OK;
+    for (int i = 0; i < steps && !rc; ++i) {
+        rc = srbd_device_step_local(c, c->d_myrec);
+        if (!rc) rc = gather_records(c);
+        if (!rc) rc = srbd_device_step_finish(c, c->d_gath, c->comm_world);
+    }
+    HIP_TRY(c, hipEventRecord(e1, c->stream));
+    HIP_TRY(c, hipEventSynchronize(e1));
+    float ms = 0.0f;
+    HIP_TRY(c, hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (elapsed_ms) *elapsed_ms = ms;
+    return rc;
 }
 
 // ------------------------------------------------------------------ measurement

@@ -85,6 +85,10 @@ SIGNATURES = {
     "srbd_copy_costs": (_I, [_P, _FP]),
     "srbd_selftest_div": (_I, [_FP, _FP, _I, _FP, _FP]),
     "srbd_debug_merge_phases": (_I, [_P, _I, _FP]),
+    "srbd_comm_get_unique_id": (_I, [C.c_char_p, _P]),
+    "srbd_comm_init": (_I, [_P, C.c_char_p, _P]),
+    "srbd_step_sharded": (_I, [_P, _P, _P, _P, _I, _P, _P, _P, C.c_uint64, C.c_uint64, C.POINTER(SrbdResult), _P]),
+    "srbd_sharded_device_steps": (_I, [_P, _I, _FP]),
     "srbd_tamols_create": (_I, [_I, C.POINTER(_P)]),
     "srbd_tamols_destroy": (None, [_P]),
     "srbd_tamols_last_error": (C.c_char_p, [_P]),
@@ -285,7 +289,7 @@ class Context:
     def check(self, rc, what):
         check(rc, self.h, what)
 
-    def step(self, state, ref, contact, best, sigma=None, noise=None, seed=42, counter=0, want_costs=False):
+    def _stage(self, state, ref, contact, best, sigma, noise):
         io, H = self._io, self.cfg.horizon
         io[:24] = np.reshape(state, 24)
         io[24:] = np.reshape(ref, 24)
@@ -304,13 +308,27 @@ class Context:
             if noise.shape != (self.n_local, self.P):
                 raise ValueError(f"noise must be ({self.n_local}, {self.P})")
             a_noise = noise.ctypes.data
+        return a_sigma, a_noise, noise
+
+    def _call_step(self, fn, name, state, ref, contact, best, sigma, noise, seed, counter, want_costs):
+        a_sigma, a_noise, _keep = self._stage(state, ref, contact, best, sigma, noise)
         res = SrbdResult()
         costs = np.empty(self.n_local, dtype=np.float32) if want_costs else None
-        rc = lib.srbd_step(self.h, self._a_state, self._a_ref, self._a_contact, H, self._a_best, a_sigma, a_noise,
-                           int(seed), int(counter), C.byref(res), None if costs is None else costs.ctypes.data)
-        self.check(rc, "srbd_step")
+        rc = fn(self.h, self._a_state, self._a_ref, self._a_contact, self.cfg.horizon, self._a_best, a_sigma, a_noise,
+                int(seed), int(counter), C.byref(res), None if costs is None else costs.ctypes.data)
+        self.check(rc, name)
         self.step_id += 1
         return self._best.copy(), (self._sigma.copy() if sigma is not None else None), res, costs
+
+    def step(self, state, ref, contact, best, sigma=None, noise=None, seed=42, counter=0, want_costs=False):
+        return self._call_step(lib.srbd_step, "srbd_step", state, ref, contact, best, sigma, noise, seed, counter,
+                               want_costs)
+
+    def step_sharded(self, state, ref, contact, best, sigma=None, noise_local=None, seed=42, counter=0,
+                     want_costs=False):
+        """srbd_step_sharded: this rank's rows, the RCCL all-gather and the merge in one call."""
+        return self._call_step(lib.srbd_step_sharded, "srbd_step_sharded", state, ref, contact, best, sigma,
+                               noise_local, seed, counter, want_costs)
 
     def copy_costs(self) -> np.ndarray:
         out = np.empty(self.n_local, dtype=np.float32)

@@ -1,7 +1,8 @@
 """The sharded driver (quadruped_pympc_amd.sharded) over a real RCCL group on one GPU.
 
-World size 1 (the box has one GPU; RCCL refuses two ranks on one device): the rank record
-goes through all_gather_into_tensor on torch's stream and srbd_step_finish merges it.  The
+World size 1 (the box has one GPU; RCCL refuses two ranks on one device), both transports: the
+library's own RCCL communicator (ncclAllGather issued from C++ on the context stream) and
+torch.distributed.all_gather_into_tensor on a torch stream shared with the library.  The
 result must match the unsharded srbd_step on the same noise to reduction-order tolerance, and
 the device-resident chain must run.  Multi-rank merging is covered on CPU with gloo
 (tests/test_distributed_gloo.py) and on this GPU with several contexts
@@ -17,7 +18,8 @@ from helpers import make_case, product_cfg
 pytestmark = pytest.mark.gpu
 
 
-def test_sharded_driver_world1_matches_step():
+@pytest.mark.parametrize("transport", ["rccl", "torch"])
+def test_sharded_driver_world1_matches_step(transport):
     import torch
     import torch.distributed as dist
 
@@ -39,7 +41,7 @@ def test_sharded_driver_world1_matches_step():
             b0, s0, r0, _ = ref.step(case["state"], case["ref"], case["contact"], case["best"], sigma=case["sigma"],
                                      noise=case["noise"])
             ref.close()
-            mpc = ShardedSamplingMPC(product_cfg(case), 0, 1, 0)
+            mpc = ShardedSamplingMPC(product_cfg(case), 0, 1, 0, transport=transport)
             b1, s1, r1 = mpc.step(case["state"], case["ref"], case["contact"], case["best"], sigma=case["sigma"],
                                   noise_local=case["noise"])
             assert r1.best_index == r0.best_index
@@ -49,10 +51,14 @@ def test_sharded_driver_world1_matches_step():
                 np.testing.assert_allclose(s1, s0, rtol=1e-5, atol=1e-6)
             # device-resident chain on the torch stream
             b2, _, _ = mpc.step(case["state"], case["ref"], case["contact"], b1, sigma=s1, seed=42, counter=5)
-            for _ in range(4):
-                mpc.device_step()
+            assert mpc.device_steps(4) > 0
             torch.cuda.synchronize()
             assert np.all(np.isfinite(b2))
+            # after a device chain, a host step still reproduces the unsharded step
+            b3, s3, r3 = mpc.step(case["state"], case["ref"], case["contact"], case["best"], sigma=case["sigma"],
+                                  noise_local=case["noise"])
+            assert r3.best_index == r0.best_index
+            np.testing.assert_allclose(b3, b0, rtol=1e-5, atol=1e-5)
             mpc.close()
     finally:
         dist.destroy_process_group()
