@@ -49,16 +49,22 @@ def roofline(w: Workload, n_local: int, kern: dict, traffic):
 
     Algorithmic bytes (SURVEY 8(d)): each noise row read once and one cost written, N*(4P+4);
     when the launch also draws the next step's noise (fused), + N*4P written.
+    Duration: HIP events around each launch on the context stream (kernel_us).  This agrees with
+    rocprofv3's kernel-trace average for the same kernel (profiles/).  event_floor_us (the same event
+    pair around an empty kernel) is reported beside it for reference and is NOT subtracted: it holds a
+    minimal kernel's own duration as well as dispatch.
     """
     P = w.num_params()
     fused = "fused_rollout_us" in kern
     us = kern["fused_rollout_us"] if fused else kern["rollout_us"]
+    floor = kern.get("event_floor_us", 0.0)
     algo = n_local * (4 * P + 4) + (n_local * 4 * P if fused else 0)
     achieved = algo / (us * 1e-6) / 1e9
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "kernel": "rollout_quad_kernel" + (" (+ next-step Philox blocks)" if fused else ""),
-            "kernel_us": round(us, 3), "algorithmic_bytes_per_launch": algo}
+            "kernel_us": round(us, 3), "event_floor_us": round(floor, 3),
+            "algorithmic_bytes_per_launch": algo}
 
 
 def pmc_traffic(workload_name: str):

@@ -132,9 +132,11 @@ int srbd_make_record_host(const srbd_config* cfg, int32_t rank, int32_t world_si
 int srbd_bench_device_steps(srbd_ctx* ctx, int32_t steps, float* elapsed_ms);
 /* Average per-launch duration (us) of each kernel of one step, hipEvents around every launch.
  * fused_rollout_us: the rollout launch that also draws the next step's noise (the form the step
- * chain runs when fusion applies; 0 otherwise).  Any out pointer may be NULL. */
+ * chain runs when fusion applies; 0 otherwise).  event_floor_us: the same event pair around an
+ * empty kernel (dispatch + kernel boundary; rocprof's kernel durations exclude it).  Any out
+ * pointer may be NULL. */
 int srbd_time_kernels(srbd_ctx* ctx, int32_t iters, float* rollout_us, float* rng_us, float* reduce_us,
-                      float* fused_rollout_us);
+                      float* fused_rollout_us, float* event_floor_us);
 
 /* Device-resident sharded chain (benchmark / pipelined callers): reuses the inputs of the last
  * srbd_step_local on the device.  srbd_device_step_local: RNG -> rollout -> rank record into d_record;
@@ -161,6 +163,23 @@ int srbd_step_sharded(srbd_ctx* ctx, const float* state, const float* ref, const
                       int32_t contact_stride, float* best_params, float* sigma, const float* noise_local,
                       uint64_t seed, uint64_t counter, srbd_result* out, float* out_costs_local);
 int srbd_sharded_device_steps(srbd_ctx* ctx, int32_t steps, float* elapsed_ms);
+
+/*
+ * xGMI exchange (no collective launch): the merge kernel stores its rank record straight into
+ * every rank's mailbox (uncached device memory, IPC-mapped over xGMI), sets per-rank epoch flags,
+ * waits (bounded, 2 s) for the W records in its own mailbox and merges them in the same launch.
+ * Once connected, srbd_step_sharded / srbd_sharded_device_steps use it instead of RCCL.
+ *   srbd_xgmi_export        : allocate this rank's mailbox, 64-byte IPC handle out
+ *   srbd_xgmi_connect       : world x 64 handle bytes in rank order (the caller all-gathers them)
+ *   srbd_xgmi_connect_local : every rank's context in this process (index r = rank r)
+ *   srbd_xgmi_probe         : one bounded round trip through the mailboxes (*ok = 1 on success)
+ *   srbd_xgmi_disconnect    : back to RCCL (srbd_comm_init) for later steps
+ */
+int srbd_xgmi_export(srbd_ctx* ctx, uint8_t* handle_out);
+int srbd_xgmi_connect(srbd_ctx* ctx, const uint8_t* handles);
+int srbd_xgmi_connect_local(srbd_ctx* const* ctxs, int32_t world);
+int srbd_xgmi_probe(srbd_ctx* ctx, int32_t* ok);
+int srbd_xgmi_disconnect(srbd_ctx* ctx);
 
 /* Diagnostic: mean duration (us) of the merge kernel's 5 phases (s_memrealtime stamps). */
 int srbd_debug_merge_phases(srbd_ctx* ctx, int32_t iters, float* out_us);

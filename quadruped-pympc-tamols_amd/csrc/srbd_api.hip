@@ -72,6 +72,16 @@ struct srbd_ctx {
     int comm_world = 0;
     float* d_myrec = nullptr;
     float* d_gath = nullptr;
+    // xGMI exchange (merge_xchg_kernel): this rank's mailbox (uncached device memory, IPC-exported),
+    // the peer table handed to the kernel, a device word pair {error, epoch counter}, the cached stage
+    // the second merge pass reads, and the two-step / one-step graphs of the device-resident chain.
+    float* xg_base = nullptr;
+    std::vector<void*> xg_opened;
+    XchgArgs xa{};
+    int xg_world = 0;
+    int* xg_err = nullptr;
+    float* xg_stage = nullptr;
+    hipGraphExec_t g_xg2 = nullptr, g_xg1 = nullptr;
     // Noise matrices, double buffered: the rollout launch of a step reading d_noise[cur] also draws the
     // predicted next step's noise (counter + 1) into the other buffer (MPPI / random sampling; CEM's
     // draws depend on the sigma the step produces).
@@ -327,6 +337,7 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
 }
 
 static void comm_release(srbd_ctx* c);
+static void xg_drop_graphs(srbd_ctx* c);
 
 extern "C" void srbd_destroy(srbd_ctx* c) {
     if (!c) return;
@@ -359,6 +370,7 @@ extern "C" int srbd_set_stream(srbd_ctx* c, void* s) {
     if (c->g_dev2) (void)hipGraphExecDestroy(c->g_dev2);
     if (c->g_dev1) (void)hipGraphExecDestroy(c->g_dev1);
     c->g_dev2 = c->g_dev1 = nullptr;
+    xg_drop_graphs(c);
     if (s) {
         c->stream = (hipStream_t)s;
         c->own_stream = false;
@@ -762,12 +774,28 @@ bool rccl_load(const char* path) {
         if (r_ != ncclSuccess) return fail((ctx), SRBD_E_HIP, std::string(#expr ": ") + g_rccl.error_string(r_)); \
     } while (0)
 
+static void xg_drop_graphs(srbd_ctx* c) {
+    if (c->g_xg2) (void)hipGraphExecDestroy(c->g_xg2);
+    if (c->g_xg1) (void)hipGraphExecDestroy(c->g_xg1);
+    c->g_xg2 = c->g_xg1 = nullptr;
+}
+
 static void comm_release(srbd_ctx* c) {
     if (c->comm && g_rccl.comm_destroy) (void)g_rccl.comm_destroy(c->comm);
     c->comm = nullptr;
     (void)hipFree(c->d_myrec);
     (void)hipFree(c->d_gath);
     c->d_myrec = c->d_gath = nullptr;
+    for (void* p : c->xg_opened) (void)hipIpcCloseMemHandle(p);
+    c->xg_opened.clear();
+    (void)hipFree(c->xg_base);
+    (void)hipFree(c->xg_err);
+    (void)hipFree(c->xg_stage);
+    c->xg_stage = nullptr;
+    xg_drop_graphs(c);
+    c->xg_base = nullptr;
+    c->xg_err = nullptr;
+    c->xg_world = 0;
 }
 
 extern "C" int srbd_comm_get_unique_id(const char* rccl_path, uint8_t* id_out) {
@@ -801,13 +829,218 @@ static int gather_records(srbd_ctx* c) {
     return SRBD_OK;
 }
 
-// One host-driven sharded step (Sampling_MPC call) with the exchange inside: the rank's rows,
-// ncclAllGather of the rank records, the merge; outputs identical on every rank.
+// ---- xGMI exchange: rank records stored straight into every rank's mailbox by the merge kernel
+static size_t xg_bytes(const srbd_ctx* c, int world) {
+    return ((sizeof(float) * (size_t)world * c->rrec_stride + sizeof(uint32_t) * world) + 255) / 256 * 256;
+}
+
+extern "C" int srbd_xgmi_export(srbd_ctx* c, uint8_t* handle_out) {
+    if (!c || !handle_out) return SRBD_E_INVALID;
+    const int world = c->cfg.world_size > 0 ? c->cfg.world_size : 1;
+    if (world > XCHG_MAX_WORLD) return fail(c, SRBD_E_INVALID, "xGMI exchange: world_size > 16");
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    if (!c->xg_base) {
+        const size_t bytes = xg_bytes(c, world);
+        HIP_TRY(c, hipExtMallocWithFlags((void**)&c->xg_base, bytes, hipDeviceMallocUncached));
+        HIP_TRY(c, hipMemset(c->xg_base, 0, bytes));
+        HIP_TRY(c, hipMalloc((void**)&c->xg_err, 2 * sizeof(int)));
+        HIP_TRY(c, hipMemset(c->xg_err, 0, 2 * sizeof(int)));
+        HIP_TRY(c, hipMalloc((void**)&c->xg_stage, sizeof(float) * (size_t)world * c->rrec_stride));
+    }
+    hipIpcMemHandle_t h;
+    HIP_TRY(c, hipIpcGetMemHandle(&h, c->xg_base));
+    memcpy(handle_out, &h, sizeof(h));
+    return SRBD_OK;
+}
+
+// Peer table + fresh epochs: the flags and the epoch counter restart at 0 on every rank (connect runs on
+// all ranks before any exchange kernel, so no peer is writing these words yet).
+static int xg_table(srbd_ctx* c, int world, float* const* bases) {
+    const size_t flag_off = (size_t)world * c->rrec_stride;
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemset(c->xg_base + flag_off, 0, sizeof(uint32_t) * world));
+    HIP_TRY(c, hipMemset(c->xg_err, 0, 2 * sizeof(int)));
+    HIP_TRY(c, hipDeviceSynchronize());
+    xg_drop_graphs(c);
+    c->xa = XchgArgs{};
+    c->xa.mailbox = c->xg_base;
+    c->xa.flags = reinterpret_cast<uint32_t*>(c->xg_base + flag_off);
+    for (int r = 0; r < world; ++r) {
+        c->xa.peer_mailbox[r] = bases[r];
+        c->xa.peer_flags[r] = reinterpret_cast<uint32_t*>(bases[r] + flag_off);
+    }
+    c->xa.err = c->xg_err;
+    c->xa.epoch = reinterpret_cast<uint32_t*>(c->xg_err + 1);
+    c->xa.stage = c->xg_stage;
+    c->xa.rank = c->cfg.rank;
+    c->xa.world = world;
+    c->xa.stride = c->rrec_stride;
+    c->xg_world = world;
+    return SRBD_OK;
+}
+
+// handles: world x 64 bytes in rank order (each rank's srbd_xgmi_export).
+extern "C" int srbd_xgmi_connect(srbd_ctx* c, const uint8_t* handles) {
+    if (!c || !handles) return SRBD_E_INVALID;
+    if (!c->xg_base) return fail(c, SRBD_E_STATE, "srbd_xgmi_export first");
+    const int world = c->cfg.world_size > 0 ? c->cfg.world_size : 1;
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    float* bases[XCHG_MAX_WORLD] = {};
+    for (int r = 0; r < world; ++r) {
+        if (r == c->cfg.rank) {
+            bases[r] = c->xg_base;
+            continue;
+        }
+        hipIpcMemHandle_t h;
+        memcpy(&h, handles + 64 * r, sizeof(h));
+        void* p = nullptr;
+        HIP_TRY(c, hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+        c->xg_opened.push_back(p);
+        bases[r] = static_cast<float*>(p);
+    }
+    return xg_table(c, world, bases);
+}
+
+// All ranks' contexts live in this process (tests, or one process driving several GPUs).
+extern "C" int srbd_xgmi_connect_local(srbd_ctx* const* ctxs, int32_t world) {
+    if (!ctxs || world < 1 || world > XCHG_MAX_WORLD) return SRBD_E_INVALID;
+    float* bases[XCHG_MAX_WORLD] = {};
+    for (int r = 0; r < world; ++r) {
+        if (!ctxs[r] || !ctxs[r]->xg_base || ctxs[r]->cfg.rank != r || ctxs[r]->cfg.world_size != world)
+            return fail(nullptr, SRBD_E_STATE, "every context must be srbd_xgmi_export'ed, rank r at index r");
+        bases[r] = ctxs[r]->xg_base;
+    }
+    for (int r = 0; r < world; ++r)
+        if (int rc = xg_table(ctxs[r], world, bases)) return rc;
+    return SRBD_OK;
+}
+
+// Exercise the mailboxes once (every rank must call it; bounded wait).  *ok = 1 when every peer's
+// word arrived.  The caller agrees across ranks and falls back to RCCL if any rank failed.
+extern "C" int srbd_xgmi_probe(srbd_ctx* c, int32_t* ok) {
+    if (!c || !ok) return SRBD_E_INVALID;
+    if (!c->xg_world) return fail(c, SRBD_E_STATE, "srbd_xgmi_connect first");
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    int* d_ok = nullptr;
+    HIP_TRY(c, hipMalloc((void**)&d_ok, sizeof(int)));
+    launch_xchg_probe(c->xa, d_ok, c->stream);
+    int h = 0;
+    hipError_t e = hipMemcpyAsync(&h, d_ok, sizeof(int), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d_ok);
+    HIP_TRY(c, e);
+    *ok = h;
+    return SRBD_OK;
+}
+
+extern "C" int srbd_xgmi_disconnect(srbd_ctx* c) {
+    if (!c) return SRBD_E_INVALID;
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (void* p : c->xg_opened) (void)hipIpcCloseMemHandle(p);
+    c->xg_opened.clear();
+    c->xg_world = 0;
+    xg_drop_graphs(c);
+    return SRBD_OK;
+}
+
+// rollout (+ next draws) -> merge_xchg (rank record out to every mailbox, wait, merge the W records)
+static void enqueue_xchg_step(srbd_ctx* c, int buf, StepOutput* out, int chain, bool fuse_next, Publish pub) {
+    const ModelConst& mc = c->mc;
+    const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1};
+    launch_rollout(mc, c->d_in, c->d_noise[buf], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
+                   c->stream, fuse_next ? &next : nullptr);
+    launch_merge_xchg(mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, c->d_noise[buf], c->xa, out, chain,
+                      c->stream, 1, pub);
+}
+
+// Device-resident exchange chain as replayed graphs (the epoch lives on the device, so a replay is a
+// valid next exchange): two steps per graph alternating the noise buffers when the next draws fuse
+// into the rollout launch, one-step graph for an odd count.
+static int xg_capture(srbd_ctx* c) {
+    const bool fuse = fusable(c);
+    hipGraph_t g;
+    HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    for (int half = 0; half < 2; ++half) {
+        if (!fuse) launch_rng(c->mc, c->d_in, 0, 0, 1, 0, c->d_noise[0], c->stream);
+        enqueue_xchg_step(c, fuse ? half : 0, c->d_out, 1, fuse, Publish{nullptr, 0});
+    }
+    HIP_TRY(c, hipStreamEndCapture(c->stream, &g));
+    hipError_t e = hipGraphInstantiate(&c->g_xg2, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    HIP_TRY(c, e);
+    HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    if (!fuse) launch_rng(c->mc, c->d_in, 0, 0, 1, 0, c->d_noise[0], c->stream);
+    enqueue_xchg_step(c, 0, c->d_out, 1, fuse, Publish{nullptr, 0});
+    HIP_TRY(c, hipStreamEndCapture(c->stream, &g));
+    e = hipGraphInstantiate(&c->g_xg1, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    HIP_TRY(c, e);
+    return SRBD_OK;
+}
+
+static int xg_device_steps(srbd_ctx* c, int steps) {
+    int rc;
+    if (!c->g_xg2 && (rc = xg_capture(c))) return rc;
+    c->pref_valid = false;
+    if ((rc = reset_noise_scaled(c))) return rc;
+    if (fusable(c)) launch_rng(c->mc, c->d_in, 0, 0, 1, 0, c->d_noise[0], c->stream);  // first step's draws
+    for (int i = 0; i < steps / 2; ++i) HIP_TRY(c, hipGraphLaunch(c->g_xg2, c->stream));
+    if (steps & 1) HIP_TRY(c, hipGraphLaunch(c->g_xg1, c->stream));
+    c->cur = 0;
+    return SRBD_OK;
+}
+
+static int xg_check_err(srbd_ctx* c) {
+    int e = 0;
+    HIP_TRY(c, hipMemcpy(&e, c->xg_err, sizeof(int), hipMemcpyDeviceToHost));
+    return e ? fail(c, SRBD_E_HIP, "xGMI exchange timed out waiting for a peer's record") : SRBD_OK;
+}
+
+static int xg_step(srbd_ctx* c, const float* state, const float* ref, const float* contact, int32_t contact_stride,
+                   float* best, float* sigma, const float* noise_local, uint64_t seed, uint64_t counter,
+                   srbd_result* out, float* out_costs_local) {
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    int rc = fill_input(&c->cfg, c->mc, c->h_in, state, ref, contact, contact_stride, best, sigma, seed, counter);
+    if (rc) return fail(c, rc, "invalid step arguments");
+    c->h_in->noise_scaled = noise_local ? 1 : 0;
+    HIP_TRY(c, hipMemcpyAsync(c->d_in, c->h_in, sizeof(StepInput), hipMemcpyHostToDevice, c->stream));
+    int buf = 0;
+    if ((rc = acquire_noise(c, noise_local, seed, counter, &buf))) return rc;
+    const bool fuse = !noise_local && fusable(c);
+    const Publish pub{c->d_flag, ++c->seq};
+    enqueue_xchg_step(c, buf, c->d_out_host, 0, fuse, pub);
+    HIP_TRY(c, hipGetLastError());
+    if (fuse) {
+        c->pref_valid = true;
+        c->pref_buf = 1 - buf;
+        c->pref_seed = seed;
+        c->pref_ctr = counter + 1;
+    }
+    c->chain_started = false;
+    c->input_ready = true;
+    if ((rc = wait_published(c, pub.seq))) return rc;
+    if (c->h_out->status != 0) return xg_check_err(c) ? SRBD_E_HIP : fail(c, SRBD_E_HIP, "exchange step failed");
+    if (out_costs_local) {
+        HIP_TRY(c, hipMemcpyAsync(out_costs_local, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,
+                                  c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+    return copy_out(c, best, sigma, out);
+}
+
+// One host-driven sharded step (Sampling_MPC call) with the exchange inside: the rank's rows, the
+// rank records exchanged (xGMI mailboxes when connected, else ncclAllGather), the merge; outputs
+// identical on every rank.
 extern "C" int srbd_step_sharded(srbd_ctx* c, const float* state, const float* ref, const float* contact,
                                  int32_t contact_stride, float* best, float* sigma, const float* noise_local,
                                  uint64_t seed, uint64_t counter, srbd_result* out, float* out_costs_local) {
     if (!c || !best) return SRBD_E_INVALID;
-    if (!c->comm) return fail(c, SRBD_E_STATE, "srbd_comm_init first");
+    if (c->xg_world)
+        return xg_step(c, state, ref, contact, contact_stride, best, sigma, noise_local, seed, counter, out,
+                       out_costs_local);
+    if (!c->comm) return fail(c, SRBD_E_STATE, "srbd_comm_init or srbd_xgmi_connect first");
     int rc = srbd_step_local(c, state, ref, contact, contact_stride, best, sigma, noise_local, seed, counter,
                              c->d_myrec);
     if (rc) return rc;
@@ -818,16 +1051,22 @@ extern "C" int srbd_step_sharded(srbd_ctx* c, const float* state, const float* r
 // `steps` device-resident sharded steps (warm start kept on the device), elapsed ms by hipEvents.
 extern "C" int srbd_sharded_device_steps(srbd_ctx* c, int32_t steps, float* elapsed_ms) {
     if (!c || steps < 1) return SRBD_E_INVALID;
-    if (!c->comm) return fail(c, SRBD_E_STATE, "srbd_comm_init first");
+    if (!c->xg_world && !c->comm) return fail(c, SRBD_E_STATE, "srbd_comm_init or srbd_xgmi_connect first");
+    if (!c->input_ready) return fail(c, SRBD_E_STATE, "run a host step first");
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     hipEvent_t e0, e1;
     HIP_TRY(c, hipEventCreate(&e0));
     HIP_TRY(c, hipEventCreate(&e1));
     HIP_TRY(c, hipEventRecord(e0, c->stream));
     int rc = SRBD_OK;
-    for (int i = 0; i < steps && !rc; ++i) {
-        rc = srbd_device_step_local(c, c->d_myrec);
-        if (!rc) rc = gather_records(c);
-        if (!rc) rc = srbd_device_step_finish(c, c->d_gath, c->comm_world);
+    if (c->xg_world) {
+        rc = xg_device_steps(c, steps);
+    } else {
+        for (int i = 0; i < steps && !rc; ++i) {
+            rc = srbd_device_step_local(c, c->d_myrec);
+            if (!rc) rc = gather_records(c);
+            if (!rc) rc = srbd_device_step_finish(c, c->d_gath, c->comm_world);
+        }
     }
     HIP_TRY(c, hipEventRecord(e1, c->stream));
     HIP_TRY(c, hipEventSynchronize(e1));
@@ -836,6 +1075,7 @@ extern "C" int srbd_sharded_device_steps(srbd_ctx* c, int32_t steps, float* elap
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     if (elapsed_ms) *elapsed_ms = ms;
+    if (!rc && c->xg_world) rc = xg_check_err(c);
     return rc;
 }
 
@@ -892,7 +1132,7 @@ extern "C" int srbd_bench_device_steps(srbd_ctx* c, int32_t steps, float* ms) {
 }
 
 extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, float* rng_us, float* reduce_us,
-                                 float* fused_us) {
+                                 float* fused_us, float* floor_us) {
     if (!c || iters < 1) return SRBD_E_INVALID;
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step once before timing");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
@@ -941,7 +1181,21 @@ extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, 
             f += t;
         }
     }
+    // event floor: the same event pair around an empty kernel (dispatch + boundary, no work)
+    double fl = 0;
+    for (int i = 0; i < iters; ++i) {
+        HIP_TRY(c, hipEventRecord(ev[4 * i], c->stream));
+        launch_empty(c->stream);
+        HIP_TRY(c, hipEventRecord(ev[4 * i + 1], c->stream));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < iters; ++i) {
+        float t;
+        HIP_TRY(c, hipEventElapsedTime(&t, ev[4 * i], ev[4 * i + 1]));
+        fl += t;
+    }
     for (auto& e : ev) (void)hipEventDestroy(e);
+    if (floor_us) *floor_us = (float)(fl * 1000.0 / iters);
     if (fused_us) *fused_us = (float)(f * 1000.0 / iters);
     if (rng_us) *rng_us = (float)(a * 1000.0 / iters);
     if (rollout_us) *rollout_us = (float)(b * 1000.0 / iters);

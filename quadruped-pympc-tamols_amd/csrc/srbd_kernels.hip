@@ -629,14 +629,11 @@ __device__ __forceinline__ void block_topk(const float* __restrict__ recs, int n
 //  4. top-K keys: per-thread sorted lists -> per-wave K-round DPP minima -> one wave over the 16
 //     wave lists; 5. elite rows -> LDS;  6. outputs: rank record and/or final step outputs; with
 //     `chain` the new parameters, sigma and RNG counter are written back into `in` (warm start).
-__global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst mc, StepInput* __restrict__ in,
-                                                              const float* __restrict__ recs, int nrec,
-                                                              int rec_stride, int rows_in_rec,
-                                                              const float* __restrict__ noise,
-                                                              float* __restrict__ rank_out,
-                                                              StepOutput* __restrict__ out, int chain,
-                                                              int ctr_inc, uint64_t* __restrict__ dbg,
-                                                              uint32_t* __restrict__ flag, uint32_t seq) {
+__device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __restrict__ in,
+                                           const float* __restrict__ recs, int nrec, int rec_stride, int rows_in_rec,
+                                           const float* __restrict__ noise, float* __restrict__ rank_out,
+                                           StepOutput* __restrict__ out, int chain, int ctr_inc,
+                                           uint64_t* __restrict__ dbg, uint32_t* __restrict__ flag, uint32_t seq) {
     extern __shared__ float smem[];  // scale[nrec_pad] | part[G*(P+1)] | erow[K*P]
     __shared__ uint64_t red[MERGE_WAVES];
     __shared__ uint64_t wlist[MERGE_WAVES][MAXK];
@@ -881,6 +878,81 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst m
     }
 }
 
+__global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst mc, StepInput* __restrict__ in,
+                                                              const float* __restrict__ recs, int nrec,
+                                                              int rec_stride, int rows_in_rec,
+                                                              const float* __restrict__ noise,
+                                                              float* __restrict__ rank_out,
+                                                              StepOutput* __restrict__ out, int chain,
+                                                              int ctr_inc, uint64_t* __restrict__ dbg,
+                                                              uint32_t* __restrict__ flag, uint32_t seq) {
+    merge_body(mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag, seq);
+}
+
+// Sharded step without a collective launch (xGMI exchange): pass 1 merges this rank's block records
+// into its rank record, stored straight into slot `rank` of every rank's mailbox (peer mailboxes are
+// IPC-mapped over xGMI; mailboxes are uncached device memory, so no cache holds a stale slot); after
+// a system-scope fence each peer's flag for this rank is set to the next epoch (*x.epoch + 1).  The block then waits for
+// all W flags of its own mailbox (bounded: on timeout it records an error and skips the outputs) and
+// pass 2 merges the W rank records in rank order, exactly as srbd_step_finish does.
+__global__ void __launch_bounds__(MERGE_THREADS) merge_xchg_kernel(const ModelConst mc, StepInput* __restrict__ in,
+                                                                   const float* __restrict__ recs, int nrec,
+                                                                   int rec_stride, const float* __restrict__ noise,
+                                                                   XchgArgs x, StepOutput* __restrict__ out,
+                                                                   int chain, int ctr_inc, uint32_t* __restrict__ flag,
+                                                                   uint32_t seq) {
+    const int tid = threadIdx.x, T = blockDim.x;
+    const int stride = rec_floats_rank(mc.P, mc.K);
+    const uint32_t epoch = *x.epoch + 1;  // read by every thread before the first barrier
+    // own record: cached staging slot; peers get it by direct stores into their (uncached) mailboxes
+    float* mine = x.stage + (size_t)x.rank * stride;
+    merge_body(mc, in, recs, nrec, rec_stride, 0, noise, mine, nullptr, 0, 0, nullptr, nullptr, 0);
+    __threadfence();
+    __syncthreads();
+    for (int i = tid; i < (x.world - 1) * stride; i += T) {
+        const int q = i / stride, k = i - q * stride;
+        const int p = q < x.rank ? q : q + 1;
+        x.peer_mailbox[p][(size_t)x.rank * stride + k] = mine[k];
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (tid < x.world && tid != x.rank)
+        __hip_atomic_store(x.peer_flags[tid] + x.rank, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __shared__ int timed_out;
+    if (tid == 0) timed_out = 0;
+    __syncthreads();
+    if (tid < x.world && tid != x.rank) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(x.flags + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > XCHG_TIMEOUT_TICKS) {
+                timed_out = 1;
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    if (tid == 0) *x.epoch = epoch;
+    if (timed_out) {
+        if (tid == 0) {
+            *x.err = 1;
+            if (out) out->status = -1;
+            __threadfence_system();  // status (and err) visible before the host sees the flag
+            if (flag) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+    }
+    // peers' records: one parallel pass of uncached reads into the cached stage, then merge from there
+    for (int i = tid; i < (x.world - 1) * stride; i += T) {
+        const int q = i / stride, k = i - q * stride;
+        const size_t o = (size_t)(q < x.rank ? q : q + 1) * stride + k;
+        x.stage[o] = x.mailbox[o];
+    }
+    __syncthreads();
+    merge_body(mc, in, x.stage, x.world, stride, 1, noise, nullptr, out, chain, ctr_inc, nullptr, flag, seq);
+}
+
 __global__ void advance_kernel(const ModelConst mc, StepInput* __restrict__ in, const StepOutput* __restrict__ out) {
     for (int j = threadIdx.x; j < mc.P; j += blockDim.x) {
         in->best[j] = out->best[j];
@@ -992,6 +1064,50 @@ void launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nr
                        pub.seq);
 }
 
+// Setup probe of the xGMI mailboxes: slot `rank` word 0 of every mailbox <- rank, flags <- epoch;
+// then every slot of the local mailbox must hold its rank.  ok[0] = 1 on success.
+__global__ void xchg_probe_kernel(XchgArgs x, int* ok) {
+    const int tid = threadIdx.x;
+    const uint32_t epoch = *x.epoch + 1;
+    if (tid < x.world) x.peer_mailbox[tid][(size_t)x.rank * x.stride] = (float)x.rank;
+    __threadfence_system();
+    __syncthreads();
+    if (tid < x.world)
+        __hip_atomic_store(x.peer_flags[tid] + x.rank, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __shared__ int bad;
+    if (tid == 0) bad = 0;
+    __syncthreads();
+    if (tid < x.world) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        bool seen = false;
+        while (!(seen = __hip_atomic_load(x.flags + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == epoch)) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > XCHG_TIMEOUT_TICKS) break;
+        }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        if (!seen || x.mailbox[(size_t)tid * x.stride] != (float)tid) bad = 1;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        *ok = bad ? 0 : 1;
+        *x.epoch = epoch;
+    }
+}
+
+void launch_xchg_probe(const XchgArgs& x, int* ok, hipStream_t s) {
+    hipLaunchKernelGGL(xchg_probe_kernel, dim3(1), dim3(64), 0, s, x, ok);
+}
+
+void launch_merge_xchg(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
+                       const float* noise, const XchgArgs& x, StepOutput* out, int chain, hipStream_t s, int ctr_inc,
+                       Publish pub) {
+    size_t smem = merge_smem_bytes(nrec, mc.P, mc.K);
+    const size_t smem2 = merge_smem_bytes(x.world, mc.P, mc.K);
+    smem = smem > smem2 ? smem : smem2;
+    hipLaunchKernelGGL(merge_xchg_kernel, dim3(1), dim3(MERGE_THREADS), smem, s, mc, in, recs, nrec, rec_stride, noise,
+                       x, out, chain, chain ? ctr_inc : 0, pub.flag, pub.seq);
+}
+
 int tune_knob(const char* name, int dflt) {
     const char* e = getenv(name);
     return (e && atoi(e) > 0) ? atoi(e) : dflt;
@@ -1020,6 +1136,9 @@ void launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, i
     launch_merge(mc, in, partials, m, rec_floats_rank(mc.P, mc.K), 1, noise, rank_out, out, chain, s, nullptr, ctr_inc,
                  pub);
 }
+
+__global__ void empty_kernel() {}
+void launch_empty(hipStream_t s) { hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s); }
 
 void launch_advance(const ModelConst& mc, StepInput* in, const StepOutput* out, hipStream_t s) {
     hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(256), 0, s, mc, in, out);

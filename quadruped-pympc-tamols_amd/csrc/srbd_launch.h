@@ -45,12 +45,33 @@ constexpr int MERGE_DIRECT_MAX = 256;
 constexpr int MERGE_PER_BLOCK = 32;
 constexpr int MERGE_MAX_PARTIALS = 64;
 int merge_partials(int nrec);
+// xGMI exchange of rank records (merge_xchg_kernel).  mailbox: this rank's W slots of one rank
+// record each; flags: W epochs (slot r written by rank r); peer_*: every rank's mailbox / flags as
+// this GPU addresses them (IPC-mapped; entry `rank` is the local one).  epoch: this rank's exchange
+// counter in device memory, advanced by every exchange kernel (so the chain can be a replayed graph).
+constexpr int XCHG_MAX_WORLD = 16;
+constexpr uint64_t XCHG_TIMEOUT_TICKS = 200000000ull;  // 2 s at the 100 MHz s_memrealtime clock
+struct XchgArgs {
+    float* mailbox;
+    uint32_t* flags;
+    float* peer_mailbox[XCHG_MAX_WORLD];
+    uint32_t* peer_flags[XCHG_MAX_WORLD];
+    float* stage;  // cached world x stride copy the second merge pass reads (mailbox is uncached)
+    int* err;
+    uint32_t* epoch;
+    int rank, world, stride;  // stride: floats per mailbox slot (one rank record)
+};
+void launch_xchg_probe(const XchgArgs& x, int* ok, hipStream_t s);
+void launch_merge_xchg(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
+                       const float* noise, const XchgArgs& x, StepOutput* out, int chain, hipStream_t s, int ctr_inc,
+                       Publish pub);
 // Integer tuning knob from the environment (read once), else `dflt`.
 int tune_knob(const char* name, int dflt);
 void launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                        const float* noise, float* partials, float* rank_out, StepOutput* out, int chain,
                        hipStream_t s, int ctr_inc = 1, Publish pub = {nullptr, 0});
 void launch_advance(const ModelConst& mc, StepInput* in, const StepOutput* out, hipStream_t s);
+void launch_empty(hipStream_t s);  // measurement: the event floor
 void launch_div_selftest(const float* a, const float* b, int n, float* o, hipStream_t s);
 
 // TAMOLS (tamols_kernel.hip)

@@ -78,7 +78,7 @@ SIGNATURES = {
     "srbd_finish_host": (_I, [C.POINTER(SrbdConfig), _FP, _I, _FP, _FP, _I, _FP, _FP, C.POINTER(SrbdResult)]),
     "srbd_make_record_host": (_I, [C.POINTER(SrbdConfig), _I, _I, _FP, _FP, _FP]),
     "srbd_bench_device_steps": (_I, [_P, _I, _FP]),
-    "srbd_time_kernels": (_I, [_P, _I, _FP, _FP, _FP, _FP]),
+    "srbd_time_kernels": (_I, [_P, _I, _FP, _FP, _FP, _FP, _FP]),
     "srbd_device_step_local": (_I, [_P, _P]),
     "srbd_device_step_finish": (_I, [_P, _P, _I]),
     "srbd_sync_result": (_I, [_P, _FP, _FP, C.POINTER(SrbdResult)]),
@@ -89,6 +89,11 @@ SIGNATURES = {
     "srbd_comm_init": (_I, [_P, C.c_char_p, _P]),
     "srbd_step_sharded": (_I, [_P, _P, _P, _P, _I, _P, _P, _P, C.c_uint64, C.c_uint64, C.POINTER(SrbdResult), _P]),
     "srbd_sharded_device_steps": (_I, [_P, _I, _FP]),
+    "srbd_xgmi_export": (_I, [_P, _P]),
+    "srbd_xgmi_connect": (_I, [_P, _P]),
+    "srbd_xgmi_connect_local": (_I, [_P, _I]),
+    "srbd_xgmi_probe": (_I, [_P, _IP]),
+    "srbd_xgmi_disconnect": (_I, [_P]),
     "srbd_tamols_create": (_I, [_I, C.POINTER(_P)]),
     "srbd_tamols_destroy": (None, [_P]),
     "srbd_tamols_last_error": (C.c_char_p, [_P]),
@@ -326,7 +331,7 @@ class Context:
 
     def step_sharded(self, state, ref, contact, best, sigma=None, noise_local=None, seed=42, counter=0,
                      want_costs=False):
-        """srbd_step_sharded: this rank's rows, the RCCL all-gather and the merge in one call."""
+        """srbd_step_sharded: this rank's rows, the record exchange (xGMI mailboxes or RCCL) and the merge."""
         return self._call_step(lib.srbd_step_sharded, "srbd_step_sharded", state, ref, contact, best, sigma,
                                noise_local, seed, counter, want_costs)
 
@@ -341,10 +346,10 @@ class Context:
         return float(ms.value)
 
     def time_kernels(self, iters: int):
-        r, g, m, f = _F(0), _F(0), _F(0), _F(0)
-        self.check(lib.srbd_time_kernels(self.h, int(iters), C.byref(r), C.byref(g), C.byref(m), C.byref(f)),
-                   "srbd_time_kernels")
-        out = {"rollout_us": r.value, "rng_us": g.value, "merge_us": m.value}
+        r, g, m, f, fl = _F(0), _F(0), _F(0), _F(0), _F(0)
+        self.check(lib.srbd_time_kernels(self.h, int(iters), C.byref(r), C.byref(g), C.byref(m), C.byref(f),
+                                         C.byref(fl)), "srbd_time_kernels")
+        out = {"rollout_us": r.value, "rng_us": g.value, "merge_us": m.value, "event_floor_us": fl.value}
         if f.value > 0:  # rollout launch carrying the next step's draws (what the step chain runs)
             out["fused_rollout_us"] = f.value
         return out

@@ -20,7 +20,56 @@ from quadruped_pympc_amd.sharded import ShardedSamplingMPC  # noqa: E402
 from quadruped_pympc_amd.synthetic import CONFIGS, inputs  # noqa: E402
 
 
+def local_pair(steps=2000):
+    """W=2 ranks as two contexts on this one GPU, connected in-process, device chains run from two
+    threads: the exchange protocol's per-step cost (both ranks share the GPU's CUs)."""
+    import ctypes as C
+    import threading
+
+    from quadruped_pympc_amd import _lib
+
+    w = CONFIGS["c2"]
+    ctxs = [_lib.Context(make_cfg(w, 2 * w.num_samples, r, 2, 0)) for r in range(2)]
+    for cx in ctxs:
+        cx.check(_lib.lib.srbd_xgmi_export(cx.h, (C.c_uint8 * 64)()), "export")
+    arr = (C.c_void_p * 2)(*[cx.h.value for cx in ctxs])
+    assert _lib.lib.srbd_xgmi_connect_local(arr, 2) == 0
+    ms = [0.0, 0.0]
+    st, ref, con = inputs(w, 0)
+
+    def host(i):
+        b = np.zeros(ctxs[i].P, np.float32)
+        ctxs[i].step_sharded(st, ref, con, b, seed=42, counter=0)
+
+    hs = [threading.Thread(target=host, args=(i,)) for i in range(2)]
+    for t in hs:
+        t.start()
+    for t in hs:
+        t.join()
+
+    def run(i, n):
+        v = C.c_float(0)
+        ctxs[i].check(_lib.lib.srbd_sharded_device_steps(ctxs[i].h, n, C.byref(v)), "steps")
+        ms[i] = v.value
+
+    for n in (50, steps):
+        ts = [threading.Thread(target=run, args=(i, n)) for i in range(2)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        wall = time.perf_counter() - t0
+    for cx in ctxs:
+        cx.close()
+    print(json.dumps({"transport": "xgmi_local_w2", "rows_per_rank": w.num_samples,
+                      "device_chain_us_per_step": round(1e6 * wall / steps, 2),
+                      "event_ms_per_rank": [round(m, 3) for m in ms]}))
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "local2":
+        return local_pair()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]

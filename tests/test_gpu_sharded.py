@@ -18,7 +18,7 @@ from helpers import make_case, product_cfg
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("transport", ["rccl", "torch"])
+@pytest.mark.parametrize("transport", ["auto", "xgmi", "rccl", "torch"])
 def test_sharded_driver_world1_matches_step(transport):
     import torch
     import torch.distributed as dist
@@ -42,6 +42,8 @@ def test_sharded_driver_world1_matches_step(transport):
                                      noise=case["noise"])
             ref.close()
             mpc = ShardedSamplingMPC(product_cfg(case), 0, 1, 0, transport=transport)
+            if transport == "auto":
+                assert mpc.transport == "xgmi"
             b1, s1, r1 = mpc.step(case["state"], case["ref"], case["contact"], case["best"], sigma=case["sigma"],
                                   noise_local=case["noise"])
             assert r1.best_index == r0.best_index

@@ -1,0 +1,31 @@
+"""xGMI mailbox exchange (merge_xchg_kernel) with W ranks as W contexts on one GPU.
+
+The box has one GPU, so the peers' mailboxes are connected in-process (srbd_xgmi_connect_local:
+the same kernel, device pointers instead of IPC-mapped ones).  The scenarios run in one worker
+process (tests/xgmi_worker.py, see its docstring for why): the merged step must equal the unsharded
+step (to reduction-order tolerance) and be bit-identical on every rank, across host steps and the
+replayed device chain; a rank whose peer never arrives must fail after the bounded wait.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def worker_results():
+    p = subprocess.run([sys.executable, os.path.join(HERE, "xgmi_worker.py")], capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("case", ["mppi", "cem_mppi", "random_sampling", "mppi_w3", "timeout"])
+def test_xgmi_exchange_in_process(worker_results, case):
+    assert worker_results[case] == "ok", worker_results[case]
