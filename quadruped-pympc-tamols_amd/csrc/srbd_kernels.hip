@@ -872,9 +872,13 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     MERGE_STAMP(5);
 #undef MERGE_STAMP
     if (flag) {  // every thread's output writes reach the system before thread 0 publishes `seq`
-        __threadfence_system();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tid == 0) {
+            __threadfence_system();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -889,12 +893,18 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst m
     merge_body(mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag, seq);
 }
 
-// Sharded step without a collective launch (xGMI exchange): pass 1 merges this rank's block records
-// into its rank record, stored straight into slot `rank` of every rank's mailbox (peer mailboxes are
-// IPC-mapped over xGMI; mailboxes are uncached device memory, so no cache holds a stale slot); after
-// a system-scope fence each peer's flag for this rank is set to the next epoch (*x.epoch + 1).  The block then waits for
-// all W flags of its own mailbox (bounded: on timeout it records an error and skips the outputs) and
-// pass 2 merges the W rank records in rank order, exactly as srbd_step_finish does.
+// Sharded step without a collective launch (xGMI exchange).
+//  1. pass 1 merges this rank's block records into its rank record (a cached stage slot);
+//  2. the record goes to slot `rank` of every peer's mailbox as system-scope (sc0 sc1, write-through)
+//     stores; every storing wave waits for its stores (vmcnt 0), then after a block barrier one lane
+//     per peer makes a system release and sets that peer's flag for this rank to the next epoch
+//     (*x.epoch + 1; mailboxes are uncached device memory, IPC-mapped over xGMI);
+//  3. the block waits for the W-1 flags of its own mailbox (bounded: on timeout it records an error,
+//     publishes a failed status and skips the outputs), copies the peers' slots into the stage with
+//     system-scope loads (one parallel round trip; nothing is read from a cache) and
+//  4. pass 2 merges the W rank records in rank order, exactly as srbd_step_finish does.
+// Costs (MI355X, one rank): all-thread agent + system fences and a system acquire here cost 7 us per
+// step; this form measures within noise of no release at all (scripts/sharded_probe.py).
 __global__ void __launch_bounds__(MERGE_THREADS) merge_xchg_kernel(const ModelConst mc, StepInput* __restrict__ in,
                                                                    const float* __restrict__ recs, int nrec,
                                                                    int rec_stride, const float* __restrict__ noise,
@@ -903,21 +913,23 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_xchg_kernel(const ModelCo
                                                                    uint32_t seq) {
     const int tid = threadIdx.x, T = blockDim.x;
     const int stride = rec_floats_rank(mc.P, mc.K);
-    const uint32_t epoch = *x.epoch + 1;  // read by every thread before the first barrier
-    // own record: cached staging slot; peers get it by direct stores into their (uncached) mailboxes
+    const uint32_t epoch = *x.epoch + 1;
     float* mine = x.stage + (size_t)x.rank * stride;
     merge_body(mc, in, recs, nrec, rec_stride, 0, noise, mine, nullptr, 0, 0, nullptr, nullptr, 0);
-    __threadfence();
     __syncthreads();
     for (int i = tid; i < (x.world - 1) * stride; i += T) {
         const int q = i / stride, k = i - q * stride;
         const int p = q < x.rank ? q : q + 1;
-        x.peer_mailbox[p][(size_t)x.rank * stride + k] = mine[k];
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(x.peer_mailbox[p]) + (size_t)x.rank * stride + k,
+                           __float_as_uint(mine[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    __threadfence_system();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid < x.world && tid != x.rank)
+    if (tid < x.world && tid != x.rank) {
+        __threadfence_system();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(x.peer_flags[tid] + x.rank, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     __shared__ int timed_out;
     if (tid == 0) timed_out = 0;
     __syncthreads();
@@ -932,22 +944,21 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_xchg_kernel(const ModelCo
         }
     }
     __syncthreads();
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);
     if (tid == 0) *x.epoch = epoch;
     if (timed_out) {
         if (tid == 0) {
             *x.err = 1;
             if (out) out->status = -1;
-            __threadfence_system();  // status (and err) visible before the host sees the flag
+            __threadfence_system();
             if (flag) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         return;
     }
-    // peers' records: one parallel pass of uncached reads into the cached stage, then merge from there
     for (int i = tid; i < (x.world - 1) * stride; i += T) {
         const int q = i / stride, k = i - q * stride;
         const size_t o = (size_t)(q < x.rank ? q : q + 1) * stride + k;
-        x.stage[o] = x.mailbox[o];
+        x.stage[o] = __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(x.mailbox) + o,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     }
     __syncthreads();
     merge_body(mc, in, x.stage, x.world, stride, 1, noise, nullptr, out, chain, ctr_inc, nullptr, flag, seq);

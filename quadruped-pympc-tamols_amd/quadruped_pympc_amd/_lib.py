@@ -102,7 +102,7 @@ SIGNATURES = {
 }
 
 LIB_NAME = "libsrbd_hip.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+LIB_PATH = os.environ.get("SRBD_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 
 def _load():
