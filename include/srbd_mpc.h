@@ -36,6 +36,7 @@ extern "C" {
 #define SRBD_MAX_HORIZON 32
 #define SRBD_MAX_PARAMS 384
 #define SRBD_MAX_ELITE 16
+#define SRBD_MAX_FREQS 8 /* candidate step frequencies of the gait-adaptive sampler */
 
 enum {
     SRBD_OK = 0,
@@ -78,7 +79,8 @@ typedef struct srbd_result {
     float best_cost;           /* saturated cost of the best sample */
     int32_t best_index;        /* global row of the best sample (nanargmin, first on ties) */
     int32_t status;
-    int32_t _pad;
+    float best_freq;           /* gait-adaptive: step frequency of the best sample (best_step_frequency,
+                                  centroidal_nmpc_jax_gait_adaptive.py:705,861); 0 otherwise */
 } srbd_result;
 
 typedef struct srbd_ctx srbd_ctx;
@@ -108,6 +110,30 @@ int srbd_set_stream(srbd_ctx* ctx, void* hip_stream);
 int srbd_step(srbd_ctx* ctx, const float* state, const float* ref, const float* contact, int32_t contact_stride,
               float* best_params, float* sigma, const float* noise, uint64_t seed, uint64_t counter,
               srbd_result* out, float* out_costs);
+
+/*
+ * Gait-adaptive sampling (centroidal_nmpc_jax_gait_adaptive.py; replaces
+ * compute_rollout :326-501 and the step-frequency draws :687-692 (random sampling), :834-838
+ * (MPPI)).  After this call every step of the context (srbd_step, the sharded and device-resident
+ * forms) samples one step frequency per sample and rolls out with that sample's own contact
+ * sequence: PeriodicGaitGeneratorJax (periodic_gait_generator_jax.py:68-151) advanced from
+ * `timing` with pgg_dt * f per step and contact = t < duty_factor; the per-leg decode index counts
+ * the leg's stance steps (GA:353-379) and the cost gains (f - 1.3) * 100 * (f - 1.3) (GA:500).
+ * The caller's contact sequence of srbd_step is still the one the final GRFs use (GA:720-796).
+ *   timing      : 4 floats, the periodic gait generator phase of each leg (pgg_phase_signal)
+ *   pgg_dt      : mpc_params['dt'] (GA:179);  duty_factor: 0.65 in the reference (GA:179)
+ *   freq_set    : n_freq (1..SRBD_MAX_FREQS) candidate frequencies, drawn uniformly per sample
+ *                 (jax.random.choice); the caller forms the set per method and call:
+ *                 RS: optimize_swing ? step_freq_available : n x nominal; MPPI: step_freq_available
+ *   freq_local  : NULL -> device draw (Philox, keyed by seed/counter and global row); else the
+ *                 frequency of each of this shard's rows (parity / injection mode, like `noise`)
+ * Call again before each step to change any of these; srbd_clear_gait returns to the plain path.
+ * CEM is not supported (the reference's gait-adaptive CEM is broken as wired):
+ * SRBD_E_INVALID.
+ */
+int srbd_set_gait(srbd_ctx* ctx, const float* timing, float pgg_dt, float duty_factor, const float* freq_set,
+                  int32_t n_freq, const float* freq_local);
+int srbd_clear_gait(srbd_ctx* ctx);
 
 /* Sharded form.  Record size in floats (identical on every rank). */
 int srbd_record_floats(const srbd_ctx* ctx);

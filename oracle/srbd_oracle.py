@@ -114,10 +114,13 @@ class CentroidalModel:
         self.inertia_inv = calculate_inverse(self.inertia)  # CMJ:56
 
     def fd(self, x: np.ndarray, f: np.ndarray, c: np.ndarray) -> np.ndarray:
-        """CMJ:93-162.  x: (N,24) f32 state; f: (N,12) f32 foot forces (inputs[12:]); c: (4,) f32."""
+        """CMJ:93-162.  x: (N,24) f32 state; f: (N,12) f32 foot forces (inputs[12:]); c: (4,) f32
+        contact flags shared by all samples, or (N,4) per sample (gait-adaptive rollouts)."""
         x = np.asarray(x, dtype=f32)
         f = np.asarray(f, dtype=f32)
         c = np.asarray(c, dtype=f32)
+        if c.ndim == 2:
+            c = [c[:, i:i + 1] for i in range(4)]
         feet = [x[:, 12 + 3 * i: 15 + 3 * i] for i in range(4)]
         forces = [f[:, 3 * i: 3 * i + 3] for i in range(4)]
         com = x[:, 0:3]

@@ -97,6 +97,7 @@ struct srbd_ctx {
     float* d_wrec = nullptr;
     float* d_part = nullptr;  // first-level merge partials (rank-record format)
     hipGraphExec_t g_dev2 = nullptr, g_dev1 = nullptr;
+    float* d_ga_freq = nullptr;  // injected per-row step frequencies (gait-adaptive parity mode), ldn floats
     bool input_ready = false;
     std::string err;
 };
@@ -228,6 +229,9 @@ static int build_model(const srbd_config* cfg, ModelConst* mc, std::string* why)
     spline_coef(cfg, 0.0f, 1, &mc->fidx, &mc->fq, &mc->fomq, &mc->fa, &mc->fb, &mc->fc, &mc->fd);
     mc->sigma_mppi = cfg->sigma_mppi;
     for (int i = 0; i < 3; ++i) mc->sigma_rs[i] = cfg->sigma_random_sampling[i];
+    mc->ga = 0;
+    mc->ga_freq = nullptr;
+    for (int i = 0; i < 5; ++i) mc->fz_ns[i] = mc->mg / (float)i;  // the division fill_input makes per step
     return SRBD_OK;
 }
 
@@ -353,6 +357,7 @@ extern "C" void srbd_destroy(srbd_ctx* c) {
     (void)hipFree(c->d_costs);
     (void)hipFree(c->d_wrec);
     (void)hipFree(c->d_part);
+    (void)hipFree(c->d_ga_freq);
     if (c->h_in) (void)hipHostFree(c->h_in);
     if (c->h_out) (void)hipHostFree(c->h_out);
     if (c->h_flag) (void)hipHostFree(c->h_flag);
@@ -467,6 +472,7 @@ static int copy_out(srbd_ctx* c, float* best, float* sigma, srbd_result* out) {
         memcpy(out->predicted_state, o.pred, sizeof(out->predicted_state));
         out->best_cost = o.best_cost;
         out->best_index = o.best_index;
+        out->best_freq = o.best_freq;
         out->status = o.status;
     }
     return SRBD_OK;
@@ -603,6 +609,63 @@ extern "C" int srbd_copy_costs(srbd_ctx* c, float* out_costs) {
     return SRBD_OK;
 }
 
+// ------------------------------------------------------------------ gait-adaptive sampling
+static void drop_graphs(srbd_ctx* c) {
+    if (c->g_dev2) (void)hipGraphExecDestroy(c->g_dev2);
+    if (c->g_dev1) (void)hipGraphExecDestroy(c->g_dev1);
+    c->g_dev2 = c->g_dev1 = nullptr;
+    xg_drop_graphs(c);
+}
+
+extern "C" int srbd_set_gait(srbd_ctx* c, const float* timing, float pgg_dt, float duty_factor, const float* freq_set,
+                             int32_t n_freq, const float* freq_local) {
+    if (!c || !timing || !freq_set || n_freq < 1 || n_freq > SRBD_MAX_FREQS) return SRBD_E_INVALID;
+    if (c->mc.method == SRBD_CEM_MPPI)
+        return fail(c, SRBD_E_INVALID,
+                    "gait-adaptive CEM is not provided (the reference's branch is broken as wired, SURVEY App. B #2)");
+    if (c->mc.kind != SRBD_ZERO_ORDER && c->mc.S + 1 > GA_MAXCB) return fail(c, SRBD_E_INVALID, "num_splines > 32");
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));  // no step in flight reads the staging or d_ga_freq
+    StepInput* in = c->h_in;
+    for (int l = 0; l < 4; ++l) in->ga_timing[l] = timing[l];
+    in->ga_dt = pgg_dt;
+    in->ga_duty = duty_factor;
+    in->ga_nfreq = n_freq;
+    for (int i = 0; i < SRBD_MAX_FREQS; ++i) in->ga_freqs[i] = i < n_freq ? freq_set[i] : 0.0f;
+    // chunk boundaries float32(linspace(0, H, S+1)) as spline_coef forms them; integer steps compare
+    // >= a boundary exactly when they are >= its ceiling
+    for (int i = 0; i < GA_MAXCB; ++i) {
+        const int S = c->mc.S > 0 ? c->mc.S : 1;
+        const float cb = (float)((double)c->mc.H * (double)i / (double)S);
+        in->ga_cb[i] = i <= S ? (int)ceilf(cb) : 1 << 30;
+    }
+    in->ga_explicit = freq_local ? 1 : 0;
+    if (freq_local) {
+        if (!c->d_ga_freq) {
+            HIP_TRY(c, hipMalloc((void**)&c->d_ga_freq, sizeof(float) * (size_t)c->mc.ldn));
+            HIP_TRY(c, hipMemset(c->d_ga_freq, 0, sizeof(float) * (size_t)c->mc.ldn));
+        }
+        HIP_TRY(c, hipMemcpy(c->d_ga_freq, freq_local, sizeof(float) * (size_t)c->mc.n_local, hipMemcpyHostToDevice));
+    }
+    if (!c->mc.ga || c->mc.ga_freq != c->d_ga_freq) {  // kernels take ModelConst by value: recapture graphs
+        c->mc.ga = 1;
+        c->mc.ga_freq = c->d_ga_freq;
+        drop_graphs(c);
+    }
+    return SRBD_OK;
+}
+
+extern "C" int srbd_clear_gait(srbd_ctx* c) {
+    if (!c) return SRBD_E_INVALID;
+    if (c->mc.ga) {
+        HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        c->mc.ga = 0;
+        drop_graphs(c);
+    }
+    return SRBD_OK;
+}
+
 // ------------------------------------------------------------------ host merge (no device)
 static uint64_t host_rec_key(const float* R, int P, int q) {
     return ((uint64_t)f2u(R[REC_HDR + P + 2 * q + 1]) << 32) | (uint64_t)f2u(R[REC_HDR + P + 2 * q]);
@@ -667,9 +730,11 @@ extern "C" int srbd_finish_host(const srbd_config* cfg, const float* recs, int32
         return fail(nullptr, rc, "invalid arguments");
     }
     uint64_t bk = ~0ull;
+    float btag = 0.0f;
     for (int r = 0; r < nrec; ++r) {
         const float* R = recs + (size_t)r * stridef;
         const uint64_t kk = ((uint64_t)f2u(R[0]) << 32) | f2u(R[2]);
+        btag = kk < bk ? R[3] : btag;
         bk = kk < bk ? kk : bk;
     }
     const float beta = u2f((uint32_t)(bk >> 32));
@@ -719,6 +784,7 @@ extern "C" int srbd_finish_host(const srbd_config* cfg, const float* recs, int32
         memcpy(out->predicted_state, pred, sizeof(pred));
         out->best_cost = beta;
         out->best_index = (int32_t)(uint32_t)bk;
+        out->best_freq = btag;
         out->status = 0;
     }
     delete in;

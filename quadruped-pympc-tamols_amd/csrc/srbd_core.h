@@ -37,7 +37,14 @@ struct ModelConst {
     int fidx;
     float fq, fomq, fa, fb, fc, fd;
     float sigma_mppi, sigma_rs[3];
+    // gait-adaptive sampling (srbd_set_gait): on/off, float32(mg) / n_stance for n_stance = 0..4
+    // (GA:385; inf at 0), and the device array of injected per-row step frequencies (ldn entries)
+    int ga;
+    float fz_ns[5];
+    const float* ga_freq;
 };
+
+constexpr int GA_MAXCB = 33;  // chunk boundaries of S <= 32 splines
 
 // Per-step inputs: one pinned host copy -> one H2D per step.
 struct StepInput {
@@ -48,7 +55,15 @@ struct StepInput {
     float cost_feet;    // sum over feet of (e*0)*e: 0, or NaN when a foot error is not finite
     uint32_t seed_lo, seed_hi, ctr_lo, ctr_hi;
     int32_t noise_scaled;  // 0: noise holds unscaled CEM draws (device RNG), multiply by sigma on read
-    int32_t pad[3];
+    // gait-adaptive sampling (srbd_set_gait): leg phases, PGG dt and duty factor, the per-call
+    // frequency set, injected (1) or device-drawn (0) frequencies, and per chunk boundary i the
+    // smallest integer step with step >= float32(linspace(0, H, S+1)[i]) (GA:196)
+    int32_t ga_nfreq, ga_explicit;
+    float ga_timing[4];
+    float ga_dt, ga_duty;
+    float ga_freqs[SRBD_MAX_FREQS];
+    int32_t ga_cb[GA_MAXCB];
+    int32_t pad[1];
     float best[MAXP];
     float sigma[MAXP];
 };
@@ -61,7 +76,7 @@ struct StepOutput {
     float best_cost;
     int32_t best_index;
     int32_t status;
-    int32_t pad;
+    float best_freq;  // gait-adaptive: step frequency of the best row
 };
 
 SRBD_HD int rec_floats_wave(int P, int K) { return REC_HDR + P + 2 * K; }

@@ -197,11 +197,13 @@ __device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, Ns.
 
 // Per-block record (see srbd_core.h REC_*): min key, sum_k e_k, sum_k e_k * noise_k[j], top-K keys,
 // e_k = exp(-(c_k - m_b)).  SPB samples per block (multiple of 4); the thread owning sample `sib`
-// passes it (others pass sib = -1).  All threads of the block must call this.
+// passes it (others pass sib = -1) with its `tag` (the gait-adaptive step frequency, else 0), which
+// the owner of the block's best row stores in the record header.  All threads of the block must call
+// this.
 __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepInput* __restrict__ in, const int SPB,
                                                int sib, bool valid, float cost, const float* __restrict__ noise,
                                                float* __restrict__ recs, int rec_stride, float* e_sh, uint64_t* red,
-                                               uint64_t* elite_sh, bool cemt) {
+                                               uint64_t* elite_sh, bool cemt, float tag = 0.0f) {
     const int tid = threadIdx.x, T = blockDim.x;
     const int k0 = blockIdx.x * SPB;
     const uint64_t key = (sib >= 0 && valid) ? cost_key(cost, (uint32_t)(mc.row0 + k0 + sib)) : ~0ull;
@@ -246,9 +248,9 @@ __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepI
     if (tid == 0) {
         rec[0] = m;
         rec[2] = u2f((uint32_t)bkey);
-        rec[3] = 0.0f;
         if (mc.method == SRBD_RANDOM_SAMPLING) rec[1] = 1.0f;
     }
+    if (sib >= 0 && key == bkey) rec[3] = tag;  // keys are unique: exactly one writer
     if (tid < K) {
         const uint64_t kk = elite_sh[tid];
         rec[REC_HDR + P + 2 * tid] = u2f((uint32_t)kk);
@@ -335,6 +337,139 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
     if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
     if (valid && costs) costs[k] = cost;
     block_epilogue(mc, in, T, tid, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh, CEMT);
+}
+
+// ---- gait-adaptive rollout (centroidal_nmpc_jax_gait_adaptive.py:326-501).
+// One thread per sample.  The sample's step frequency f is injected (ga_explicit) or drawn from the
+// per-call set with one Philox call on the sample's own counter lane (jax.random.choice, GA:692/836;
+// the threefry stream is not reproduced); its contact sequence is the JAX gait
+// generator's (periodic_gait_generator_jax.py:68-151) run from the caller's leg phases, kept as one
+// bit mask per leg; each leg's decode index counts its stance steps so far (n_, GA:339/353-356,
+// -1 before the first touchdown: jnp's negative index wraps to the leg's last parameter) with
+// horizon_leg = stance steps + 1 (GA:345-348); the cost gains (f - 1.3) * 100 * (f - 1.3) (GA:500).
+constexpr uint32_t GA_FREQ_LANE = 0x10000u;  // Philox counter word 1 of the frequency draw (noise uses < P/4)
+
+__device__ __forceinline__ float ga_sample_freq(const ModelConst& mc, const StepInput* __restrict__ in, int k) {
+    if (in->ga_explicit) return mc.ga_freq[k];
+    const uint64_t seed = ((uint64_t)in->seed_hi << 32) | in->seed_lo;
+    uint32_t c[4] = {(uint32_t)(mc.row0 + k), GA_FREQ_LANE, in->ctr_lo, in->ctr_hi};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint32_t i = (uint32_t)(((uint64_t)c[0] * (uint32_t)in->ga_nfreq) >> 32);  // uniform in [0, n)
+    return in->ga_freqs[i];
+}
+
+// Per-leg contact masks of one sample (bit n = stance at step n), PGGJ:136-151 with run :68-89:
+// restart (t >= 1 -> 0), advance by pgg_dt * f (the product first), stance while t < duty.
+__device__ __forceinline__ void ga_contact_masks(const StepInput* __restrict__ in, int H, float f, uint32_t mask[4]) {
+    const float inc = in->ga_dt * f;
+    float t[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        t[l] = in->ga_timing[l];
+        mask[l] = 0u;
+    }
+    for (int n = 0; n < H; ++n)
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            t[l] = t[l] >= 1.0f ? 0.0f : t[l];
+            t[l] = t[l] + inc;
+            mask[l] |= (t[l] < in->ga_duty ? 1u : 0u) << n;
+        }
+}
+
+template <int KIND>
+__global__ void __launch_bounds__(256) rollout_ga_kernel(const ModelConst mc, const StepInput* __restrict__ in,
+                                                         const float* __restrict__ noise, float* __restrict__ costs,
+                                                         float* __restrict__ recs, int rec_stride,
+                                                         const RngJob next_rng, int nroll) {
+    if ((int)blockIdx.x >= nroll) {
+        rng_items(mc, in, next_rng, ((int)blockIdx.x - nroll) * (int)blockDim.x + (int)threadIdx.x,
+                  ((int)gridDim.x - nroll) * (int)blockDim.x);
+        return;
+    }
+    __shared__ float e_sh[256];
+    __shared__ uint64_t red[4];
+    __shared__ uint64_t elite_sh[MAXK];
+    const int H = mc.H, S = mc.S, PL = mc.PL;
+    const int tid = threadIdx.x, T = blockDim.x;
+    const int k = blockIdx.x * T + tid;  // rows >= n_local are padding (readable zeros)
+    const bool valid = k < mc.n_local;
+    const size_t ldn = (size_t)mc.ldn;
+    const float* __restrict__ nz = noise + k;
+    const float* __restrict__ best = in->best;
+
+    const float f = ga_sample_freq(mc, in, k);
+    uint32_t mask[4];
+    ga_contact_masks(in, H, f, mask);
+    float seg[4];  // horizon_leg / S (GA:200 / :223), IEEE division
+#pragma unroll
+    for (int l = 0; l < 4; ++l) seg[l] = ((float)__popc(mask[l]) + 1.0f) / (float)S;
+    int cnt[4] = {-1, -1, -1, -1};
+
+    float x[12], feet[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+        x[i] = in->state[i];
+        feet[i] = in->state[12 + i];
+    }
+    float cost3[3] = {0.0f, 0.0f, 0.0f};
+    for (int n = 0; n < H; ++n) {
+        float c[4];
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            const uint32_t b = (mask[l] >> n) & 1u;
+            c[l] = b ? 1.0f : 0.0f;
+            cnt[l] += (int)b;
+        }
+        const float ns = ((c[0] + c[1]) + c[2]) + c[3];
+        const float fref = mc.fz_ns[(int)ns];
+        float F[12];
+#pragma unroll
+        for (int leg = 0; leg < 4; ++leg) {
+            const int base = leg * PL;
+            auto acc = [&](int j) {
+                j = j < 0 ? j + PL : j;
+                return best[base + j] + nz[(size_t)(base + j) * ldn];
+            };
+            const int st = cnt[leg];
+            int idx = 0;
+            float q = 0.0f, omq = 0.0f, a = 0.0f, bb = 0.0f, cc = 0.0f, d = 0.0f;
+            if (KIND != SRBD_ZERO_ORDER) {  // spline_coef of srbd_api.hip with (step, horizon_leg) per leg
+                for (int i = 0; i <= S; ++i)
+                    if (st >= in->ga_cb[i]) idx = i;
+                float tau = (float)st / seg[leg];
+                tau = tau - (float)idx;
+                q = tau / 1.0f;
+                omq = 1.0f - q;
+                a = 2.0f * q * q * q - 3.0f * q * q + 1.0f;
+                bb = (q * q * q - 2.0f * q * q + q) * 1.0f;
+                cc = -2.0f * q * q * q + 3.0f * q * q;
+                d = (q * q * q - q * q) * 1.0f;
+            }
+            float fx, fy, fz;
+            decode_leg(KIND, H, S, idx, q, omq, a, bb, cc, d, st, acc, fx, fy, fz);
+            shape_leg(mc, fref, c[leg], fx, fy, fz);
+            F[3 * leg] = fx;
+            F[3 * leg + 1] = fy;
+            F[3 * leg + 2] = fz;
+        }
+        integrate(mc, x, feet, F, c, mc.dts[n]);
+        float t[12];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+            const float e = x[i] - in->ref[i];
+            t[i] = (e * mc.Q[i]) * e;
+        }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) cost3[q] = cost3[q] + (((t[q] + t[3 + q]) + t[6 + q]) + t[9 + q]);
+    }
+    float cost = (cost3[0] + cost3[1]) + cost3[2];
+    cost = cost + in->cost_feet;
+    const float df = f - 1.3f;
+    cost = cost + (df * 100.0f) * df;  // GA:500
+    if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
+    if (valid && costs) costs[k] = cost;
+    block_epilogue(mc, in, T, tid, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh, false, f);
 }
 
 // ---- four lanes per sample: lane c in {0,1,2} owns component c (x, y, z) of every 3-vector of
@@ -642,6 +777,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     __shared__ float Vs[MAXP + 1];
     __shared__ float nb[MAXP];
     __shared__ float grf_sh[12];
+    __shared__ float tag_sh;  // header tag (gait-adaptive step frequency) of the record holding beta's row
 #define MERGE_STAMP(i) \
     if (dbg && threadIdx.x == 0) dbg[i] = __builtin_amdgcn_s_memrealtime()
     MERGE_STAMP(0);
@@ -680,6 +816,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     const float state_hi = (out && tid >= 12 && tid < 24) ? in->state[tid] : 0.0f;
     float mr[MERGE_RPT];
     uint64_t mine = KEY_NONE;
+    float mtag = 0.0f;
 #pragma unroll
     for (int i = 0; i < MERGE_RPT; ++i) {
         const int r = tid + i * T;
@@ -687,7 +824,10 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         if (r < nrec) {
             const float* R = recs + (size_t)r * rec_stride;
             mr[i] = R[0];
-            mine = umin64(mine, ((uint64_t)f2u(mr[i]) << 32) | (uint64_t)f2u(R[2]));
+            const uint64_t kk = ((uint64_t)f2u(mr[i]) << 32) | (uint64_t)f2u(R[2]);
+            const float tg = R[3];
+            mtag = kk < mine ? tg : mtag;
+            mine = umin64(mine, kk);
         }
     }
     const int j = tid % cols, g = tid / cols;
@@ -706,6 +846,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
 #pragma unroll
     for (int i = 1; i < MERGE_WAVES; ++i) bkey = umin64(bkey, red[i]);
     const float beta = u2f((uint32_t)(bkey >> 32));
+    if (mine == bkey && mine != KEY_NONE) tag_sh = mtag;  // keys are unique: one writer
     MERGE_STAMP(1);
 
     // ---- 2./3. softmax-weighted sums
@@ -793,7 +934,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
             rank_out[0] = beta;
             rank_out[1] = rs ? 1.0f : Vs[P];
             rank_out[2] = u2f((uint32_t)bkey);
-            rank_out[3] = 0.0f;
+            rank_out[3] = tag_sh;
         }
     }
     if (out) {
@@ -858,6 +999,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         if (tid == 0) {
             out->best_cost = beta;
             out->best_index = (int32_t)(uint32_t)bkey;
+            out->best_freq = tag_sh;
             out->status = 0;
             if (chain) in->noise_scaled = 0;  // the chain's next draws come from the device RNG
             if (chain && ctr_inc) {
@@ -1022,8 +1164,28 @@ bool rollout_specialised(int kind, int H, int S) {
     return S == 2 && (H == 12 || H == 16);
 }
 
+// Same samples per block as the context's rollout mode (the merge reads one record per block).
+static void launch_rollout_ga(const ModelConst& mc, const StepInput* in, const float* noise, float* costs,
+                              float* recs, int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next) {
+    const RngJob job = next ? *next : RngJob{nullptr, 0, 0, 0, 0};
+    const int extra = next ? (rng_grid(mc) < 1024 ? rng_grid(mc) : 1024) : 0;
+    const int spb = mode == ROLLOUT_QUAD ? threads / 4 : threads;
+    const int blocks = (mc.n_local + spb - 1) / spb;
+    const dim3 grid(blocks + extra * 256 / spb), block(spb);
+    if (mc.kind == SRBD_ZERO_ORDER)
+        hipLaunchKernelGGL((rollout_ga_kernel<SRBD_ZERO_ORDER>), grid, block, 0, s, mc, in, noise, costs, recs,
+                           rec_stride, job, blocks);
+    else if (mc.kind == SRBD_LINEAR_SPLINE)
+        hipLaunchKernelGGL((rollout_ga_kernel<SRBD_LINEAR_SPLINE>), grid, block, 0, s, mc, in, noise, costs, recs,
+                           rec_stride, job, blocks);
+    else
+        hipLaunchKernelGGL((rollout_ga_kernel<SRBD_CUBIC_SPLINE>), grid, block, 0, s, mc, in, noise, costs, recs,
+                           rec_stride, job, blocks);
+}
+
 void launch_rollout(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
                     int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next) {
+    if (mc.ga) return launch_rollout_ga(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next);
     const int H = mc.H, S = mc.S;
 #define SRBD_LR(K, HH, SS) \
     return launch_rollout_t<K, HH, SS>(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next)

@@ -50,7 +50,7 @@ class SrbdConfig(C.Structure):
 
 class SrbdResult(C.Structure):
     _fields_ = [("grf", _F * 12), ("predicted_state", _F * 24), ("best_cost", _F), ("best_index", _I),
-                ("status", _I), ("_pad", _I)]
+                ("status", _I), ("best_freq", _F)]
 
 
 class TamolsParams(C.Structure):
@@ -72,6 +72,8 @@ SIGNATURES = {
     "srbd_set_stream": (_I, [_P, _P]),
     # host-step pointers are plain addresses (Context passes cached ints: ndarray.ctypes costs ~2.5 us each)
     "srbd_step": (_I, [_P, _P, _P, _P, _I, _P, _P, _P, C.c_uint64, C.c_uint64, C.POINTER(SrbdResult), _P]),
+    "srbd_set_gait": (_I, [_P, _FP, _F, _F, _FP, _I, _FP]),
+    "srbd_clear_gait": (_I, [_P]),
     "srbd_record_floats": (_I, [_P]),
     "srbd_step_local": (_I, [_P, _FP, _FP, _FP, _I, _FP, _FP, _FP, C.c_uint64, C.c_uint64, _P]),
     "srbd_step_finish": (_I, [_P, _P, _I, _FP, _FP, C.POINTER(SrbdResult), _FP]),
@@ -358,6 +360,19 @@ class Context:
         out = np.zeros(5, np.float32)
         self.check(lib.srbd_debug_merge_phases(self.h, int(iters), fptr(out)), "srbd_debug_merge_phases")
         return dict(zip(("min_key", "weighted_sums", "elite", "outputs", "tail"), (round(float(x), 3) for x in out)))
+
+    def set_gait(self, timing, pgg_dt: float, duty_factor: float, freq_set, freq_local=None):
+        """srbd_set_gait: gait-adaptive sampling for the following steps (see include/srbd_mpc.h)."""
+        t = np.ascontiguousarray(np.asarray(timing, np.float32).reshape(4))
+        fs = np.ascontiguousarray(np.asarray(freq_set, np.float32).reshape(-1))
+        fl = None if freq_local is None else np.ascontiguousarray(np.asarray(freq_local, np.float32).reshape(-1))
+        if fl is not None and fl.shape[0] != self.n_local:
+            raise ValueError(f"freq_local: {self.n_local} rows expected, got {fl.shape[0]}")
+        self.check(lib.srbd_set_gait(self.h, fptr(t), float(pgg_dt), float(duty_factor), fptr(fs), int(fs.shape[0]),
+                                     fptr(fl)), "srbd_set_gait")
+
+    def clear_gait(self):
+        self.check(lib.srbd_clear_gait(self.h), "srbd_clear_gait")
 
     def set_stream(self, stream_handle: int | None):
         """Launch on a caller-owned hipStream_t; None (or 0, the legacy null stream) -> the context's own."""

@@ -164,6 +164,7 @@ class Sampling_MPC:
         best, new_sigma, res, _ = ctx.step(state, reference, np.asarray(contact_sequence, dtype=f32),
                                            best_control_parameters, sigma=sigma, noise=noise, seed=int(key[0]),
                                            counter=int(key[1]) if key.shape[0] > 1 else 0)
+        self.last_result = res
         grf = np.array(res.grf, dtype=f32)
         pred = np.array(res.predicted_state, dtype=f32)
         costs = LazyCosts(ctx, ctx.step_id)

@@ -28,9 +28,10 @@ class SRBDControllerInterface:
         self.previous_contact_mpc = np.array([1, 1, 1, 1])
         if self.type != "sampling":
             raise NotImplementedError(f"controller type {self.type!r}: only 'sampling' is provided (MI355X HIP)")
-        if self.optimize_step_freq:
-            raise NotImplementedError("gait-adaptive sampling MPC (optimize_step_freq) is not provided yet")
-        from ..controllers.sampling.centroidal_nmpc_hip import Sampling_MPC
+        if self.optimize_step_freq:  # srbd_controller_interface.py:77-81
+            from ..controllers.sampling.centroidal_nmpc_hip_gait_adaptive import Sampling_MPC
+        else:
+            from ..controllers.sampling.centroidal_nmpc_hip import Sampling_MPC
 
         self.controller = Sampling_MPC(cfg)
 

@@ -183,10 +183,26 @@ def test_interface_rejects_out_of_scope_types():
 
     with pytest.raises(NotImplementedError):
         SRBDControllerInterface(cfg_module(type="nominal"))
-    with pytest.raises(NotImplementedError):
-        SRBDControllerInterface(cfg_module(optimize_step_freq=True))
     itf = SRBDControllerInterface(cfg_module(sampling_method="mppi", control_parametrization="zero_order"))
     assert isinstance(itf.controller, Sampling_MPC)
+
+
+def test_interface_selects_gait_adaptive_controller():
+    """optimize_step_freq selects the gait-adaptive Sampling_MPC (srbd_controller_interface.py:77-81);
+    its CEM branch (broken in the reference, SURVEY App. B #2) refuses before touching a device."""
+    from quadruped_pympc_amd.controllers.sampling import centroidal_nmpc_hip_gait_adaptive as ga
+    from quadruped_pympc_amd.interfaces.srbd_controller_interface import SRBDControllerInterface
+
+    itf = SRBDControllerInterface(cfg_module(optimize_step_freq=True, sampling_method="mppi"))
+    assert isinstance(itf.controller, ga.Sampling_MPC)
+    np.testing.assert_array_equal(itf.controller._freq_set(1.65, 0), np.array([1.4, 2.0, 2.4], f32))
+    rs = ga.Sampling_MPC(cfg_module(optimize_step_freq=True, sampling_method="random_sampling"))
+    np.testing.assert_array_equal(rs._freq_set(1.65, 1), np.array([1.4, 2.0, 2.4], f32))
+    np.testing.assert_array_equal(rs._freq_set(1.65, 0), np.full(3, f32(1.65)))
+    cem = ga.Sampling_MPC(cfg_module(optimize_step_freq=True, sampling_method="cem_mppi"))
+    with pytest.raises(NotImplementedError, match="App. B #2"):
+        cem.jitted_compute_control(np.zeros(24), np.zeros(24), np.ones((4, 12)), cem.best_control_parameters,
+                                   cem.master_key, 3.0)
 
 
 def test_interface_masks_grfs_and_reassigns_params():
