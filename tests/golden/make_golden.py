@@ -19,6 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path[:0] = [ROOT, os.path.join(ROOT, "quadruped-pympc-tamols_amd")]
 
 from oracle.pgg_oracle import PGGOracle  # noqa: E402
+from oracle.srbd_ga_oracle import GA_DUTY, GaitAdaptiveOracle, freq_set  # noqa: E402
 from oracle.srbd_oracle import SamplingMPCOracle, prepare_state_and_reference  # noqa: E402
 from oracle.tamols_oracle import TamolsOracle, synthetic_patch  # noqa: E402
 from quadruped_pympc_amd.config import HIP_HEIGHTS, simulation_params  # noqa: E402
@@ -61,6 +62,37 @@ def srbd_fixture(name, wkey, method, par, H, N, nonuniform):
         # outputs
         costs=out["costs"], best=out["best"], grf=out["grf"], pred=out["pred"], best_index=out["best_index"],
         best_cost=out["best_cost"], sigma=out.get("sigma", np.zeros(0, f32)))
+
+
+# gait-adaptive: name: (workload, method, parametrization, H, N, leg phases)
+GA_CASES = {
+    "c2_mppi_zo_h12": ("c2", "mppi", "zero_order", 12, 160, (0.1, 0.6, 0.6, 0.1)),
+    "c2_rs_linear_h12": ("c2", "random_sampling", "linear_spline", 12, 128, (0.64, 0.99, 1.0, 0.3)),
+}
+
+
+def ga_fixture(name, wkey, method, par, H, N, timing):
+    w = CONFIGS[wkey]
+    o = GaitAdaptiveOracle(pgg_dt=0.02, mass=w.mass, inertia=w.inertia, horizon=H, num_samples=N, method=method,
+                           parametrization=par)
+    rng = np.random.default_rng(sum(map(ord, name)))
+    state, ref, contact = inputs(w, 4)
+    contact = contact[:, :H]
+    t = N // 3
+    noise = o.assemble_noise(rng.standard_normal((N - 1, o.P)).astype(f32),
+                             U=rng.uniform(-10, 10, (N - 1 - 2 * t, o.P)).astype(f32))
+    fs = freq_set(o.method, (1.4, 2.0, 2.4), 1.65, 1)
+    freqs = rng.choice(fs, N).astype(f32)
+    best = rng.standard_normal(o.P).astype(f32)
+    out = o.compute_control_ga(state.astype(f32), ref.astype(f32), contact.astype(f32), best, noise, freqs, timing)
+    np.savez_compressed(
+        os.path.join(OUT, f"ga_{name}.npz"),
+        method=method, parametrization=par, horizon=H, num_samples=N, num_splines=2, mass=w.mass,
+        inertia=w.inertia, dts=o.robot.dts, state=state.astype(f32), ref=ref.astype(f32),
+        contact=contact.astype(f32), best_in=best, noise=noise, timing=np.asarray(timing, f32), pgg_dt=0.02,
+        duty=GA_DUTY, freq_set=fs, freqs=freqs,
+        costs=out["costs"], best=out["best"], grf=out["grf"], pred=out["pred"], best_index=out["best_index"],
+        best_cost=out["best_cost"], best_freq=out["best_freq"])
 
 
 def prepare_fixture():
@@ -128,6 +160,8 @@ def tamols_fixture():
 def main():
     for name, spec in SRBD_CASES.items():
         srbd_fixture(name, *spec)
+    for name, spec in GA_CASES.items():
+        ga_fixture(name, *spec)
     prepare_fixture()
     pgg_fixture()
     tamols_fixture()

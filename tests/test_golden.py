@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 from oracle import c_oracle as co
+from oracle.srbd_ga_oracle import GaitAdaptiveOracle
 from oracle.srbd_oracle import SamplingMPCOracle
 from oracle.tamols_oracle import TamolsOracle
 from quadruped_pympc_amd import _lib
@@ -22,6 +23,7 @@ from quadruped_pympc_amd.helpers.periodic_gait_generator import PeriodicGaitGene
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 SRBD = sorted(glob.glob(os.path.join(GOLDEN, "srbd_*.npz")))
+GA = sorted(glob.glob(os.path.join(GOLDEN, "ga_*.npz")))
 f32 = np.float32
 METHODS = {"random_sampling": 0, "mppi": 1, "cem_mppi": 2}
 PARS = {"zero_order": 0, "linear_spline": 1, "cubic_spline": 2}
@@ -41,6 +43,20 @@ def oracle_for(g):
 
 def test_fixtures_present():
     assert len(SRBD) >= 5
+    assert len(GA) >= 2
+
+
+@pytest.mark.parametrize("path", GA, ids=os.path.basename)
+def test_ga_oracle_reproduces_fixture(path):
+    g = load(path)
+    o = GaitAdaptiveOracle(pgg_dt=float(g["pgg_dt"]), mass=float(g["mass"]), inertia=g["inertia"],
+                           horizon=int(g["horizon"]), num_samples=int(g["num_samples"]), method=str(g["method"]),
+                           parametrization=str(g["parametrization"]), num_splines=int(g["num_splines"]))
+    out = o.compute_control_ga(g["state"], g["ref"], g["contact"], g["best_in"], g["noise"], g["freqs"],
+                               g["timing"])
+    for k in ("costs", "best", "grf", "pred"):
+        np.testing.assert_array_equal(out[k], g[k])
+    assert out["best_index"] == int(g["best_index"]) and out["best_freq"] == g["best_freq"]
 
 
 @pytest.mark.parametrize("path", SRBD, ids=os.path.basename)

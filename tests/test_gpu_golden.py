@@ -14,6 +14,7 @@ pytestmark = pytest.mark.gpu
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 SRBD = sorted(glob.glob(os.path.join(GOLDEN, "srbd_*.npz")))
+GA = sorted(glob.glob(os.path.join(GOLDEN, "ga_*.npz")))
 f32 = np.float32
 
 
@@ -47,6 +48,26 @@ def test_gpu_step_matches_fixture(lib, path, graph):
     np.testing.assert_allclose(np.array(res.predicted_state), g["pred"], rtol=1e-5, atol=1e-4)
     if sigma is not None:
         np.testing.assert_allclose(ns, g["sigma"], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("path", GA, ids=os.path.basename)
+def test_gpu_gait_adaptive_step_matches_fixture(lib, path):
+    g = dict(np.load(path, allow_pickle=False))
+    cfg = lib.make_config(num_samples=int(g["num_samples"]), horizon=int(g["horizon"]), method=str(g["method"]),
+                          parametrization=str(g["parametrization"]), num_splines=int(g["num_splines"]),
+                          mass=float(g["mass"]), inertia=g["inertia"], dts=g["dts"])
+    ctx = lib.Context(cfg)
+    try:
+        ctx.set_gait(g["timing"], float(g["pgg_dt"]), float(g["duty"]), g["freq_set"], g["freqs"])
+        best, _, res, costs = ctx.step(g["state"], g["ref"], g["contact"], g["best_in"], noise=g["noise"],
+                                       want_costs=True)
+    finally:
+        ctx.close()
+    np.testing.assert_allclose(costs, g["costs"], rtol=2e-5, atol=1e-3)
+    assert res.best_index == int(g["best_index"]) and res.best_freq == g["best_freq"]
+    np.testing.assert_allclose(np.array(res.grf), g["grf"], rtol=1e-4, atol=5e-3)
+    np.testing.assert_allclose(best, g["best"], rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(np.array(res.predicted_state), g["pred"], rtol=1e-5, atol=1e-4)
 
 
 def test_gpu_tamols_matches_fixture(lib):

@@ -59,13 +59,20 @@ def probe(cx):
     return r.value
 
 
-def exchange_case(method, W=2, N=4000):
+def exchange_case(method, W=2, N=4000, ga=False):
     case = make_case("c2", N=N, method=method, seed=23)
+    freqs = np.random.default_rng(1).choice(np.array([1.4, 2.0, 2.4], f32), N).astype(f32) if ga else None
     full = _lib.Context(product_cfg(case))
+    if ga:
+        full.set_gait((0.1, 0.6, 0.6, 0.1), 0.02, 0.65, np.array([1.4, 2.0, 2.4], f32), freqs)
     b0, s0, r0, _ = full.step(case["state"], case["ref"], case["contact"], case["best"], sigma=case["sigma"],
                               noise=case["noise"])
     full.close()
     ctxs = connected(case, W)
+    if ga:  # each rank injects the frequencies of its own rows; the best row's travels in the records
+        for cx in ctxs:
+            cx.set_gait((0.1, 0.6, 0.6, 0.1), 0.02, 0.65, np.array([1.4, 2.0, 2.4], f32),
+                        freqs[cx.row0:cx.row0 + cx.n_local])
     oks = run_threads([lambda cx=cx: probe(cx) for cx in ctxs])
     assert all(ok == 1 for ok in oks), f"probe {oks}"
 
@@ -82,6 +89,7 @@ def exchange_case(method, W=2, N=4000):
             np.testing.assert_allclose(np.array(res.grf), np.array(r0.grf), rtol=1e-5, atol=1e-3)
             if method == "cem_mppi":
                 np.testing.assert_allclose(sg, s0, rtol=1e-5, atol=1e-6)
+            assert res.best_freq == r0.best_freq
         for o in outs[1:]:
             np.testing.assert_array_equal(outs[0][0], o[0])
             np.testing.assert_array_equal(np.array(outs[0][2].grf, f32), np.array(o[2].grf, f32))
@@ -121,7 +129,8 @@ def main():
     res = {}
     cases = [("mppi", lambda: exchange_case("mppi")), ("cem_mppi", lambda: exchange_case("cem_mppi")),
              ("random_sampling", lambda: exchange_case("random_sampling")),
-             ("mppi_w3", lambda: exchange_case("mppi", W=3, N=3001)), ("timeout", timeout_case)]
+             ("mppi_w3", lambda: exchange_case("mppi", W=3, N=3001)),
+             ("mppi_ga_w3", lambda: exchange_case("mppi", W=3, N=3001, ga=True)), ("timeout", timeout_case)]
     for name, fn in cases:
         try:
             fn()
