@@ -232,6 +232,21 @@ static int build_model(const srbd_config* cfg, ModelConst* mc, std::string* why)
     mc->ga = 0;
     mc->ga_freq = nullptr;
     for (int i = 0; i < 5; ++i) mc->fz_ns[i] = mc->mg / (float)i;  // the division fill_input makes per step
+    // the parameter columns final_grf_pred's decode reads (the column-split merge's tail block)
+    mc->ntail = 0;
+    for (int leg = 0; leg < 4; ++leg) {
+        auto rec = [&](int j) {
+            const int col = leg * mc->PL + j;
+            if (!is_tail_col(*mc, col)) {
+                mc->tailmask[col >> 5] |= 1u << (col & 31);
+                mc->tailc[mc->ntail++] = (short)col;
+            }
+            return 0.0f;
+        };
+        float fx, fy, fz;
+        decode_leg(mc->kind, mc->H, mc->S, mc->fidx, mc->fq, mc->fomq, mc->fa, mc->fb, mc->fc, mc->fd, 0, rec, fx, fy,
+                   fz);
+    }
     return SRBD_OK;
 }
 
@@ -309,11 +324,11 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
         return cleanup_fail("hipHostMalloc", e);
     if ((e = hipHostGetDevicePointer((void**)&c->d_out_host, c->h_out, 0)) != hipSuccess)
         return cleanup_fail("hipHostGetDevicePointer", e);
-    if ((e = hipHostMalloc((void**)&c->h_flag, 64, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+    if ((e = hipHostMalloc((void**)&c->h_flag, sizeof(uint32_t) * MERGE_MAX_BLOCKS, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
         return cleanup_fail("hipHostMalloc", e);
     if ((e = hipHostGetDevicePointer((void**)&c->d_flag, c->h_flag, 0)) != hipSuccess)
         return cleanup_fail("hipHostGetDevicePointer", e);
-    __atomic_store_n(c->h_flag, 0u, __ATOMIC_RELEASE);
+    for (int i = 0; i < MERGE_MAX_BLOCKS; ++i) __atomic_store_n(c->h_flag + i, 0u, __ATOMIC_RELEASE);
     memset(c->h_in, 0, sizeof(StepInput));
     memset(c->h_out, 0, sizeof(StepOutput));
     const size_t noise_bytes = sizeof(float) * (size_t)mc.P * mc.ldn;
@@ -326,7 +341,7 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     if ((e = hipMalloc((void**)&c->d_wrec, sizeof(float) * (size_t)c->nblocks * c->wrec_stride)) != hipSuccess)
         return cleanup_fail("hipMalloc", e);
     {
-        const int m = merge_partials(c->nblocks);
+        const int m = merge_partials(c->nblocks, false);  // the larger of the two partial counts
         if (m > 0 && (e = hipMalloc((void**)&c->d_part, sizeof(float) * (size_t)m * c->rrec_stride)) != hipSuccess)
             return cleanup_fail("hipMalloc", e);
     }
@@ -436,25 +451,33 @@ static int acquire_noise(srbd_ctx* c, const float* noise, uint64_t seed, uint64_
 }
 
 // rollout (+ next draws, counter + 1 from the device StepInput) -> merge on noise buffer `buf`
-static void enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput* out, int chain = 0,
-                                int ctr_inc = 1, bool fuse_next = false, Publish pub = {nullptr, 0}) {
+// Returns the number of merge blocks that publish (wait_published).
+static int enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput* out, int chain = 0,
+                               int ctr_inc = 1, bool fuse_next = false, Publish pub = {nullptr, 0}) {
     const ModelConst& mc = c->mc;
     const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1};
     launch_rollout(mc, c->d_in, c->d_noise[buf], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
                    c->stream, fuse_next ? &next : nullptr);
-    launch_merge_tree(mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, c->d_noise[buf], c->d_part, rank_out, out,
-                      chain, c->stream, ctr_inc, pub);
+    return launch_merge_tree(mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, c->d_noise[buf], c->d_part,
+                             rank_out, out, chain, c->stream, ctr_inc, pub);
 }
 
 // Wait for the merge to publish `seq`.  Polls the stream now and then so a device fault or a launch
 // failure surfaces as an error instead of a hang.
-static int wait_published(srbd_ctx* c, uint32_t seq) {
+// `nflags` merge blocks publish, each into its own word.
+static bool published(const srbd_ctx* c, uint32_t seq, int nflags) {
+    for (int i = 0; i < nflags; ++i)
+        if (__atomic_load_n(c->h_flag + i, __ATOMIC_ACQUIRE) != seq) return false;
+    return true;
+}
+
+static int wait_published(srbd_ctx* c, uint32_t seq, int nflags = 1) {
     for (uint64_t it = 1;; ++it) {
-        if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == seq) return SRBD_OK;
+        if (published(c, seq, nflags)) return SRBD_OK;
         if ((it & 4095) == 0) {
             const hipError_t e = hipStreamQuery(c->stream);
-            if (e == hipSuccess) {  // drained: the flag store has completed
-                if (__atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == seq) return SRBD_OK;
+            if (e == hipSuccess) {  // drained: the flag stores have completed
+                if (published(c, seq, nflags)) return SRBD_OK;
                 return fail(c, SRBD_E_HIP, "step completed without publishing its outputs");
             }
             if (e != hipErrorNotReady) HIP_TRY(c, e);
@@ -492,7 +515,7 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
     if ((rc = acquire_noise(c, noise, seed, counter, &buf))) return rc;
     const bool fuse = !noise && fusable(c);
     const Publish pub{c->d_flag, ++c->seq};
-    enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fuse, pub);
+    const int nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fuse, pub);
     HIP_TRY(c, hipGetLastError());
     if (fuse) {
         c->pref_valid = true;
@@ -500,7 +523,7 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
         c->pref_seed = seed;
         c->pref_ctr = counter + 1;
     }
-    if ((rc = wait_published(c, pub.seq))) return rc;
+    if ((rc = wait_published(c, pub.seq, nflags))) return rc;
     if (out_costs) {
         HIP_TRY(c, hipMemcpyAsync(out_costs, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,
                                   c->stream));
@@ -546,10 +569,10 @@ extern "C" int srbd_step_finish(srbd_ctx* c, const void* d_records, int32_t nrec
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "srbd_step_finish before srbd_step_local");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     const Publish pub{c->d_flag, ++c->seq};
-    launch_merge(c->mc, c->d_in, (const float*)d_records, nrec, c->rrec_stride, 1, nullptr, nullptr, c->d_out_host,
-                 0, c->stream, nullptr, 1, pub);
+    const int nflags = launch_merge(c->mc, c->d_in, (const float*)d_records, nrec, c->rrec_stride, 1, nullptr,
+                                    nullptr, c->d_out_host, 0, c->stream, nullptr, 1, pub);
     HIP_TRY(c, hipGetLastError());
-    int rc = wait_published(c, pub.seq);
+    int rc = wait_published(c, pub.seq, nflags);
     if (rc) return rc;
     if (out_costs_local) {
         HIP_TRY(c, hipMemcpyAsync(out_costs_local, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,

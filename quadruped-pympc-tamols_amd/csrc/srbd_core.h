@@ -21,6 +21,7 @@ constexpr int MAXH = SRBD_MAX_HORIZON;
 constexpr int MAXP = SRBD_MAX_PARAMS;
 constexpr int MAXK = SRBD_MAX_ELITE;
 constexpr int REC_HDR = 4;
+constexpr int MAX_TAIL = 48;  // 4 legs x 3 axes x 4 cubic control points
 
 // Per-context constants, passed to every kernel by value (kernarg segment -> SGPRs).
 struct ModelConst {
@@ -42,7 +43,13 @@ struct ModelConst {
     int ga;
     float fz_ns[5];
     const float* ga_freq;
+    // columns the final decode reads (decode_leg at step 0.0, horizon_leg 1): in the column-split
+    // merge the tail block computes and owns them (list + bit mask)
+    int ntail;
+    short tailc[MAX_TAIL];
+    uint32_t tailmask[MAXP / 32];
 };
+SRBD_HD bool is_tail_col(const ModelConst& mc, int j) { return (mc.tailmask[j >> 5] >> (j & 31)) & 1u; }
 
 constexpr int GA_MAXCB = 33;  // chunk boundaries of S <= 32 splines
 

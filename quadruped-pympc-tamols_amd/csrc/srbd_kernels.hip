@@ -18,6 +18,24 @@
 
 namespace srbd {
 
+// Timeline probe (measurement build only, `make probe`): thread 0 of every rollout-launch block
+// stores s_memrealtime (100 MHz) at fixed points after draining its outstanding memory operations.
+#ifdef SRBD_ROLLOUT_STAMPS
+constexpr int RSTAMP_N = 6, RSTAMP_BLOCKS = 8192;
+__device__ uint64_t g_rstamp[RSTAMP_BLOCKS * RSTAMP_N];
+#define SRBD_RSTAMP(i)                                                                  \
+    do {                                                                                \
+        if (threadIdx.x == 0 && blockIdx.x < RSTAMP_BLOCKS) {                           \
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                 \
+            g_rstamp[blockIdx.x * RSTAMP_N + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                               \
+    } while (0)
+#else
+#define SRBD_RSTAMP(i) \
+    do {               \
+    } while (0)
+#endif
+
 // ------------------------------------------------------------------ helpers
 // 64-bit wave minimum with DPP (row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15/31, gfx9
 // family), result read from lane 63.  All 64 lanes must be active.
@@ -218,6 +236,7 @@ __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepI
         last = block_min_u64(cand, red);
         if (tid == 0) elite_sh[r] = last;
     }
+    SRBD_RSTAMP(3);
     if (mc.method != SRBD_RANDOM_SAMPLING) {
         if (sib >= 0) e_sh[sib] = valid ? expf(-1.0f * (cost - m)) : 0.0f;
         __syncthreads();
@@ -245,6 +264,7 @@ __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepI
         }
     }
     __syncthreads();
+    SRBD_RSTAMP(4);
     if (tid == 0) {
         rec[0] = m;
         rec[2] = u2f((uint32_t)bkey);
@@ -564,9 +584,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
                                                            float* __restrict__ recs, int rec_stride,
     const RngJob next_rng, int nroll) {
     // blocks past the rollout grid generate the next step's noise on the CUs the rollout leaves idle
+    SRBD_RSTAMP(0);
     if ((int)blockIdx.x >= nroll) {
         rng_items(mc, in, next_rng, ((int)blockIdx.x - nroll) * (int)blockDim.x + (int)threadIdx.x,
                   ((int)gridDim.x - nroll) * (int)blockDim.x);
+        SRBD_RSTAMP(5);
         return;
     }
     __shared__ float e_sh[128];
@@ -619,10 +641,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
         const int voff = (cblk * mc.ldn + k) * 4;
         const float* __restrict__ bl = best + cblk;
         const float* __restrict__ sl = in->sigma + cblk;
+        // slot-major issue order: step n's operands are the first to return (loads complete in order),
+        // so the horizon starts while the later steps' parameters are still in flight
 #pragma unroll
-        for (int l = 0; l < 4; ++l)
+        for (int i = 0; i < NPRE; ++i)
 #pragma unroll
-            for (int i = 0; i < NPRE; ++i) {
+            for (int l = 0; l < 4; ++l) {
                 const int jr = l * PL + (KIND == SRBD_CUBIC_SPLINE ? 10 * (i >> 2) + (i & 3) : i);  // row - cblk
                 const float nzv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, jr * mc.ldn * 4, 0));
                 pre[l][i] = bl[jr] + (zs ? nzv * sl[jr] : nzv);
@@ -684,12 +708,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
     } else {
         for (int n = 0; n < H; ++n) step(n);
     }
+    SRBD_RSTAMP(2);
     cost = (qp<QP_B0>(cost) + qp<QP_B1>(cost)) + qp<QP_B2>(cost);
     cost = cost + in->cost_feet;  // 0, or NaN when a foot term is non-finite (Q_feet = 0)
     if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
     if (valid && q4 == 0 && costs) costs[k] = cost;
     block_epilogue(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh,
                    CEMT);
+    SRBD_RSTAMP(5);
 }
 
 // ------------------------------------------------------------------ merge
@@ -764,12 +790,20 @@ __device__ __forceinline__ void block_topk(const float* __restrict__ recs, int n
 //  4. top-K keys: per-thread sorted lists -> per-wave K-round DPP minima -> one wave over the 16
 //     wave lists; 5. elite rows -> LDS;  6. outputs: rank record and/or final step outputs; with
 //     `chain` the new parameters, sigma and RNG counter are written back into `in` (warm start).
+// Column-split launch (split_cs > 0, final step outputs only): the blocks share no data.  Every block
+// reads all record headers (beta, the sums' normaliser and the top-K are recomputed per block, in the
+// same order, so they agree bit for bit) but only its own columns of the weighted sums and elite rows:
+// block 0 (the tail block) the mc.tailc columns final_grf_pred decodes -- it writes those parameters,
+// the GRFs, the predicted state and the step scalars; block b >= 1 the columns [(b-1)cs, b cs) -- it
+// writes the other parameters and sigma.  Each block publishes flag[blockIdx.x] = seq.  This spreads
+// the record reads over CUs and drops the single block's serial column loop (C2: 8.8 -> see DESIGN).
 __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __restrict__ in,
                                            const float* __restrict__ recs, int nrec, int rec_stride, int rows_in_rec,
                                            const float* __restrict__ noise, float* __restrict__ rank_out,
                                            StepOutput* __restrict__ out, int chain, int ctr_inc,
-                                           uint64_t* __restrict__ dbg, uint32_t* __restrict__ flag, uint32_t seq) {
-    extern __shared__ float smem[];  // scale[nrec_pad] | part[G*(P+1)] | erow[K*P]
+                                           uint64_t* __restrict__ dbg, uint32_t* __restrict__ flag, uint32_t seq,
+                                           int split_cs = 0) {
+    extern __shared__ float smem[];  // scale[nrec_pad] | part[G*(ncol+1)] | erow[K*ncol]
     __shared__ uint64_t red[MERGE_WAVES];
     __shared__ uint64_t wlist[MERGE_WAVES][MAXK];
     __shared__ uint64_t elite[MAXK];
@@ -779,19 +813,28 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     __shared__ float grf_sh[12];
     __shared__ float tag_sh;  // header tag (gait-adaptive step frequency) of the record holding beta's row
 #define MERGE_STAMP(i) \
-    if (dbg && threadIdx.x == 0) dbg[i] = __builtin_amdgcn_s_memrealtime()
+    if (dbg && threadIdx.x == 0 && blockIdx.x == 0) dbg[i] = __builtin_amdgcn_s_memrealtime()
     MERGE_STAMP(0);
 
     const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wv = tid >> 6;
     const int P = mc.P, K = mc.K;
-    const bool rs = mc.method == SRBD_RANDOM_SAMPLING;
-    const int cols = P + 1;
-    if (gridDim.x > 1) {  // first level of a two-level merge: block b reduces its slice into rank_out[b]
+    const bool rs = mc.method == SRBD_RANDOM_SAMPLING, cem = mc.method == SRBD_CEM_MPPI;
+    const bool split = split_cs > 0;
+    const bool tailblk = split && blockIdx.x == 0;
+    if (!split && gridDim.x > 1) {  // first level of a two-level merge: block b reduces its slice into rank_out[b]
         const int b0 = (int)((long)blockIdx.x * nrec / gridDim.x), b1 = (int)((long)(blockIdx.x + 1) * nrec / gridDim.x);
         recs += (size_t)b0 * rec_stride;
         nrec = b1 - b0;
         rank_out += (size_t)blockIdx.x * rec_floats_rank(P, K);
     }
+    // this block's columns: local index i -> parameter column jc(i)
+    const int j0 = split && !tailblk ? ((int)blockIdx.x - 1) * split_cs : 0;
+    const int ncol = !split ? P : (tailblk ? mc.ntail : min(split_cs, P - j0));
+    auto jc = [&](int i) { return tailblk ? (int)mc.tailc[i] : j0 + i; };
+    // parameters this block writes: all (unsplit), the tail columns (tail block), the others (slices)
+    auto owns = [&](int jj) { return !split || tailblk || !is_tail_col(mc, jj); };
+    const bool do_tail = out && (!split || tailblk);
+    const int cols = ncol + 1;
     int G = T / cols;
     G = G < 1 ? 1 : (G > nrec ? nrec : G);
     const int nrec_pad = (nrec + 3) & ~3;
@@ -801,10 +844,10 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
 
     // ---- L: loads.  The StepInput fields the output phases need are fetched here too, so their
     // latency hides under the record loads instead of stalling the tail.
-    const float best_pre = (out && tid < P) ? in->best[tid] : 0.0f;
+    const float best_pre = (out && tid < ncol && owns(jc(tid))) ? in->best[jc(tid)] : 0.0f;
     const int qc = tid < 3 ? tid : 2;  // tail lanes 0..3: component of the four-lane layout
     float tail_pre[13];
-    if (out && tid < 4) {
+    if (do_tail && tid < 4) {
         tail_pre[0] = in->fzref[0];
 #pragma unroll
         for (int l = 0; l < 4; ++l) tail_pre[1 + l] = in->contact[l][0];
@@ -813,7 +856,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
 #pragma unroll
         for (int l = 0; l < 4; ++l) tail_pre[9 + l] = in->state[12 + 3 * l + qc];  // feet
     }
-    const float state_hi = (out && tid >= 12 && tid < 24) ? in->state[tid] : 0.0f;
+    const float state_hi = (do_tail && tid >= 12 && tid < 24) ? in->state[tid] : 0.0f;
     float mr[MERGE_RPT];
     uint64_t mine = KEY_NONE;
     float mtag = 0.0f;
@@ -833,7 +876,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     const int j = tid % cols, g = tid / cols;
     const bool summer = !rs && tid < G * cols;
     const int r0 = summer ? (int)((long)g * nrec / G) : 0, r1 = summer ? (int)((long)(g + 1) * nrec / G) : 0;
-    const int off = j < P ? REC_HDR + j : 1;
+    const int off = j < ncol ? REC_HDR + jc(j) : 1;
     float pv[MERGE_PREF];
 #pragma unroll
     for (int i = 0; i < MERGE_PREF; ++i) pv[i] = (r0 + i < r1) ? recs[(size_t)(r0 + i) * rec_stride + off] : 0.0f;
@@ -881,9 +924,12 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     }
     MERGE_STAMP(2);
 
-    // ---- 4. top-K keys (ascending; keys are unique)
-    if (K == 1) {
+    // ---- 4. top-K keys (ascending; keys are unique).  The tail block of a CEM split never reads
+    // elite rows (sigma belongs to the slices), so it skips them.
+    const bool want_elite = !tailblk || rs;
+    if (K == 1 || !want_elite) {
         if (tid == 0) elite[0] = bkey;
+        for (int e = 1 + tid; e < K; e += T) elite[e] = KEY_NONE;
     } else {
         if (K <= 10)
             block_topk<10>(recs, nrec, rec_stride, P, K, wlist, elite);
@@ -892,7 +938,8 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     }
     __syncthreads();
     // record slot of every elite key (needed when rows travel inside the records)
-    if (rows_in_rec) {
+    const bool need_rows = want_elite && (rs || cem);  // MPPI's update is the weighted sum alone
+    if (rows_in_rec && need_rows) {
         for (int t = tid; t < nrec * K; t += T) {
             const int r = t / K, q = t % K;
             const uint64_t x = rec_key(recs + (size_t)r * rec_stride, P, q);
@@ -903,11 +950,12 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     }
     MERGE_STAMP(3);
 
-    // ---- 5. elite rows -> LDS
+    // ---- 5. elite rows (this block's columns) -> LDS
     int Kv = 0;
     for (int e = 0; e < K; ++e) Kv += elite[e] != KEY_NONE;
-    for (int t = tid; t < K * P; t += T) {
-        const int e = t / P, jj = t % P;
+    const bool zs = zs_scaled(mc, in);
+    for (int t = tid; need_rows && t < K * ncol; t += T) {
+        const int e = t / ncol, i = t % ncol, jj = jc(i);
         float v = 0.0f;
         if (elite[e] != KEY_NONE) {
             if (rows_in_rec) {
@@ -915,7 +963,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
                 v = recs[(size_t)(st / K) * rec_stride + REC_HDR + P + 2 * K + (size_t)(st % K) * P + jj];
             } else {
                 v = noise[(size_t)jj * mc.ldn + ((int)(uint32_t)elite[e] - mc.row0)];
-                if (zs_scaled(mc, in)) v = v * in->sigma[jj];
+                if (zs) v = v * in->sigma[jj];
             }
         }
         erow[t] = v;
@@ -923,13 +971,13 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     __syncthreads();
 
     // ---- 6. outputs
-    if (rank_out) {
+    if (rank_out) {  // unsplit: column i == parameter i
         for (int jj = tid; jj < P; jj += T) rank_out[REC_HDR + jj] = rs ? 0.0f : Vs[jj];
         for (int e = tid; e < K; e += T) {
             rank_out[REC_HDR + P + 2 * e] = u2f((uint32_t)elite[e]);
             rank_out[REC_HDR + P + 2 * e + 1] = u2f((uint32_t)(elite[e] >> 32));
         }
-        for (int t = tid; t < K * P; t += T) rank_out[REC_HDR + P + 2 * K + t] = erow[t];
+        for (int t = tid; t < K * P; t += T) rank_out[REC_HDR + P + 2 * K + t] = need_rows ? erow[t] : 0.0f;
         if (tid == 0) {
             rank_out[0] = beta;
             rank_out[1] = rs ? 1.0f : Vs[P];
@@ -938,18 +986,21 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         }
     }
     if (out) {
-        for (int jj = tid; jj < P; jj += T) {
-            const float b0 = jj == tid ? best_pre : in->best[jj];
-            const float v = rs ? b0 + erow[jj] : b0 + Vs[jj] / Vs[P];
-            nb[jj] = v;
-            out->best[jj] = v;
-            if (mc.method == SRBD_CEM_MPPI) {  // NMPC:1075-1081
+        for (int i = tid; i < ncol; i += T) {
+            const int jj = jc(i);
+            if (owns(jj)) {
+                const float b0 = i == tid ? best_pre : in->best[jj];
+                const float v = rs ? b0 + erow[i] : b0 + Vs[i] / Vs[ncol];
+                nb[jj] = v;
+                out->best[jj] = v;
+            }
+            if (cem && !tailblk) {  // NMPC:1075-1081
                 float s = 0.0f;
-                for (int e = 0; e < Kv; ++e) s = s + erow[e * P + jj];
+                for (int e = 0; e < Kv; ++e) s = s + erow[e * ncol + i];
                 const float mean = s / (float)Kv;
                 float var = 0.0f;
                 for (int e = 0; e < Kv; ++e) {
-                    const float d = erow[e * P + jj] - mean;
+                    const float d = erow[e * ncol + i] - mean;
                     var = var + d * d;
                 }
                 var = var / (float)(Kv - 1);
@@ -962,7 +1013,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         }
         __syncthreads();
         MERGE_STAMP(4);
-        if (tid < 4) {  // final GRFs, one thread per leg (NMPC:695-750)
+        if (do_tail && tid < 4) {  // final GRFs, one thread per leg (NMPC:695-750)
             const int leg = tid;
             const float* pl = nb + leg * mc.PL;
             auto acc = [pl](int jj) { return pl[jj]; };
@@ -975,8 +1026,8 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
             grf_sh[3 * leg + 2] = fz;
         }
         __syncthreads();
-        if (tid < 12) out->grf[tid] = grf_sh[tid];
-        if (tid < 4) {  // predicted state (NMPC:752-784): one Euler step in the four-lane layout
+        if (do_tail && tid < 12) out->grf[tid] = grf_sh[tid];
+        if (do_tail && tid < 4) {  // predicted state (NMPC:752-784): one Euler step in the four-lane layout
             const int c = qc;
             const QuadLane L = quad_lane(mc, c);
             float p = tail_pre[5], v = tail_pre[6], r = tail_pre[7], w = tail_pre[8];
@@ -995,13 +1046,15 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
                 out->pred[9 + c] = w;
             }
         }
-        if (tid >= 12 && tid < 24) out->pred[tid] = state_hi;
-        if (tid == 0) {
+        if (do_tail && tid >= 12 && tid < 24) out->pred[tid] = state_hi;
+        if (do_tail && tid == 0) {
             out->best_cost = beta;
             out->best_index = (int32_t)(uint32_t)bkey;
             out->best_freq = tag_sh;
             out->status = 0;
-            if (chain) in->noise_scaled = 0;  // the chain's next draws come from the device RNG
+            // chain: the next draws come from the device RNG.  (Split: slices read noise_scaled too, but a
+            // chain's steps all run with it 0 already -- reset_noise_scaled -- so this store never changes it.)
+            if (chain) in->noise_scaled = 0;
             if (chain && ctr_inc) {
                 const uint64_t cc = (((uint64_t)in->ctr_hi << 32) | in->ctr_lo) + (uint64_t)ctr_inc;
                 in->ctr_lo = (uint32_t)cc;
@@ -1009,7 +1062,10 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
             }
         }
         if (chain)
-            for (int jj = tid; jj < P; jj += T) in->best[jj] = nb[jj];
+            for (int i = tid; i < ncol; i += T) {
+                const int jj = jc(i);
+                if (owns(jj)) in->best[jj] = nb[jj];
+            }
     }
     MERGE_STAMP(5);
 #undef MERGE_STAMP
@@ -1019,7 +1075,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         if (tid == 0) {
             __threadfence_system();
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(flag + (split ? blockIdx.x : 0), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
@@ -1031,8 +1087,10 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst m
                                                               float* __restrict__ rank_out,
                                                               StepOutput* __restrict__ out, int chain,
                                                               int ctr_inc, uint64_t* __restrict__ dbg,
-                                                              uint32_t* __restrict__ flag, uint32_t seq) {
-    merge_body(mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag, seq);
+                                                              uint32_t* __restrict__ flag, uint32_t seq,
+                                                              int split_cs) {
+    merge_body(mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag, seq,
+               split_cs);
 }
 
 // Sharded step without a collective launch (xGMI exchange).
@@ -1229,12 +1287,31 @@ size_t merge_smem_bytes(int nrec, int P, int K) {
     return sizeof(float) * ((size_t)nrec_pad + MERGE_THREADS + 4 + (size_t)K * P);
 }
 
-void launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
-                  int rows_in_rec, const float* noise, float* rank_out, StepOutput* out, int chain, hipStream_t s,
-                  uint64_t* dbg, int ctr_inc, Publish pub) {
-    hipLaunchKernelGGL(merge_kernel, dim3(1), dim3(MERGE_THREADS), merge_smem_bytes(nrec, mc.P, mc.K), s, mc, in, recs,
-                       nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, chain ? ctr_inc : 0, dbg, pub.flag,
-                       pub.seq);
+int merge_split_cols(const ModelConst& mc) {
+    static const int knob = tune_knob("SRBD_MERGE_SPLIT_COLS", MERGE_SPLIT_COLS);
+    if (knob >= mc.P) return 0;  // 0: one block (SRBD_MERGE_SPLIT_COLS >= P disables the split)
+    const int lo = (mc.P + MERGE_MAX_BLOCKS - 2) / (MERGE_MAX_BLOCKS - 1);  // at most MERGE_MAX_BLOCKS flags
+    return knob > lo ? knob : lo;
+}
+
+int merge_blocks(const ModelConst& mc) {
+    const int cs = merge_split_cols(mc);
+    return cs ? 1 + (mc.P + cs - 1) / cs : 1;
+}
+
+int launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
+                 int rows_in_rec, const float* noise, float* rank_out, StepOutput* out, int chain, hipStream_t s,
+                 uint64_t* dbg, int ctr_inc, Publish pub) {
+    // step outputs only (no rank record): column-split over merge_blocks() blocks when the column work
+    // is large (many records, or CEM's per-column elite statistics); a few hundred MPPI records merge
+    // faster in one block (C2: 157 records, 24.9 vs 25.5 us/step)
+    const bool split = out && !rank_out && (nrec > MERGE_SPLIT_MIN_RECS || mc.method == SRBD_CEM_MPPI);
+    const int cs = split ? merge_split_cols(mc) : 0;
+    const int nb = cs ? merge_blocks(mc) : 1;
+    hipLaunchKernelGGL(merge_kernel, dim3(nb), dim3(MERGE_THREADS), merge_smem_bytes(nrec, mc.P, mc.K), s, mc, in,
+                       recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, chain ? ctr_inc : 0, dbg,
+                       pub.flag, pub.seq, cs);
+    return nb;
 }
 
 // Setup probe of the xGMI mailboxes: slot `rank` word 0 of every mailbox <- rank, flags <- epoch;
@@ -1286,28 +1363,25 @@ int tune_knob(const char* name, int dflt) {
     return (e && atoi(e) > 0) ? atoi(e) : dflt;
 }
 
-int merge_partials(int nrec) {
+int merge_partials(int nrec, bool to_outputs) {
     static const int direct_max = tune_knob("SRBD_MERGE_DIRECT_MAX", MERGE_DIRECT_MAX);
     static const int per_block = tune_knob("SRBD_MERGE_PER_BLOCK", MERGE_PER_BLOCK);
-    if (nrec <= direct_max) return 0;
+    if (nrec <= (to_outputs ? direct_max : MERGE_DIRECT_MAX_RECORD)) return 0;
     int m = (nrec + per_block - 1) / per_block;
     return m > MERGE_MAX_PARTIALS ? MERGE_MAX_PARTIALS : m;
 }
 
-void launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
-                       const float* noise, float* partials, float* rank_out, StepOutput* out, int chain,
-                       hipStream_t s, int ctr_inc, Publish pub) {
-    const int m = merge_partials(nrec);
-    if (m == 0) {
-        launch_merge(mc, in, recs, nrec, rec_stride, 0, noise, rank_out, out, chain, s, nullptr, ctr_inc, pub);
-        return;
-    }
+int launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
+                      const float* noise, float* partials, float* rank_out, StepOutput* out, int chain,
+                      hipStream_t s, int ctr_inc, Publish pub) {
+    const int m = merge_partials(nrec, out && !rank_out);
+    if (m == 0) return launch_merge(mc, in, recs, nrec, rec_stride, 0, noise, rank_out, out, chain, s, nullptr, ctr_inc, pub);
     const int per = (nrec + m - 1) / m;
     hipLaunchKernelGGL(merge_kernel, dim3(m), dim3(MERGE_THREADS), merge_smem_bytes(per, mc.P, mc.K), s, mc, in, recs,
                        nrec, rec_stride, 0, noise, partials, (StepOutput*)nullptr, 0, 0, (uint64_t*)nullptr,
-                       (uint32_t*)nullptr, 0u);
-    launch_merge(mc, in, partials, m, rec_floats_rank(mc.P, mc.K), 1, noise, rank_out, out, chain, s, nullptr, ctr_inc,
-                 pub);
+                       (uint32_t*)nullptr, 0u, 0);
+    return launch_merge(mc, in, partials, m, rec_floats_rank(mc.P, mc.K), 1, noise, rank_out, out, chain, s, nullptr,
+                        ctr_inc, pub);
 }
 
 __global__ void empty_kernel() {}
@@ -1322,3 +1396,15 @@ void launch_div_selftest(const float* a, const float* b, int n, float* o, hipStr
 }
 
 }  // namespace srbd
+
+#ifdef SRBD_ROLLOUT_STAMPS
+// Probe build only: copy out the last rollout launch's block stamps (n <= RSTAMP_BLOCKS * RSTAMP_N).
+extern "C" int srbd_probe_rstamps(uint64_t* host, int n) {
+    if (n > srbd::RSTAMP_BLOCKS * srbd::RSTAMP_N) return -1;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(srbd::g_rstamp), sizeof(uint64_t) * n) == hipSuccess ? 0 : -2;
+}
+extern "C" int srbd_probe_rstamps_clear() {
+    static uint64_t z[srbd::RSTAMP_BLOCKS * srbd::RSTAMP_N];
+    return hipMemcpyToSymbol(HIP_SYMBOL(srbd::g_rstamp), z, sizeof(z)) == hipSuccess ? 0 : -2;
+}
+#endif

@@ -33,18 +33,29 @@ struct Publish {
     uint32_t* flag;
     uint32_t seq;
 };
-// chain != 0: also write the new parameters / sigma / RNG counter back into `in` (device warm start)
-void launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
+// chain != 0: also write the new parameters / sigma / RNG counter back into `in` (device warm start).
+// With step outputs and no rank record the merge is column-split over merge_blocks(mc) blocks, each
+// publishing flag[block]; returns the number of blocks that publish.
+constexpr int MERGE_SPLIT_COLS = 16;  // parameter columns per slice block (SRBD_MERGE_SPLIT_COLS overrides)
+constexpr int MERGE_MAX_BLOCKS = 64;  // publish flags the host context holds
+constexpr int MERGE_SPLIT_MIN_RECS = 256;
+int merge_split_cols(const ModelConst& mc);
+int merge_blocks(const ModelConst& mc);
+int launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                   int rows_in_rec, const float* noise, float* rank_out, StepOutput* out, int chain, hipStream_t s,
                   uint64_t* dbg = nullptr, int ctr_inc = 1, Publish pub = {nullptr, 0});
 // Two-level merge when there are many block records: merge_partials(nrec) first-level blocks each
 // reduce a slice of the records (spreading the record reads over CUs) into rank-format partials,
-// then one block merges the partials.
+// then the partials are merged.
 // Defaults (measured, scripts/kernel_sweep.py); SRBD_MERGE_DIRECT_MAX / SRBD_MERGE_PER_BLOCK override.
-constexpr int MERGE_DIRECT_MAX = 256;
+// Up to 1024 records the column-split merge reads them directly (N = 65 536 quad: CEM cubic H16 90.6 ->
+// 79.0 us/step, MPPI 53.7 -> 52.7); at 4096 the tree is faster (130.8 vs 158.5 us).
+constexpr int MERGE_DIRECT_MAX = 1024;
+constexpr int MERGE_DIRECT_MAX_RECORD = 256;  // merging into a rank record: one block, no split
 constexpr int MERGE_PER_BLOCK = 32;
 constexpr int MERGE_MAX_PARTIALS = 64;
-int merge_partials(int nrec);
+// to_outputs: the merge produces step outputs (column-split final level), else a rank record.
+int merge_partials(int nrec, bool to_outputs);
 // xGMI exchange of rank records (merge_xchg_kernel).  mailbox: this rank's W slots of one rank
 // record each; flags: W epochs (slot r written by rank r); peer_*: every rank's mailbox / flags as
 // this GPU addresses them (IPC-mapped; entry `rank` is the local one).  epoch: this rank's exchange
@@ -67,7 +78,7 @@ void launch_merge_xchg(const ModelConst& mc, StepInput* in, const float* recs, i
                        Publish pub);
 // Integer tuning knob from the environment (read once), else `dflt`.
 int tune_knob(const char* name, int dflt);
-void launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
+int launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                        const float* noise, float* partials, float* rank_out, StepOutput* out, int chain,
                        hipStream_t s, int ctr_inc = 1, Publish pub = {nullptr, 0});
 void launch_advance(const ModelConst& mc, StepInput* in, const StepOutput* out, hipStream_t s);
