@@ -4,7 +4,8 @@ Row a16 of SURVEY 8(a): the producer of the (4, H) contact_sequence the sampling
 Follows quadruped_pympc/helpers/periodic_gait_generator.py: phase offsets per gait (:22-40),
 reset (:41-46), the per-leg loop of run() (:48-76), set_phase_signal (:78-88) and
 compute_contact_sequence (:93-118), leg by leg in plain Python like the reference.
-Only tests/ may import this module; the product's vectorised generator lives in
+Only tests/ may import this module; the product's generator is C++ (srbd_pgg_* in
+include/srbd_host.h, quadruped-pympc-tamols_amd/csrc/srbd_host.cpp) behind
 quadruped_pympc_amd/helpers/periodic_gait_generator.py.
 """
 import numpy as np

@@ -1,4 +1,4 @@
-"""ctypes binding of ``libsrbd_hip.so`` (C-ABI declared in ``include/srbd_mpc.h``).
+"""ctypes binding of ``libsrbd_hip.so`` (C-ABI declared in ``include/srbd_mpc.h`` and ``include/srbd_host.h``).
 
 The library is the only compute path: there is no CPU fallback.  Loading fails
 loudly (ImportError) when the shared object is missing, and creating a context
@@ -102,6 +102,33 @@ SIGNATURES = {
     "srbd_tamols_run": (_I, [_P, _DP, _I, _I, _DP, _DP, _DP, _DP, _IP, _DP, C.POINTER(TamolsParams), _DP, _DP, _IP,
                              _DP, _DP]),
 }
+
+class SrbdPgg(C.Structure):
+    """srbd_pgg (include/srbd_host.h): PeriodicGaitGenerator state."""
+    _fields_ = [("duty_factor", _D), ("step_freq", _D), ("phase_signal", _D * 4), ("phase_offset", _D * 4),
+                ("init", _I * 4), ("gait_type", _I), ("previous_gait_type", _I), ("horizon", _I)]
+
+
+SHM_DOUBLES = 75
+
+
+class ShmMsg(C.Structure):
+    """srbd_shm_msg (include/srbd_host.h): one MPC -> WBC message."""
+    _fields_ = [("grf", _D * 12), ("footholds", _D * 12), ("joints_pos", _D * 12), ("joints_vel", _D * 12),
+                ("joints_acc", _D * 12), ("pred", _D * 12), ("best_freq", _D), ("loop_time", _D), ("stamp", _D)]
+
+
+_U64P = C.POINTER(C.c_uint64)
+SIGNATURES.update({
+    "srbd_pgg_init": (_I, [C.POINTER(SrbdPgg), _I, _D, _D, _I]),
+    "srbd_pgg_reset": (_I, [C.POINTER(SrbdPgg)]),
+    "srbd_pgg_run": (_I, [C.POINTER(SrbdPgg), _D, _D, _DP]),
+    "srbd_pgg_set_phase_signal": (_I, [C.POINTER(SrbdPgg), _DP, _IP]),
+    "srbd_pgg_contact_sequence": (_I, [C.POINTER(SrbdPgg), _DP, _IP, _I, _DP, _I]),
+    "srbd_prepare_state": (_I, [_DP, _DP, _DP, _DP, _I, _FP, _DP, _DP]),
+    "srbd_shm_publish": (_I, [_P, _P, C.POINTER(ShmMsg)]),
+    "srbd_shm_read": (_I, [_P, _P, C.POINTER(ShmMsg), _U64P]),
+})
 
 LIB_NAME = "libsrbd_hip.so"
 LIB_PATH = os.environ.get("SRBD_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)

@@ -250,23 +250,24 @@ class Sampling_MPC:
         """centroidal_nmpc_jax.py:563-627."""
         if self._cfg.mpc_params["shift_solution"]:
             self.best_control_parameters = self.shift_solution(self.best_control_parameters, 1.0 / mpc_frequency)
-        state = np.concatenate(
-            (state_current["position"], state_current["linear_velocity"], state_current["orientation"],
-             state_current["angular_velocity"], state_current["foot_FL"], state_current["foot_FR"],
-             state_current["foot_RL"], state_current["foot_RR"])).reshape((24,))
         legs = ("FL", "FR", "RL", "RR")
-        for leg, name in enumerate(legs):
-            if current_contact[leg] == 0.0:
-                state[12 + 3 * leg:15 + 3 * leg] = reference_state["ref_foot_" + name].reshape((3,))
-        ref = np.concatenate(
+        state_in = np.concatenate(
+            (state_current["position"], state_current["linear_velocity"], state_current["orientation"],
+             state_current["angular_velocity"]) + tuple(state_current["foot_" + n] for n in legs),
+            dtype=np.float64).reshape((24,))
+        ref_in = np.concatenate(
             (reference_state["ref_position"], reference_state["ref_linear_velocity"],
              reference_state["ref_orientation"], reference_state["ref_angular_velocity"])
-            + tuple(reference_state["ref_foot_" + n].reshape((3,)) for n in legs)).reshape((24,))
+            + tuple(reference_state["ref_foot_" + n].reshape((3,)) for n in legs), dtype=np.float64).reshape((24,))
+        # swing-foot substitution and lift-off zeroing in the C++ host producer (include/srbd_host.h)
         self.best_control_parameters = np.array(self.best_control_parameters, dtype=f32)
-        PL = self.num_control_parameters_single_leg
-        for leg in range(4):
-            if previous_contact[leg] == 1 and current_contact[leg] == 0:
-                self.best_control_parameters[leg * PL:(leg + 1) * PL] = 0.0
+        cur = np.ascontiguousarray(current_contact, dtype=np.float64)
+        prev = np.ascontiguousarray(previous_contact, dtype=np.float64)
+        state, ref = np.empty(24), np.empty(24)
+        _lib.check(_lib.lib.srbd_prepare_state(_lib.dptr(state_in), _lib.dptr(ref_in), _lib.dptr(cur),
+                                               _lib.dptr(prev), self.num_control_parameters_single_leg,
+                                               _lib.fptr(self.best_control_parameters), _lib.dptr(state),
+                                               _lib.dptr(ref)), what="srbd_prepare_state")
         return state, ref
 
     def reset(self):

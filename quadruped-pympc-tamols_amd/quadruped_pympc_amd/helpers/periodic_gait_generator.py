@@ -1,77 +1,90 @@
 """Periodic gait generator: the producer of the (4, H) ``contact_sequence`` the sampling MPC consumes.
 
-Behaviour of ``quadruped_pympc/helpers/periodic_gait_generator.py`` (reference):
-phase offsets per gait (:22-46), the per-leg phase/duty-factor contact rule with
-its start-up ``init`` hold (:48-76), and the look-ahead sequence
-(:93-118, full stance returns 2H ones).  Vectorised over the four legs.
+Mirror of ``quadruped_pympc/helpers/periodic_gait_generator.py`` (reference): the same
+constructor, attributes and methods (phase offsets per gait :22-46, ``run`` :48-76,
+``set_phase_signal`` :78-87, ``compute_contact_sequence`` :93-118, full stance -> 2H ones).
+The state lives in a ``srbd_pgg`` struct and every method runs in ``libsrbd_hip.so``'s C++
+host producers (``include/srbd_host.h``), so the 100 Hz loop pays one
+ctypes call per sequence instead of H NumPy passes.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
+
+from .. import _lib
 
 TROT, PACE, BOUNDING, CIRCULARCRAWL, BFDIAGONALCRAWL, BACKDIAGONALCRAWL, FRONTDIAGONALCRAWL, FULL_STANCE = range(8)
 
-PHASE_OFFSETS = {
-    TROT: (0.5, 1.0, 1.0, 0.5),
-    PACE: (0.8, 0.3, 0.8, 0.3),
-    BOUNDING: (0.5, 0.5, 0.0, 0.0),
-    CIRCULARCRAWL: (0.0, 0.25, 0.75, 0.5),
-    BFDIAGONALCRAWL: (0.0, 0.25, 0.5, 0.75),
-    BACKDIAGONALCRAWL: (0.0, 0.5, 0.75, 0.25),
-    FRONTDIAGONALCRAWL: (0.5, 1.0, 0.75, 1.25),
-}
+
+def _check(rc, what):
+    if rc < 0:
+        raise ValueError(f"{what} failed ({rc})")
+    return rc
 
 
 class PeriodicGaitGenerator:
     def __init__(self, duty_factor, step_freq, gait_type, horizon):
-        self.duty_factor = duty_factor
-        self.step_freq = step_freq
-        self.horizon = horizon
-        self.gait_type = int(getattr(gait_type, "value", gait_type))
-        self.previous_gait_type = self.gait_type
-        self.reset()
+        self._g = _lib.SrbdPgg()
+        self._gp = C.byref(self._g)
+        _check(_lib.lib.srbd_pgg_init(self._gp, int(getattr(gait_type, "value", gait_type)), float(duty_factor),
+                                      float(step_freq), int(horizon)), "srbd_pgg_init")
+        self.start_and_stop_activated = False
+        self.time_before_switch_freq = 0
+        self._seq_key = None  # (dts, lens) bytes of the cached sequence-call arguments
+        self._out = np.empty(8 * _lib.MAX_HORIZON)
+        self._out_p = _lib.dptr(self._out)
+
+    # plain attributes of the reference, backed by the C struct
+    duty_factor = property(lambda s: s._g.duty_factor, lambda s, v: setattr(s._g, "duty_factor", float(v)))
+    step_freq = property(lambda s: s._g.step_freq, lambda s, v: setattr(s._g, "step_freq", float(v)))
+    horizon = property(lambda s: s._g.horizon, lambda s, v: setattr(s._g, "horizon", int(v)))
+    gait_type = property(lambda s: s._g.gait_type, lambda s, v: setattr(s._g, "gait_type", int(getattr(v, "value", v))))
+    previous_gait_type = property(lambda s: s._g.previous_gait_type,
+                                  lambda s, v: setattr(s._g, "previous_gait_type", int(getattr(v, "value", v))))
+    n_contact = 4
+
+    @property
+    def phase_offset(self):
+        return list(self._g.phase_offset)
+
+    @property
+    def _init(self):
+        return np.array(self._g.init, dtype=bool)
 
     def reset(self):
-        self.phase_offset = list(PHASE_OFFSETS.get(self.gait_type, (0.0, 0.5, 0.5, 0.0)))
-        self._phase_signal = np.asarray(self.phase_offset, dtype=np.float64).copy()
-        self._init = np.zeros(4, dtype=bool)
-        self.n_contact = 4
+        _lib.lib.srbd_pgg_reset(self._gp)
         self.time_before_switch_freq = 0
 
     def run(self, dt, new_step_freq):
-        ph = (self._phase_signal + dt * new_step_freq) % 1.0
-        off = np.asarray(self.phase_offset)
-        holding = self._init & (ph <= off)
-        releasing = self._init & ~(ph <= off)
-        contact = np.where(self._init, 1.0, (ph < self.duty_factor).astype(np.float64))
-        ph = np.where(releasing, 0.0, ph)
-        self._init = holding
-        self._phase_signal = ph
-        return contact
+        out = np.zeros(4)
+        _lib.lib.srbd_pgg_run(self._gp, float(dt), float(new_step_freq), _lib.dptr(out))
+        return out
 
     def set_phase_signal(self, phase_signal, init=None):
         assert len(phase_signal) == 4
-        self._phase_signal = np.asarray(phase_signal, dtype=np.float64).copy()
-        self._init = np.zeros(4, dtype=bool) if init is None else np.asarray(init, dtype=bool).copy()
+        ph = np.ascontiguousarray(phase_signal, dtype=np.float64)
+        ini = None if init is None else np.ascontiguousarray(init, dtype=np.int32)
+        _lib.lib.srbd_pgg_set_phase_signal(self._gp, _lib.dptr(ph), _lib.iptr(ini))
 
     @property
     def phase_signal(self):
-        return np.array(self._phase_signal)
+        return np.array(self._g.phase_signal)
 
     def compute_contact_sequence(self, contact_sequence_dts, contact_sequence_lenghts):
-        if self.gait_type == FULL_STANCE:
-            self.reset()
-            return np.ones((4, self.horizon * 2))
-        t0, i0 = self._phase_signal.copy(), self._init.copy()
-        seq = np.zeros((4, self.horizon))
-        seq[:, 0] = self.run(0.0, self.step_freq)
-        j = 0
-        for i in range(1, self.horizon):
-            if i >= contact_sequence_lenghts[j]:
-                j += 1
-            seq[:, i] = self.run(contact_sequence_dts[j], self.step_freq)
-        self.set_phase_signal(t0, i0)
-        return seq
+        key = (np.asarray(contact_sequence_dts, dtype=np.float64).tobytes(),
+               np.asarray(contact_sequence_lenghts, dtype=np.int32).tobytes())
+        if key != self._seq_key:  # the 100 Hz caller passes the same arrays every step
+            self._dts = np.frombuffer(key[0], dtype=np.float64).copy()
+            self._lens = np.frombuffer(key[1], dtype=np.int32).copy()
+            self._dts_p, self._lens_p = _lib.dptr(self._dts), _lib.iptr(self._lens)
+            self._seq_key = key
+        H = self._g.horizon
+        cols = _check(_lib.lib.srbd_pgg_contact_sequence(self._gp, self._dts_p, self._lens_p, len(self._dts),
+                                                         self._out_p, min(self._out.size, 8 * H)),
+                      "compute_contact_sequence")
+        return self._out[:4 * cols].reshape(4, cols).copy()  # row-major 4 x cols
 
     def set_full_stance(self):
         self.gait_type = FULL_STANCE

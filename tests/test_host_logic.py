@@ -66,6 +66,26 @@ def test_pgg_full_stance_sequence():
     assert a.gait_type == 0
 
 
+def test_pgg_c_abi_argument_checks():
+    import ctypes as C
+    g = _lib.SrbdPgg()
+    assert _lib.lib.srbd_pgg_init(C.byref(g), 0, 0.65, 1.4, 0) == _lib.E_INVALID  # horizon < 1
+    assert _lib.lib.srbd_pgg_init(C.byref(g), 0, 0.65, 1.4, 12) == _lib.OK
+    out = np.zeros(4 * 12)
+    dts, lens = np.array([0.02]), np.array([5], np.int32)  # the reference would run past its dts list
+    assert _lib.lib.srbd_pgg_contact_sequence(C.byref(g), _lib.dptr(dts), _lib.iptr(lens), 1, _lib.dptr(out),
+                                              out.size) == _lib.E_INVALID
+    assert list(g.phase_signal) == [0.5, 1.0, 1.0, 0.5]  # state restored after the failure
+    lens[0] = 12
+    assert _lib.lib.srbd_pgg_contact_sequence(C.byref(g), _lib.dptr(dts), _lib.iptr(lens), 1, _lib.dptr(out),
+                                              out.size - 1) == _lib.E_INVALID  # capacity
+    assert _lib.lib.srbd_pgg_contact_sequence(C.byref(g), _lib.dptr(dts), _lib.iptr(lens), 1, _lib.dptr(out),
+                                              out.size) == 12
+    z = np.zeros(24)
+    assert _lib.lib.srbd_prepare_state(None, _lib.dptr(z), None, None, 36, None, _lib.dptr(z),
+                                       _lib.dptr(z)) == _lib.E_INVALID
+
+
 # ---------------------------------------------------------------- LegsAttr / config
 def test_legs_attr():
     la = LegsAttr(FL=1, FR=2, RL=3, RR=4)
