@@ -16,6 +16,7 @@
  *                             (row-sharded rollouts)
  *   srbd_tamols_run        <- VisualFootholdAdaptation.compute_adaptation, strategy 'tamols'
  *                             visual_foothold_adaptation.py:153-231 (+ helpers :261-714)
+ *   srbd_terrain_patches   <- gym_quadruped HeightMap.update_height_map (wb_interface.py:233-234)
  *
  * Conventions: plain pointers and sizes, caller owns every host array, nothing is
  * retained past a call, 0 = success and negative SRBD_E* codes on failure (message
@@ -244,6 +245,48 @@ int srbd_tamols_run(srbd_tamols_ctx* ctx, const double* heightmaps, int32_t rows
                     const double* hips, const double* forward_vel, const double* base_pos, const int32_t* contact,
                     const double* feet, const srbd_tamols_params* params, double* out_footholds, double* out_boxes,
                     int32_t* out_valid, double* out_scores, double* out_seed_heights);
+
+/* ------------------------------------------------------------------ terrain heightmap patches
+ * GPU producer of the per-leg heightmap patches TAMOLS consumes: replaces
+ * gym_quadruped's HeightMap.update_height_map (a MuJoCo mj_ray per patch point on the CPU; called at
+ * quadruped_pympc/interfaces/wb_interface.py:233-234 with HeightMap(13, 7, 0.04, 0.04), simulation.py
+ * :490-511).  The scene is uploaded once; every patch point casts a vertical ray down from ray_z and
+ * takes the highest surface at or below ray_z: the ground plane, the top face of a box (yawed about
+ * z) or of an upright cylinder, or a height field (cells split along the (i, j)-(i+1, j+1) diagonal).
+ * A ray that hits nothing reports miss_z.  Patch point (i, j) of a patch centred at c with yaw psi:
+ *   dx = (i - (rows - 1) / 2) * dist_x,  dy = (j - (cols - 1) / 2) * dist_y,
+ *   x = c.x + cos(psi) dx - sin(psi) dy,  y = c.y + sin(psi) dx + cos(psi) dy   (float64).
+ * gym_quadruped is absent here, so this layout is the one our PatchHeightMap uses (parity unpinned
+ * against the real sensor; pinned against oracle/terrain_oracle.py bit for bit). */
+enum { SRBD_PRIM_BOX = 0, SRBD_PRIM_CYLINDER = 1 };
+typedef struct srbd_terrain_prim {
+    int32_t type, pad;
+    double cx, cy, cz; /* centre */
+    double a, b, c;    /* box: half sizes x, y, z;  cylinder: radius, unused, half height */
+    double yaw;        /* box rotation about z (radians) */
+} srbd_terrain_prim;
+
+typedef struct srbd_terrain srbd_terrain;
+
+/* hfield: hf_nx x hf_ny heights, row-major [ix][iy], point (ix, iy) at (hf_x0 + ix hf_dx, hf_y0 + iy hf_dy);
+ * NULL for none.  has_ground: a plane at ground_z. */
+int srbd_terrain_create(int32_t device_id, const srbd_terrain_prim* prims, int32_t nprims, int32_t has_ground,
+                        double ground_z, const double* hfield, int32_t hf_nx, int32_t hf_ny, double hf_x0,
+                        double hf_y0, double hf_dx, double hf_dy, double miss_z, srbd_terrain** out);
+void srbd_terrain_destroy(srbd_terrain* terrain);
+const char* srbd_terrain_last_error(const srbd_terrain* terrain);
+/* npatch patches (centres npatch x 3, yaws npatch) -> out npatch x rows x cols x 3 (x, y, z). */
+int srbd_terrain_patches(srbd_terrain* terrain, const double* centers, const double* yaws, int32_t npatch,
+                         int32_t rows, int32_t cols, double dist_x, double dist_y, double ray_z, double* out);
+/* srbd_tamols_run with the four patches raycast on the device from `terrain` (centres = the seeds,
+ * one yaw) in the same stream: no host round trip of the patch.  out_heightmaps (4 x rows x cols x 3)
+ * may be NULL. */
+int srbd_tamols_run_terrain(srbd_tamols_ctx* ctx, srbd_terrain* terrain, double yaw, int32_t rows, int32_t cols,
+                            double dist_x, double dist_y, double ray_z, const double* seeds, const double* hips,
+                            const double* forward_vel, const double* base_pos, const int32_t* contact,
+                            const double* feet, const srbd_tamols_params* params, double* out_footholds,
+                            double* out_boxes, int32_t* out_valid, double* out_scores, double* out_seed_heights,
+                            double* out_heightmaps);
 
 #ifdef __cplusplus
 }

@@ -1388,6 +1388,13 @@ extern "C" const char* srbd_tamols_last_error(const srbd_tamols_ctx* t) {
         }                                                                                           \
     } while (0)
 
+static int tamols_reserve(srbd_tamols_ctx* t, int nc);
+// The TAMOLS launch on a device heightmap buffer `d_hm` (4 x nc x 3) already ordered on t->stream.
+static int tamols_enqueue(srbd_tamols_ctx* t, const double* d_hm, int32_t rows, int32_t cols, const double* seeds,
+                          const double* hips, const double* vel, const double* base, const int32_t* contact,
+                          const double* feet, const srbd_tamols_params* p, double* out_fh, double* out_box,
+                          int32_t* out_valid, double* out_scores, double* out_seedh);
+
 extern "C" int srbd_tamols_run(srbd_tamols_ctx* t, const double* hm, int32_t rows, int32_t cols, const double* seeds,
                                const double* hips, const double* vel, const double* base, const int32_t* contact,
                                const double* feet, const srbd_tamols_params* p, double* out_fh, double* out_box,
@@ -1399,6 +1406,13 @@ extern "C" int srbd_tamols_run(srbd_tamols_ctx* t, const double* hm, int32_t row
         return SRBD_E_INVALID;
     }
     TAM_TRY(t, hipSetDevice(t->device));
+    if (int rc = tamols_reserve(t, nc)) return rc;
+    TAM_TRY(t, hipMemcpyAsync(t->d_hm, hm, sizeof(double) * 12 * nc, hipMemcpyHostToDevice, t->stream));
+    return tamols_enqueue(t, t->d_hm, rows, cols, seeds, hips, vel, base, contact, feet, p, out_fh, out_box,
+                          out_valid, out_scores, out_seedh);
+}
+
+static int tamols_reserve(srbd_tamols_ctx* t, int nc) {
     if (t->cap_cand < (size_t)nc) {
         (void)hipFree(t->d_hm);
         (void)hipFree(t->d_out);
@@ -1407,6 +1421,14 @@ extern "C" int srbd_tamols_run(srbd_tamols_ctx* t, const double* hm, int32_t row
         TAM_TRY(t, hipMalloc((void**)&t->d_out, sizeof(double) * (4 * (size_t)nc + 12 + 24 + 4)));
         t->cap_cand = nc;
     }
+    return SRBD_OK;
+}
+
+static int tamols_enqueue(srbd_tamols_ctx* t, const double* d_hm, int32_t rows, int32_t cols, const double* seeds,
+                          const double* hips, const double* vel, const double* base, const int32_t* contact,
+                          const double* feet, const srbd_tamols_params* p, double* out_fh, double* out_box,
+                          int32_t* out_valid, double* out_scores, double* out_seedh) {
+    const int nc = rows * cols;
     TamolsArgs a;
     memset(&a, 0, sizeof(a));
     a.rows = rows;
@@ -1430,8 +1452,7 @@ extern "C" int srbd_tamols_run(srbd_tamols_ctx* t, const double* hm, int32_t row
     double* d_fh = d_scores + 4 * (size_t)nc;
     double* d_box = d_fh + 12;
     double* d_seedh = d_box + 24;
-    TAM_TRY(t, hipMemcpyAsync(t->d_hm, hm, sizeof(double) * 12 * nc, hipMemcpyHostToDevice, t->stream));
-    launch_tamols(a, t->d_hm, d_scores, d_fh, d_box, t->d_valid, d_seedh, t->stream);
+    launch_tamols(a, d_hm, d_scores, d_fh, d_box, t->d_valid, d_seedh, t->stream);
     TAM_TRY(t, hipGetLastError());
     TAM_TRY(t, hipMemcpyAsync(out_fh, d_fh, sizeof(double) * 12, hipMemcpyDeviceToHost, t->stream));
     TAM_TRY(t, hipMemcpyAsync(out_box, d_box, sizeof(double) * 24, hipMemcpyDeviceToHost, t->stream));
@@ -1441,4 +1462,35 @@ extern "C" int srbd_tamols_run(srbd_tamols_ctx* t, const double* hm, int32_t row
     if (out_seedh) TAM_TRY(t, hipMemcpyAsync(out_seedh, d_seedh, sizeof(double) * 4, hipMemcpyDeviceToHost, t->stream));
     TAM_TRY(t, hipStreamSynchronize(t->stream));
     return SRBD_OK;
+}
+
+// TAMOLS on patches raycast from a device terrain in the same stream (centres = the seeds).
+extern "C" int srbd_tamols_run_terrain(srbd_tamols_ctx* t, srbd_terrain* ter, double yaw, int32_t rows, int32_t cols,
+                                       double dist_x, double dist_y, double ray_z, const double* seeds,
+                                       const double* hips, const double* vel, const double* base,
+                                       const int32_t* contact, const double* feet, const srbd_tamols_params* p,
+                                       double* out_fh, double* out_box, int32_t* out_valid, double* out_scores,
+                                       double* out_seedh, double* out_hm) {
+    if (!t || !ter || !seeds || !hips || !p || !out_fh || !out_box || !out_valid) return SRBD_E_INVALID;
+    const int nc = rows * cols;
+    if (rows < 1 || cols < 1 || nc > TAMOLS_MAXCAND) {
+        t->err = "patch must have 1..320 points";
+        return SRBD_E_INVALID;
+    }
+    if (ter->device != t->device) {
+        t->err = "terrain and TAMOLS contexts are on different devices";
+        return SRBD_E_INVALID;
+    }
+    TAM_TRY(t, hipSetDevice(t->device));
+    if (int rc = tamols_reserve(t, nc)) return rc;
+    const double yaws[4] = {yaw, yaw, yaw, yaw};
+    double* d_hm = nullptr;
+    if (terrain_enqueue(ter, seeds, yaws, 4, rows, cols, dist_x, dist_y, ray_z, t->stream, &d_hm)) {
+        t->err = ter->err;
+        return SRBD_E_HIP;
+    }
+    if (out_hm)
+        TAM_TRY(t, hipMemcpyAsync(out_hm, d_hm, sizeof(double) * 12 * nc, hipMemcpyDeviceToHost, t->stream));
+    return tamols_enqueue(t, d_hm, rows, cols, seeds, hips, vel, base, contact, feet, p, out_fh, out_box, out_valid,
+                          out_scores, out_seedh);
 }

@@ -1,6 +1,9 @@
 // srbd_launch.h -- internal launchers shared by srbd_kernels.hip, tamols_kernel.hip and srbd_api.hip.
 #pragma once
 
+#include <string>
+#include <vector>
+
 #include "srbd_core.h"
 
 namespace srbd {
@@ -97,6 +100,50 @@ struct TamolsArgs {
     double feet[12], seeds[12], hips[12];
     srbd_tamols_params p;
 };
+
+// Terrain raycast (terrain_kernel.hip).  Device scene: primitives with the box yaw's cos / sin
+// precomputed on the host (prim.pad unused).
+struct TerrainDev {
+    const srbd_terrain_prim* prims;
+    const double* cs;  // nprims x (cos yaw, sin yaw)
+    int nprims;
+    int has_ground;
+    double ground_z, miss_z;
+    const double* hf;
+    int hf_nx, hf_ny;
+    double hf_x0, hf_y0, hf_dx, hf_dy;
+};
+// Patch p: centre centers[3p..], yaw cos / sin in cs_yaw[2p..] (device arrays).
+struct PatchJob {
+    const double* centers;
+    const double* cs_yaw;
+    int npatch, rows, cols;
+    double dist_x, dist_y, ray_z;
+    double* out;  // npatch x rows x cols x 3
+};
+void launch_terrain_patches(const TerrainDev& t, const PatchJob& j, hipStream_t s);
+
+}  // namespace srbd
+
+// Device-resident terrain scene (opaque in the C-ABI).
+struct srbd_terrain {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    srbd_terrain_prim* d_prims = nullptr;
+    double* d_cs = nullptr;
+    double* d_hf = nullptr;
+    double* d_job = nullptr;  // centres | yaw cos, sin
+    double* d_out = nullptr;
+    size_t cap_job = 0, cap_out = 0;
+    std::vector<double> h_job;
+    srbd::TerrainDev dev{};
+    std::string err;
+};
+
+namespace srbd {
+// Raycast npatch patches on stream s into the scene's device output buffer (*d_out).
+int terrain_enqueue(srbd_terrain* t, const double* centers, const double* yaws, int npatch, int rows, int cols,
+                    double dist_x, double dist_y, double ray_z, hipStream_t s, double** d_out);
 
 size_t tamols_smem_bytes(int ncand);
 void launch_tamols(const TamolsArgs& a, const double* hm, double* scores, double* footholds, double* boxes,

@@ -118,6 +118,13 @@ class ShmMsg(C.Structure):
                 ("joints_acc", _D * 12), ("pred", _D * 12), ("best_freq", _D), ("loop_time", _D), ("stamp", _D)]
 
 
+class TerrainPrim(C.Structure):
+    """srbd_terrain_prim (include/srbd_mpc.h)."""
+    _fields_ = [("type", _I), ("pad", _I), ("cx", _D), ("cy", _D), ("cz", _D), ("a", _D), ("b", _D), ("c", _D),
+                ("yaw", _D)]
+
+
+PRIM_BOX, PRIM_CYLINDER = 0, 1
 _U64P = C.POINTER(C.c_uint64)
 SIGNATURES.update({
     "srbd_pgg_init": (_I, [C.POINTER(SrbdPgg), _I, _D, _D, _I]),
@@ -128,6 +135,13 @@ SIGNATURES.update({
     "srbd_prepare_state": (_I, [_DP, _DP, _DP, _DP, _I, _FP, _DP, _DP]),
     "srbd_shm_publish": (_I, [_P, _P, C.POINTER(ShmMsg)]),
     "srbd_shm_read": (_I, [_P, _P, C.POINTER(ShmMsg), _U64P]),
+    "srbd_terrain_create": (_I, [_I, C.POINTER(TerrainPrim), _I, _I, _D, _DP, _I, _I, _D, _D, _D, _D, _D,
+                                 C.POINTER(_P)]),
+    "srbd_terrain_destroy": (None, [_P]),
+    "srbd_terrain_last_error": (C.c_char_p, [_P]),
+    "srbd_terrain_patches": (_I, [_P, _DP, _DP, _I, _I, _I, _D, _D, _D, _DP]),
+    "srbd_tamols_run_terrain": (_I, [_P, _P, _D, _I, _I, _D, _D, _D, _DP, _DP, _DP, _DP, _IP, _DP,
+                                     C.POINTER(TamolsParams), _DP, _DP, _IP, _DP, _DP, _DP]),
 })
 
 LIB_NAME = "libsrbd_hip.so"

@@ -1,14 +1,25 @@
-"""Synthetic terrains and a heightmap-patch producer (stand-in for gym_quadruped's HeightMap).
+"""Terrains and heightmap-patch producers (stand-ins for gym_quadruped's HeightMap).
 
 The reference samples a 13 x 7 patch at 0.04 m around each reference foothold with
-MuJoCo ray casts (simulation.py:490-511, wb_interface.py:233-234).  Here the patch
-is sampled from an analytic height field: ``flat`` or ``stepping_stones_medium``
-(stones of radius 0.15 m, 0.40 m apart, 3 per row, alternate rows offset, top
-+0.05 m, gaps at -0.5 m; geometry from docs/STEPPING_STONES_TERRAIN.md:9-50).
+MuJoCo ray casts (simulation.py:490-511, wb_interface.py:233-234).  Two producers here:
+
+* ``GpuTerrain`` / ``GpuHeightMap``: the scene (ground plane, boxes, upright cylinders, a
+  height field) lives on the GPU and every patch point is one lane's vertical ray cast
+  (``srbd_terrain_patches``, terrain_kernel.hip).  ``TamolsSearch.run_terrain``
+  feeds the raycast patches straight into the TAMOLS kernel without a host round trip.
+* ``PatchHeightMap``: the same patch layout sampled from an analytic height function on the host
+  (``flat`` or ``stepping_stones_medium``: stones of radius 0.15 m, 0.40 m apart, 3 per row,
+  alternate rows offset, top +0.05 m, gaps at -0.5 m; geometry from
+  docs/STEPPING_STONES_TERRAIN.md:9-50).  ``stepping_stones_scene`` builds the equivalent
+  primitive scene for the GPU.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
+
+from .. import _lib
 
 
 def flat(height: float = 0.0):
@@ -66,3 +77,94 @@ class PatchHeightMap:
         pts = self.data[:, :, 0, :].reshape(-1, 3)
         d = (pts[:, 0] - target[0]) ** 2 + (pts[:, 1] - target[1]) ** 2
         return pts[int(np.argmin(d)), 2] + 0.02
+
+
+def stepping_stones_scene(radius=0.15, spacing=0.40, per_row=3, top=0.05, gap=-0.5, x0=0.4, n_rows=20,
+                          platform_from=-10.0):
+    """Primitive scene of ``stepping_stones`` for ``GpuTerrain``: ``n_rows`` rows of upright cylinders
+    (top ``top``), the start platform as a box with top 0 over [platform_from, x0], the gaps as the
+    ground plane at ``gap``.  Equal to the analytic terrain except within one stone radius before the
+    platform edge, where the analytic function lets the platform (z = 0) cut the first row's stones and
+    the scene keeps their tops (+0.05)."""
+    ys = (np.arange(per_row) - (per_row - 1) / 2) * spacing
+    prims = []
+    for row in range(n_rows):
+        shift = spacing / 2 if row % 2 == 1 else 0.0
+        for yc in ys:
+            prims.append(dict(type=_lib.PRIM_CYLINDER, cx=x0 + row * spacing, cy=float(yc + shift), cz=0.0,
+                              a=radius, b=0.0, c=top, yaw=0.0))
+    half = (x0 - platform_from) / 2
+    prims.append(dict(type=_lib.PRIM_BOX, cx=platform_from + half, cy=0.0, cz=-0.25, a=half, b=50.0, c=0.25, yaw=0.0))
+    return dict(prims=prims, has_ground=True, ground_z=gap)
+
+
+class GpuTerrain:
+    """A device-resident scene (``srbd_terrain``); ``patches`` casts one vertical ray per patch point."""
+
+    def __init__(self, prims=(), has_ground=True, ground_z=0.0, hfield=None, miss_z=float("nan"), device_id=0):
+        prims = list(prims)
+        arr = (_lib.TerrainPrim * max(1, len(prims)))()
+        for i, p in enumerate(prims):
+            arr[i] = _lib.TerrainPrim(int(p["type"]), 0, float(p["cx"]), float(p["cy"]), float(p["cz"]),
+                                      float(p["a"]), float(p.get("b", 0.0)), float(p["c"]), float(p.get("yaw", 0.0)))
+        hf = None
+        nx = ny = 0
+        x0 = y0 = dx = dy = 0.0
+        if hfield is not None:
+            hf = np.ascontiguousarray(hfield["z"], dtype=np.float64)
+            nx, ny = hf.shape
+            x0, y0, dx, dy = (float(hfield[k]) for k in ("x0", "y0", "dx", "dy"))
+        h = C.c_void_p()
+        rc = _lib.lib.srbd_terrain_create(int(device_id), arr, len(prims), int(bool(has_ground)), float(ground_z),
+                                          _lib.dptr(hf), nx, ny, x0, y0, dx, dy, float(miss_z), C.byref(h))
+        if rc != _lib.OK:
+            msg = _lib.lib.srbd_terrain_last_error(None)
+            raise RuntimeError(f"srbd_terrain_create failed ({rc}): {msg.decode() if msg else ''}")
+        self.h = h
+
+    @classmethod
+    def stepping_stones(cls, device_id=0, **kw):
+        return cls(device_id=device_id, **stepping_stones_scene(**kw))
+
+    def patches(self, centers, yaws, rows=13, cols=7, dist_x=0.04, dist_y=0.04, ray_z=10.0) -> np.ndarray:
+        """(npatch, rows, cols, 3) points (x, y, z) around each centre (rows along the yawed x axis)."""
+        c = np.ascontiguousarray(centers, dtype=np.float64).reshape(-1, 3)
+        y = np.ascontiguousarray(np.broadcast_to(np.asarray(yaws, dtype=np.float64), (c.shape[0],)))
+        out = np.empty((c.shape[0], rows, cols, 3))
+        rc = _lib.lib.srbd_terrain_patches(self.h, _lib.dptr(c), _lib.dptr(y), c.shape[0], rows, cols, float(dist_x),
+                                           float(dist_y), float(ray_z), _lib.dptr(out))
+        if rc != _lib.OK:
+            msg = _lib.lib.srbd_terrain_last_error(self.h)
+            raise RuntimeError(f"srbd_terrain_patches failed ({rc}): {msg.decode() if msg else ''}")
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.lib.srbd_terrain_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class GpuHeightMap:
+    """``HeightMap``-like object over a ``GpuTerrain``: ``update_height_map`` raycasts the patch on the GPU;
+    ``.data`` is (rows, cols, 1, 3); ``get_height`` is nearest-point height + 0.02, as ``PatchHeightMap``."""
+
+    def __init__(self, terrain: GpuTerrain, num_rows=13, num_cols=7, dist_x=0.04, dist_y=0.04, ray_z=10.0):
+        self.terrain = terrain
+        self.num_rows, self.num_cols, self.dist_x, self.dist_y, self.ray_z = num_rows, num_cols, dist_x, dist_y, ray_z
+        self.data = None
+
+    def update_height_map(self, center, yaw=0.0):
+        c = np.asarray(center, dtype=np.float64).reshape(-1)[:3]
+        if c.size < 3:
+            c = np.concatenate([c, np.zeros(3 - c.size)])
+        p = self.terrain.patches(c[None], [yaw], self.num_rows, self.num_cols, self.dist_x, self.dist_y, self.ray_z)
+        self.data = p[0][:, :, None, :]
+        return self.data
+
+    get_height = PatchHeightMap.get_height

@@ -104,6 +104,30 @@ class TamolsSearch:
                     scores=scores.reshape(4, rows * cols), seed_heights=seedh)
 
 
+    def run_terrain(self, terrain, yaw, seeds, hips, params, rows=13, cols=7, dist_x=0.04, dist_y=0.04, ray_z=10.0,
+                    forward_vel=None, base_position=None, current_contact=None, current_feet_pos=None):
+        """``run`` on patches raycast from a ``GpuTerrain`` around the seeds, in the same stream as the search
+        (``srbd_tamols_run_terrain``).  The result also holds the patches (``heightmaps``, (4, rows, cols, 3))."""
+        seeds = np.ascontiguousarray(seeds, dtype=np.float64).reshape(12)
+        hips = np.ascontiguousarray(hips, dtype=np.float64).reshape(12)
+        vel = None if forward_vel is None else np.ascontiguousarray(np.asarray(forward_vel, np.float64)[:3])
+        base = None if base_position is None else np.ascontiguousarray(np.asarray(base_position, np.float64)[:3])
+        contact = None if current_contact is None else np.ascontiguousarray(current_contact, dtype=np.int32)
+        feet = None if current_feet_pos is None else np.ascontiguousarray(current_feet_pos, dtype=np.float64).reshape(12)
+        fh, boxes, valid = np.zeros(12), np.zeros(24), np.zeros(4, dtype=np.int32)
+        scores, seedh, hm = np.zeros(4 * rows * cols), np.zeros(4), np.zeros((4, rows, cols, 3))
+        rc = _lib.lib.srbd_tamols_run_terrain(self.h, terrain.h, float(yaw), rows, cols, float(dist_x), float(dist_y),
+                                              float(ray_z), _lib.dptr(seeds), _lib.dptr(hips), _lib.dptr(vel),
+                                              _lib.dptr(base), _lib.iptr(contact), _lib.dptr(feet), C.byref(params),
+                                              _lib.dptr(fh), _lib.dptr(boxes), _lib.iptr(valid), _lib.dptr(scores),
+                                              _lib.dptr(seedh), _lib.dptr(hm))
+        if rc != _lib.OK:
+            msg = _lib.lib.srbd_tamols_last_error(self.h)
+            raise RuntimeError(f"srbd_tamols_run_terrain failed ({rc}): {msg.decode() if msg else ''}")
+        return dict(footholds=fh.reshape(4, 3), boxes=boxes.reshape(4, 2, 3), valid=valid.astype(bool),
+                    scores=scores.reshape(4, rows * cols), seed_heights=seedh, heightmaps=hm)
+
+
 class VisualFootholdAdaptation:
     def __init__(self, legs_order, adaptation_strategy="height", config_module=None, device_id=None):
         cfg = config_module if config_module is not None else default_config
