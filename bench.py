@@ -101,6 +101,86 @@ def cpu_baseline(w: Workload, seconds: float):
             "ms_per_step": round(1e3 * dt / max(n, 1), 3)}
 
 
+def interface_latency(w: Workload, steps: int):
+    """p50 / p99 ms of one MPC step through the reference's Python plugin API at the workload's shape:
+    PeriodicGaitGenerator.compute_contact_sequence (C++ host producer) + SRBDControllerInterface.
+    compute_control (prepare_state_and_reference, with_newkey, jitted_compute_control, LegsAttr masking),
+    dict state in, LegsAttr GRFs out -- the 100 Hz loop's controller cost (srbd_controller_interface.py:113-180)."""
+    import copy
+    import types
+
+    from quadruped_pympc_amd import config as base
+    from quadruped_pympc_amd.config import ROBOTS
+    from quadruped_pympc_amd.helpers.periodic_gait_generator import PeriodicGaitGenerator
+    from quadruped_pympc_amd.interfaces.srbd_controller_interface import SRBDControllerInterface
+    from quadruped_pympc_amd.synthetic import GAITS
+
+    cfg = types.SimpleNamespace(**{k: copy.deepcopy(getattr(base, k)) for k in
+                                   ("robot", "mass", "inertia", "hip_height", "gravity_constant", "mpc_params",
+                                    "simulation_params")})
+    cfg.robot, cfg.mass, cfg.inertia = w.robot, ROBOTS[w.robot][0], np.array(ROBOTS[w.robot][1])
+    cfg.mpc_params.update(horizon=w.horizon, sampling_method=w.method, control_parametrization=w.parametrization,
+                          num_splines=w.num_splines, num_parallel_computations=w.num_samples, sigma_mppi=w.sigma,
+                          grf_max=cfg.mass * 9.81)
+    iface = SRBDControllerInterface(cfg)
+    gtype, freq, duty = GAITS[w.gait]
+    pgg = PeriodicGaitGenerator(duty, freq, gtype, w.horizon)
+    s, r, _ = inputs(w, 0)
+    legs = ("FL", "FR", "RL", "RR")
+    state = {"position": s[0:3], "linear_velocity": s[3:6], "orientation": s[6:9], "angular_velocity": s[9:12]}
+    state.update({"foot_" + n: s[12 + 3 * i:15 + 3 * i] for i, n in enumerate(legs)})
+    ref = {"ref_position": r[0:3], "ref_linear_velocity": r[3:6], "ref_orientation": r[6:9],
+           "ref_angular_velocity": r[9:12]}
+    ref.update({"ref_foot_" + n: r[12 + 3 * i:15 + 3 * i].reshape(1, 3) for i, n in enumerate(legs)})
+    dts, lens = np.array([w.dt]), np.array([w.horizon])
+    lat = []
+    for k in range(steps + 20):
+        for _ in range(5):
+            pgg.run(0.002, pgg.step_freq)
+        t0 = time.perf_counter()
+        cs = pgg.compute_contact_sequence(dts, lens)
+        out = iface.compute_control(state, ref, cs, cfg.inertia, pgg.phase_signal, pgg.step_freq, 0)
+        lat.append(time.perf_counter() - t0)
+    assert np.isfinite(np.concatenate([out[0].FL, out[6]])).all()
+    iface.controller.close()
+    lat = np.array(lat[20:]) * 1e3
+    return {"p50_ms": round(float(np.percentile(lat, 50)), 4), "p99_ms": round(float(np.percentile(lat, 99)), 4),
+            "steps": steps, "path": "PeriodicGaitGenerator.compute_contact_sequence + "
+                                    "SRBDControllerInterface.compute_control (Python plugin API)"}
+
+
+def tamols_latency(calls: int):
+    """p50 / p99 ms of one TAMOLS foothold adaptation for the four legs on stepping_stones_medium (C4):
+    13 x 7 patches raycast on the GPU from the device-resident scene + the TAMOLS search, one call
+    (srbd_tamols_run_terrain), Go2 trot stance feet."""
+    from quadruped_pympc_amd import config
+    from quadruped_pympc_amd.helpers.terrain import GpuTerrain
+    from quadruped_pympc_amd.helpers.visual_foothold_adaptation import TamolsSearch, tamols_params_struct
+
+    ter = GpuTerrain.stepping_stones()
+    srch = TamolsSearch(0)
+    params = dict(config.simulation_params["tamols_params"])
+    params["h_des"] = 0.25
+    ps = tamols_params_struct(params, "go2")
+    feet = np.array([[1.22, 0.13, 0.05], [1.22, -0.13, 0.05], [0.84, 0.13, 0.05], [0.84, -0.13, 0.05]])
+    hips = feet + np.array([0.0, 0.0, 0.3])
+    contact = np.array([0, 1, 1, 0], np.int32)
+    lat = []
+    for k in range(calls + 10):
+        seeds = feet + np.array([0.12 + 0.001 * (k % 7), 0.01, 0.0])
+        t0 = time.perf_counter()
+        out = srch.run_terrain(ter, 0.0, seeds, hips, ps, forward_vel=np.array([0.5, 0.0, 0.0]),
+                               base_position=np.array([1.03, 0.0, 0.35]), current_contact=contact,
+                               current_feet_pos=feet)
+        lat.append(time.perf_counter() - t0)
+    srch.close()
+    ter.close()
+    lat = np.array(lat[10:]) * 1e3
+    return {"p50_ms": round(float(np.percentile(lat, 50)), 4), "p99_ms": round(float(np.percentile(lat, 99)), 4),
+            "calls": calls, "valid_legs": int(out["valid"].sum()),
+            "path": "srbd_tamols_run_terrain: 4 x 13 x 7 raycast patches + TAMOLS, stepping_stones_medium"}
+
+
 def bench_single(w, args):
     ctx = _lib.Context(make_cfg(w, w.num_samples, 0, 1, 0))
     s, r, c = inputs(w, 0)
@@ -169,6 +249,8 @@ def main():
     ap.add_argument("--latency-steps", type=int, default=500)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--extras", type=int, default=200,
+                    help="steps of the supplementary interface / TAMOLS latency probes (0: skip)")
     ap.add_argument("--force-sharded", action="store_true", help=argparse.SUPPRESS)  # 1-GPU rehearsal
     args = ap.parse_args()
     rank = int(os.environ.get("RANK", "0"))
@@ -211,6 +293,9 @@ def main():
         line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
     else:
         line["cpu_baseline"] = None
+    if world == 1 and args.extras:  # supplementary latencies of the callers either side of the path
+        line["interface_step"] = interface_latency(w, args.extras)
+        line["tamols_c4"] = tamols_latency(args.extras)
     print(json.dumps(line), flush=True)
 
 
