@@ -1341,8 +1341,12 @@ struct srbd_tamols_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     double* d_hm = nullptr;
-    double* d_out = nullptr;  // scores | footholds | boxes | seedh
+    // scores (4 nc) | footholds 12 | boxes 24 | seed heights 4 | valid (4 int32 in 2 doubles): one block,
+    // so the results come back in one D2H copy into pinned staging (h_out)
+    double* d_out = nullptr;
     int* d_valid = nullptr;
+    double* h_out = nullptr;
+    double* h_hm = nullptr;  // pinned staging of heightmaps in (srbd_tamols_run) or out (run_terrain)
     size_t cap_cand = 0;
     std::string err;
 };
@@ -1355,8 +1359,7 @@ extern "C" int srbd_tamols_create(int32_t device_id, srbd_tamols_ctx** out) {
         return fail(nullptr, SRBD_E_NODEVICE, "no HIP device visible (this library has no CPU fallback)");
     srbd_tamols_ctx* t = new srbd_tamols_ctx();
     t->device = device_id;
-    if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc((void**)&t->d_valid, 4 * sizeof(int)) != hipSuccess) {
+    if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess) {
         srbd_tamols_destroy(t);
         return fail(nullptr, SRBD_E_HIP, "TAMOLS context allocation failed");
     }
@@ -1370,7 +1373,8 @@ extern "C" void srbd_tamols_destroy(srbd_tamols_ctx* t) {
     if (t->stream) (void)hipStreamSynchronize(t->stream);
     (void)hipFree(t->d_hm);
     (void)hipFree(t->d_out);
-    (void)hipFree(t->d_valid);
+    if (t->h_out) (void)hipHostFree(t->h_out);
+    if (t->h_hm) (void)hipHostFree(t->h_hm);
     if (t->stream) (void)hipStreamDestroy(t->stream);
     delete t;
 }
@@ -1407,20 +1411,31 @@ extern "C" int srbd_tamols_run(srbd_tamols_ctx* t, const double* hm, int32_t row
     }
     TAM_TRY(t, hipSetDevice(t->device));
     if (int rc = tamols_reserve(t, nc)) return rc;
-    TAM_TRY(t, hipMemcpyAsync(t->d_hm, hm, sizeof(double) * 12 * nc, hipMemcpyHostToDevice, t->stream));
+    memcpy(t->h_hm, hm, sizeof(double) * 12 * nc);
+    TAM_TRY(t, hipMemcpyAsync(t->d_hm, t->h_hm, sizeof(double) * 12 * nc, hipMemcpyHostToDevice, t->stream));
     return tamols_enqueue(t, t->d_hm, rows, cols, seeds, hips, vel, base, contact, feet, p, out_fh, out_box,
                           out_valid, out_scores, out_seedh);
 }
 
 static int tamols_reserve(srbd_tamols_ctx* t, int nc) {
     if (t->cap_cand < (size_t)nc) {
+        TAM_TRY(t, hipStreamSynchronize(t->stream));
         (void)hipFree(t->d_hm);
         (void)hipFree(t->d_out);
-        t->d_hm = t->d_out = nullptr;
+        if (t->h_out) (void)hipHostFree(t->h_out);
+        if (t->h_hm) (void)hipHostFree(t->h_hm);
+        t->d_hm = t->d_out = t->h_out = t->h_hm = nullptr;
+        t->d_valid = nullptr;
+        t->cap_cand = 0;
+        const size_t out_doubles = 4 * (size_t)nc + 12 + 24 + 4 + 2;
         TAM_TRY(t, hipMalloc((void**)&t->d_hm, sizeof(double) * 4 * 3 * nc));
-        TAM_TRY(t, hipMalloc((void**)&t->d_out, sizeof(double) * (4 * (size_t)nc + 12 + 24 + 4)));
+        TAM_TRY(t, hipMalloc((void**)&t->d_out, sizeof(double) * out_doubles));
+        TAM_TRY(t, hipHostMalloc((void**)&t->h_out, sizeof(double) * out_doubles, hipHostMallocDefault));
+        TAM_TRY(t, hipHostMalloc((void**)&t->h_hm, sizeof(double) * 4 * 3 * nc, hipHostMallocDefault));
+        t->d_valid = reinterpret_cast<int*>(t->d_out + 4 * (size_t)nc + 40);
         t->cap_cand = nc;
     }
+    t->d_valid = reinterpret_cast<int*>(t->d_out + 4 * (size_t)nc + 40);  // this call's layout
     return SRBD_OK;
 }
 
@@ -1454,13 +1469,17 @@ static int tamols_enqueue(srbd_tamols_ctx* t, const double* d_hm, int32_t rows, 
     double* d_seedh = d_box + 24;
     launch_tamols(a, d_hm, d_scores, d_fh, d_box, t->d_valid, d_seedh, t->stream);
     TAM_TRY(t, hipGetLastError());
-    TAM_TRY(t, hipMemcpyAsync(out_fh, d_fh, sizeof(double) * 12, hipMemcpyDeviceToHost, t->stream));
-    TAM_TRY(t, hipMemcpyAsync(out_box, d_box, sizeof(double) * 24, hipMemcpyDeviceToHost, t->stream));
-    TAM_TRY(t, hipMemcpyAsync(out_valid, t->d_valid, sizeof(int) * 4, hipMemcpyDeviceToHost, t->stream));
-    if (out_scores)
-        TAM_TRY(t, hipMemcpyAsync(out_scores, d_scores, sizeof(double) * 4 * nc, hipMemcpyDeviceToHost, t->stream));
-    if (out_seedh) TAM_TRY(t, hipMemcpyAsync(out_seedh, d_seedh, sizeof(double) * 4, hipMemcpyDeviceToHost, t->stream));
+    // one D2H: the whole block when the scores are wanted, else its 42-double tail
+    const size_t first = out_scores ? 0 : 4 * (size_t)nc, total = 4 * (size_t)nc + 42;
+    TAM_TRY(t, hipMemcpyAsync(t->h_out + first, t->d_out + first, sizeof(double) * (total - first),
+                              hipMemcpyDeviceToHost, t->stream));
     TAM_TRY(t, hipStreamSynchronize(t->stream));
+    const double* h = t->h_out + 4 * (size_t)nc;
+    memcpy(out_fh, h, sizeof(double) * 12);
+    memcpy(out_box, h + 12, sizeof(double) * 24);
+    if (out_seedh) memcpy(out_seedh, h + 36, sizeof(double) * 4);
+    memcpy(out_valid, h + 40, sizeof(int32_t) * 4);
+    if (out_scores) memcpy(out_scores, t->h_out, sizeof(double) * 4 * nc);
     return SRBD_OK;
 }
 
@@ -1490,7 +1509,9 @@ extern "C" int srbd_tamols_run_terrain(srbd_tamols_ctx* t, srbd_terrain* ter, do
         return SRBD_E_HIP;
     }
     if (out_hm)
-        TAM_TRY(t, hipMemcpyAsync(out_hm, d_hm, sizeof(double) * 12 * nc, hipMemcpyDeviceToHost, t->stream));
-    return tamols_enqueue(t, d_hm, rows, cols, seeds, hips, vel, base, contact, feet, p, out_fh, out_box, out_valid,
-                          out_scores, out_seedh);
+        TAM_TRY(t, hipMemcpyAsync(t->h_hm, d_hm, sizeof(double) * 12 * nc, hipMemcpyDeviceToHost, t->stream));
+    const int rc = tamols_enqueue(t, d_hm, rows, cols, seeds, hips, vel, base, contact, feet, p, out_fh, out_box,
+                                  out_valid, out_scores, out_seedh);  // synchronises the stream
+    if (!rc && out_hm) memcpy(out_hm, t->h_hm, sizeof(double) * 12 * nc);
+    return rc;
 }

@@ -135,7 +135,7 @@ struct srbd_terrain {
     double* d_job = nullptr;  // centres | yaw cos, sin
     double* d_out = nullptr;
     size_t cap_job = 0, cap_out = 0;
-    std::vector<double> h_job;
+    double* h_job = nullptr;  // pinned staging of the job inputs
     srbd::TerrainDev dev{};
     std::string err;
 };

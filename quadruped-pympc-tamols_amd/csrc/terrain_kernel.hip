@@ -97,6 +97,7 @@ extern "C" void srbd_terrain_destroy(srbd_terrain* t) {
     (void)hipFree(t->d_hf);
     (void)hipFree(t->d_job);
     (void)hipFree(t->d_out);
+    if (t->h_job) (void)hipHostFree(t->h_job);
     if (t->stream) (void)hipStreamDestroy(t->stream);
     delete t;
 }
@@ -163,17 +164,21 @@ extern "C" int srbd_terrain_create(int32_t device_id, const srbd_terrain_prim* p
     return SRBD_OK;
 }
 
-// Job inputs (centres, yaw cos / sin) staged through one H2D copy into d_job; the output buffer
-// grows on demand.  Returns the device output pointer in *d_out.
+// Job inputs (centres, yaw cos / sin) staged through pinned memory and one H2D copy into d_job; the
+// output buffer grows on demand.  Returns the device output pointer in *d_out.
 int srbd::terrain_enqueue(srbd_terrain* t, const double* centers, const double* yaws, int npatch, int rows, int cols,
                     double dist_x, double dist_y, double ray_z, hipStream_t s, double** d_out) {
     if (!t || !centers || !yaws || npatch < 1 || rows < 1 || cols < 1)
         return terrain_fail(t, SRBD_E_INVALID, "bad patch arguments");
     const size_t need_out = (size_t)npatch * rows * cols * 3, need_job = 5 * (size_t)npatch;
     if (t->cap_job < need_job) {
+        TER_TRY(t, hipStreamSynchronize(s));
         (void)hipFree(t->d_job);
-        t->d_job = nullptr;
+        if (t->h_job) (void)hipHostFree(t->h_job);
+        t->d_job = t->h_job = nullptr;
+        t->cap_job = 0;
         TER_TRY(t, hipMalloc((void**)&t->d_job, sizeof(double) * need_job));
+        TER_TRY(t, hipHostMalloc((void**)&t->h_job, sizeof(double) * need_job, hipHostMallocDefault));
         t->cap_job = need_job;
     }
     if (t->cap_out < need_out) {
@@ -182,13 +187,13 @@ int srbd::terrain_enqueue(srbd_terrain* t, const double* centers, const double* 
         TER_TRY(t, hipMalloc((void**)&t->d_out, sizeof(double) * need_out));
         t->cap_out = need_out;
     }
-    t->h_job.resize(need_job);
+    // the previous call's copy out of h_job has completed: every call ends with a stream synchronise
     for (int p = 0; p < npatch; ++p) {
         for (int q = 0; q < 3; ++q) t->h_job[3 * p + q] = centers[3 * p + q];
         t->h_job[3 * npatch + 2 * p] = cos(yaws[p]);
         t->h_job[3 * npatch + 2 * p + 1] = sin(yaws[p]);
     }
-    TER_TRY(t, hipMemcpyAsync(t->d_job, t->h_job.data(), sizeof(double) * need_job, hipMemcpyHostToDevice, s));
+    TER_TRY(t, hipMemcpyAsync(t->d_job, t->h_job, sizeof(double) * need_job, hipMemcpyHostToDevice, s));
     PatchJob j;
     j.centers = t->d_job;
     j.cs_yaw = t->d_job + 3 * npatch;
