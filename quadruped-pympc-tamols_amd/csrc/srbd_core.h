@@ -75,6 +75,8 @@ struct StepInput {
     float sigma[MAXP];
 };
 
+static_assert(sizeof(StepInput) % 16 == 0, "StepInput is copied in 16-byte words");
+
 struct StepOutput {
     float best[MAXP];
     float sigma[MAXP];

@@ -1388,6 +1388,13 @@ int launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, in
                         ctr_inc, pub);
 }
 
+__global__ void __launch_bounds__(256) copy16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int n) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+void launch_copy16(const void* src, void* dst, size_t bytes, hipStream_t s) {
+    hipLaunchKernelGGL(copy16_kernel, dim3(1), dim3(256), 0, s, (const uint4*)src, (uint4*)dst, (int)(bytes / 16));
+}
+
 __global__ void empty_kernel() {}
 void launch_empty(hipStream_t s) { hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s); }
 

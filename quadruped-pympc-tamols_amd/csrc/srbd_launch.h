@@ -86,6 +86,7 @@ int launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, in
                        hipStream_t s, int ctr_inc = 1, Publish pub = {nullptr, 0});
 void launch_advance(const ModelConst& mc, StepInput* in, const StepOutput* out, hipStream_t s);
 void launch_empty(hipStream_t s);  // measurement: the event floor
+void launch_copy16(const void* src, void* dst, size_t bytes, hipStream_t s);  // bytes % 16 == 0
 void launch_div_selftest(const float* a, const float* b, int n, float* o, hipStream_t s);
 
 // TAMOLS (tamols_kernel.hip)
