@@ -459,8 +459,11 @@ static int acquire_noise(srbd_ctx* c, const float* noise, uint64_t seed, uint64_
 // async H2D copy.
 static int upload_input(srbd_ctx* c) {
     static const int memcpy_upload = tune_knob("SRBD_UPLOAD_MEMCPY", 0);
-    if (!memcpy_upload) {
-        launch_copy16(c->d_in_host, c->d_in, sizeof(StepInput), c->stream);
+    if (!memcpy_upload) {  // the header and best[P] (+ sigma[P] for CEM): the bytes the step reads
+        const size_t P4 = sizeof(float) * (size_t)c->mc.P;
+        const size_t sig = offsetof(StepInput, sigma);
+        launch_copy16(c->d_in_host, c->d_in, offsetof(StepInput, best) + P4, sig,
+                      c->mc.method == SRBD_CEM_MPPI ? P4 : 0, c->stream);
         return SRBD_OK;
     }
     HIP_TRY(c, hipMemcpyAsync(c->d_in, c->h_in, sizeof(StepInput), hipMemcpyHostToDevice, c->stream));
@@ -1363,6 +1366,7 @@ struct srbd_tamols_ctx {
     int* d_valid = nullptr;
     double* h_out = nullptr;
     double* h_hm = nullptr;  // pinned staging of heightmaps in (srbd_tamols_run) or out (run_terrain)
+    double* d_nn = nullptr;  // phase-A query heights, 4 x (nc * NQ + 1)
     size_t cap_cand = 0;
     std::string err;
 };
@@ -1389,6 +1393,7 @@ extern "C" void srbd_tamols_destroy(srbd_tamols_ctx* t) {
     if (t->stream) (void)hipStreamSynchronize(t->stream);
     (void)hipFree(t->d_hm);
     (void)hipFree(t->d_out);
+    (void)hipFree(t->d_nn);
     if (t->h_out) (void)hipHostFree(t->h_out);
     if (t->h_hm) (void)hipHostFree(t->h_hm);
     if (t->stream) (void)hipStreamDestroy(t->stream);
@@ -1438,13 +1443,15 @@ static int tamols_reserve(srbd_tamols_ctx* t, int nc) {
         TAM_TRY(t, hipStreamSynchronize(t->stream));
         (void)hipFree(t->d_hm);
         (void)hipFree(t->d_out);
+        (void)hipFree(t->d_nn);
         if (t->h_out) (void)hipHostFree(t->h_out);
         if (t->h_hm) (void)hipHostFree(t->h_hm);
-        t->d_hm = t->d_out = t->h_out = t->h_hm = nullptr;
+        t->d_hm = t->d_out = t->h_out = t->h_hm = t->d_nn = nullptr;
         t->d_valid = nullptr;
         t->cap_cand = 0;
         const size_t out_doubles = 4 * (size_t)nc + 12 + 24 + 4 + 2;
         TAM_TRY(t, hipMalloc((void**)&t->d_hm, sizeof(double) * 4 * 3 * nc));
+        TAM_TRY(t, hipMalloc((void**)&t->d_nn, sizeof(double) * 4 * ((size_t)nc * TAMOLS_NQ + 1)));
         TAM_TRY(t, hipMalloc((void**)&t->d_out, sizeof(double) * out_doubles));
         TAM_TRY(t, hipHostMalloc((void**)&t->h_out, sizeof(double) * out_doubles, hipHostMallocDefault));
         TAM_TRY(t, hipHostMalloc((void**)&t->h_hm, sizeof(double) * 4 * 3 * nc, hipHostMallocDefault));
@@ -1483,7 +1490,7 @@ static int tamols_enqueue(srbd_tamols_ctx* t, const double* d_hm, int32_t rows, 
     double* d_fh = d_scores + 4 * (size_t)nc;
     double* d_box = d_fh + 12;
     double* d_seedh = d_box + 24;
-    launch_tamols(a, d_hm, d_scores, d_fh, d_box, t->d_valid, d_seedh, t->stream);
+    launch_tamols(a, d_hm, t->d_nn, d_scores, d_fh, d_box, t->d_valid, d_seedh, t->stream);
     TAM_TRY(t, hipGetLastError());
     // one D2H: the whole block when the scores are wanted, else its 42-double tail
     const size_t first = out_scores ? 0 : 4 * (size_t)nc, total = 4 * (size_t)nc + 42;

@@ -9,6 +9,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/srbd_mpc.h"
@@ -75,7 +76,9 @@ struct StepInput {
     float sigma[MAXP];
 };
 
-static_assert(sizeof(StepInput) % 16 == 0, "StepInput is copied in 16-byte words");
+static_assert(sizeof(StepInput) % 16 == 0 && offsetof(StepInput, best) % 16 == 0 &&
+                  offsetof(StepInput, sigma) % 16 == 0,
+              "StepInput is copied in 16-byte words (P is a multiple of 12, so P floats are too)");
 
 struct StepOutput {
     float best[MAXP];

@@ -1388,11 +1388,17 @@ int launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, in
                         ctr_inc, pub);
 }
 
-__global__ void __launch_bounds__(256) copy16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int n) {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+// Two byte ranges [0, n0) and [off1, off1 + n1) (16-byte words) of src -> dst, one block.
+__global__ void __launch_bounds__(256) copy16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int n0,
+                                                     int off1, int n1) {
+    for (int i = threadIdx.x; i < n0 + n1; i += blockDim.x) {
+        const int k = i < n0 ? i : off1 + (i - n0);
+        dst[k] = src[k];
+    }
 }
-void launch_copy16(const void* src, void* dst, size_t bytes, hipStream_t s) {
-    hipLaunchKernelGGL(copy16_kernel, dim3(1), dim3(256), 0, s, (const uint4*)src, (uint4*)dst, (int)(bytes / 16));
+void launch_copy16(const void* src, void* dst, size_t bytes0, size_t off1, size_t bytes1, hipStream_t s) {
+    hipLaunchKernelGGL(copy16_kernel, dim3(1), dim3(256), 0, s, (const uint4*)src, (uint4*)dst, (int)(bytes0 / 16),
+                       (int)(off1 / 16), (int)(bytes1 / 16));
 }
 
 __global__ void empty_kernel() {}

@@ -86,7 +86,8 @@ int launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, in
                        hipStream_t s, int ctr_inc = 1, Publish pub = {nullptr, 0});
 void launch_advance(const ModelConst& mc, StepInput* in, const StepOutput* out, hipStream_t s);
 void launch_empty(hipStream_t s);  // measurement: the event floor
-void launch_copy16(const void* src, void* dst, size_t bytes, hipStream_t s);  // bytes % 16 == 0
+// src -> dst bytes [0, bytes0) and [off1, off1 + bytes1); all multiples of 16
+void launch_copy16(const void* src, void* dst, size_t bytes0, size_t off1, size_t bytes1, hipStream_t s);
 void launch_div_selftest(const float* a, const float* b, int n, float* o, hipStream_t s);
 
 // TAMOLS (tamols_kernel.hip)
@@ -147,7 +148,8 @@ int terrain_enqueue(srbd_terrain* t, const double* centers, const double* yaws, 
                     double dist_x, double dist_y, double ray_z, hipStream_t s, double** d_out);
 
 size_t tamols_smem_bytes(int ncand);
-void launch_tamols(const TamolsArgs& a, const double* hm, double* scores, double* footholds, double* boxes,
-                   int* valid, double* seedh, hipStream_t s);
+// nn: scratch of 4 x (ncand * TAMOLS_NQ + 1) doubles (the phase-A query heights)
+void launch_tamols(const TamolsArgs& a, const double* hm, double* nn, double* scores, double* footholds,
+                   double* boxes, int* valid, double* seedh, hipStream_t s);
 
 }  // namespace srbd

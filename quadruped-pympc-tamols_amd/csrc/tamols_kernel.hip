@@ -2,11 +2,12 @@
 //
 // Restates VisualFootholdAdaptation.compute_adaptation, strategy 'tamols'
 // (quadruped_pympc/helpers/visual_foothold_adaptation.py:153-231, helpers :261-714).
-// One workgroup per leg; the leg's heightmap patch (rows x cols points) is staged in LDS.
-//   phase A: every nearest-neighbour height query of every candidate (19 per candidate:
-//            the candidate, 5 leg-collision samples, 4 edge samples, 9 roughness samples) plus
-//            the seed, one lane per query, brute force over the LDS patch (strict <: first
-//            nearest point wins)
+// The leg's heightmap patch (rows x cols points) is staged in LDS.
+//   phase A (tamols_nn_kernel, 7 blocks per leg): every nearest-neighbour height query of every
+//            candidate (19 per candidate: the candidate, 5 leg-collision samples, 4 edge samples,
+//            9 roughness samples) plus the seed, one lane per query, brute force over the LDS
+//            patch (strict <: first nearest point wins)
+// and then one workgroup per leg (tamols_kernel):
 //   phase B: one lane per candidate evaluates the hard constraints and the soft costs
 //   phase C: one lane takes the strict-< argmin in candidate order (first minimum wins)
 // float64 keeps the host oracle's decisions (reach bounds, argmin) bit-for-bit comparable.
@@ -14,10 +15,74 @@
 
 namespace srbd {
 
+// Query t of a leg (0 <= t < nc * NQ: candidate t / NQ, sample t % NQ; t == nc * NQ: the seed) and its
+// nearest-neighbour height over the patch (strict <: the first nearest point wins), FastHeightMap.get_height
+// (VFA:31-35).  Shared by the phase-A kernel and nothing else, so every query is computed one way.
+__device__ __forceinline__ double tamols_query(const TamolsArgs& a, int leg, int t, const double* px, const double* py,
+                                               const double* pz) {
+    const int nc = a.ncand, nq = nc * TAMOLS_NQ + 1;
+    const srbd_tamols_params& p = a.p;
+    const double dl = p.gradient_delta;
+    const double hx = a.hips[3 * leg], hy = a.hips[3 * leg + 1];
+    const double sx = a.seeds[3 * leg], sy = a.seeds[3 * leg + 1];
+    double qx, qy;
+    if (t == nq - 1) {
+        qx = sx;
+        qy = sy;
+    } else {
+        const int c = t / TAMOLS_NQ, q = t % TAMOLS_NQ;
+        const double cx = px[c], cy = py[c];
+        if (q == 0) {
+            qx = cx;
+            qy = cy;
+        } else if (q <= 5) {  // VFA:406 p_leg = (1 - alpha) * hip + alpha * candidate
+            const double al = p.alphas[q - 1];
+            qx = (1.0 - al) * hx + al * cx;
+            qy = (1.0 - al) * hy + al * cy;
+        } else if (q <= 9) {  // VFA:443 offsets (+d,0), (-d,0), (0,+d), (0,-d)
+            const int o = q - 6;
+            qx = o == 0 ? cx + dl : (o == 1 ? cx + (-dl) : cx + 0.0);
+            qy = o == 2 ? cy + dl : (o == 3 ? cy + (-dl) : cy + 0.0);
+        } else {  // VFA:489-493 3x3 grid, i outer, j inner
+            const int g = q - 10, i = g / 3 - 1, j = g % 3 - 1;
+            qx = cx + (double)i * dl;
+            qy = cy + (double)j * dl;
+        }
+    }
+    double bd = INFINITY, bh = 0.0;
+    for (int i = 0; i < nc; ++i) {
+        const double dx = qx - px[i], dy = qy - py[i];
+        const double d2 = dx * dx + dy * dy;
+        if (d2 < bd) {
+            bd = d2;
+            bh = pz[i];
+        }
+    }
+    return bh + 0.02;
+}
+
+// Phase A over the whole chip: block (b, leg) answers queries b*256 .. of its leg (one lane each)
+// into nn_g[leg][t].  One block per leg did 1 730 queries x 91 points in 22 us; spread over
+// ceil(1730 / 256) = 7 blocks per leg each lane answers one.
+__global__ void __launch_bounds__(256) tamols_nn_kernel(const TamolsArgs a, const double* __restrict__ hm,
+                                                        double* __restrict__ nn_g) {
+    __shared__ double pxs[TAMOLS_MAXCAND], pys[TAMOLS_MAXCAND], pzs[TAMOLS_MAXCAND];
+    const int leg = blockIdx.y, nc = a.ncand, nq = nc * TAMOLS_NQ + 1;
+    const double* H = hm + (size_t)leg * nc * 3;
+    for (int i = threadIdx.x; i < nc; i += blockDim.x) {
+        pxs[i] = H[3 * i];
+        pys[i] = H[3 * i + 1];
+        pzs[i] = H[3 * i + 2];
+    }
+    __syncthreads();
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < nq) nn_g[(size_t)leg * nq + t] = tamols_query(a, leg, t, pxs, pys, pzs);
+}
+
 __global__ void __launch_bounds__(1024) tamols_kernel(const TamolsArgs a, const double* __restrict__ hm,
-                                                      double* __restrict__ scores, double* __restrict__ footholds,
-                                                      double* __restrict__ boxes, int* __restrict__ valid,
-                                                      double* __restrict__ seedh) {
+                                                      const double* __restrict__ nn_g, double* __restrict__ scores,
+                                                      double* __restrict__ footholds, double* __restrict__ boxes,
+                                                      int* __restrict__ valid, double* __restrict__ seedh) {
     extern __shared__ double sm[];
     const int leg = blockIdx.x, tid = threadIdx.x, T = blockDim.x, nc = a.ncand;
     double* px = sm;
@@ -31,51 +96,14 @@ __global__ void __launch_bounds__(1024) tamols_kernel(const TamolsArgs a, const 
         py[i] = H[3 * i + 1];
         pz[i] = H[3 * i + 2];
     }
-    __syncthreads();
-
     const srbd_tamols_params& p = a.p;
     const double dl = p.gradient_delta;
     const double hx = a.hips[3 * leg], hy = a.hips[3 * leg + 1], hz = a.hips[3 * leg + 2];
     const double sx = a.seeds[3 * leg], sy = a.seeds[3 * leg + 1], sz = a.seeds[3 * leg + 2];
 
-    // ---- phase A
+    // ---- phase A (tamols_nn_kernel): the leg's query heights -> LDS
     const int nq = nc * TAMOLS_NQ + 1;
-    for (int t = tid; t < nq; t += T) {
-        double qx, qy;
-        if (t == nq - 1) {
-            qx = sx;
-            qy = sy;
-        } else {
-            const int c = t / TAMOLS_NQ, q = t % TAMOLS_NQ;
-            const double cx = px[c], cy = py[c];
-            if (q == 0) {
-                qx = cx;
-                qy = cy;
-            } else if (q <= 5) {  // VFA:406 p_leg = (1 - alpha) * hip + alpha * candidate
-                const double al = p.alphas[q - 1];
-                qx = (1.0 - al) * hx + al * cx;
-                qy = (1.0 - al) * hy + al * cy;
-            } else if (q <= 9) {  // VFA:443 offsets (+d,0), (-d,0), (0,+d), (0,-d)
-                const int o = q - 6;
-                qx = o == 0 ? cx + dl : (o == 1 ? cx + (-dl) : cx + 0.0);
-                qy = o == 2 ? cy + dl : (o == 3 ? cy + (-dl) : cy + 0.0);
-            } else {  // VFA:489-493 3x3 grid, i outer, j inner
-                const int g = q - 10, i = g / 3 - 1, j = g % 3 - 1;
-                qx = cx + (double)i * dl;
-                qy = cy + (double)j * dl;
-            }
-        }
-        double bd = INFINITY, bh = 0.0;
-        for (int i = 0; i < nc; ++i) {
-            const double dx = qx - px[i], dy = qy - py[i];
-            const double d2 = dx * dx + dy * dy;
-            if (d2 < bd) {
-                bd = d2;
-                bh = pz[i];
-            }
-        }
-        nn[t] = bh + 0.02;  // FastHeightMap.get_height (VFA:31-35)
-    }
+    for (int t = tid; t < nq; t += T) nn[t] = nn_g[(size_t)leg * nq + t];
     __syncthreads();
 
     // ---- phase B
@@ -220,10 +248,12 @@ __global__ void __launch_bounds__(1024) tamols_kernel(const TamolsArgs a, const 
 
 size_t tamols_smem_bytes(int ncand) { return sizeof(double) * ((size_t)ncand * (4 + TAMOLS_NQ) + 1); }
 
-void launch_tamols(const TamolsArgs& a, const double* hm, double* scores, double* footholds, double* boxes,
-                   int* valid, double* seedh, hipStream_t s) {
-    hipLaunchKernelGGL(tamols_kernel, dim3(4), dim3(1024), tamols_smem_bytes(a.ncand), s, a, hm, scores, footholds,
-                       boxes, valid, seedh);
+void launch_tamols(const TamolsArgs& a, const double* hm, double* nn, double* scores, double* footholds,
+                   double* boxes, int* valid, double* seedh, hipStream_t s) {
+    const int nq = a.ncand * TAMOLS_NQ + 1;
+    hipLaunchKernelGGL(tamols_nn_kernel, dim3((nq + 255) / 256, 4), dim3(256), 0, s, a, hm, nn);
+    hipLaunchKernelGGL(tamols_kernel, dim3(4), dim3(1024), tamols_smem_bytes(a.ncand), s, a, hm, nn, scores,
+                       footholds, boxes, valid, seedh);
 }
 
 }  // namespace srbd

@@ -34,6 +34,8 @@ __global__ void __launch_bounds__(256) terrain_patch_kernel(const TerrainDev t, 
     double best = -INFINITY;
     int hit = 0;
     if (t.has_ground) consider(t.ground_z, j.ray_z, best, hit);
+    // unrolled so several primitives' (wave-uniform, scalar) loads are in flight per round trip
+#pragma unroll 4
     for (int q = 0; q < t.nprims; ++q) {
         const srbd_terrain_prim& pr = t.prims[q];
         const double ux = x - pr.cx, uy = y - pr.cy;
