@@ -136,6 +136,21 @@ int srbd_set_gait(srbd_ctx* ctx, const float* timing, float pgg_dt, float duty_f
                   int32_t n_freq, const float* freq_local);
 int srbd_clear_gait(srbd_ctx* ctx);
 
+/*
+ * Opt-in per-sample cost terms (the north star's "friction-cone + GRF-smoothing terms").  The
+ * reference's sampling cost has none of them (its R input cost is commented out, NMPC:132-157 and
+ * :453-484; the cone is enforced by projection), so all weights default to 0 and
+ * then the cost is exactly the reference's.  Per horizon step and leg, with f the clipped, masked
+ * force and fref the step's gravity share:
+ *   r_force[q] * u_q^2         u = (fx, fy, fz - fref if the leg is in stance else fz)
+ *                              (the reference's R; its values were 0.1, 0.1, 0.001)
+ *   w_smooth * |f_n - f_{n-1}|^2            steps n >= 1 (GRF smoothing)
+ *   w_cone * (max(0, |fx'| - mu fz)^2 + max(0, |fy'| - mu fz)^2)   fx', fy' before the cone clip
+ * Weights must be finite and >= 0.  Applies to every following step of the context (all methods,
+ * parametrizations and rollout forms, gait-adaptive included).
+ */
+int srbd_set_cost_terms(srbd_ctx* ctx, const float r_force[3], float w_smooth, float w_cone);
+
 /* Sharded form.  Record size in floats (identical on every rank). */
 int srbd_record_floats(const srbd_ctx* ctx);
 /* Rows of this rank only; writes this rank's partial record to d_record (device pointer).

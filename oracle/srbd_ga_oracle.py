@@ -25,7 +25,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .srbd_oracle import CUBIC_SPLINE, LINEAR_SPLINE, MAX_SAMPLING_FORCES_X, MAX_SAMPLING_FORCES_Y, \
+from .srbd_oracle import extra_cost, CUBIC_SPLINE, LINEAR_SPLINE, MAX_SAMPLING_FORCES_X, MAX_SAMPLING_FORCES_Y, \
     MAX_SAMPLING_FORCES_Z, MPPI, CEM_MPPI, RANDOM_SAMPLING, ZERO_ORDER, SamplingMPCOracle
 
 f32 = np.float32
@@ -122,8 +122,9 @@ class GaitAdaptiveOracle(SamplingMPCOracle):
         return axis(0), axis(4), axis(8)
 
     # ------------------------------------------------------------ rollout
-    def rollout_costs_ga(self, state, reference, params, timing, freqs):
-        """vmap(compute_rollout) of GA:326-501.  Returns unsaturated costs (N,) f32."""
+    def rollout_costs_ga(self, state, reference, params, timing, freqs, cost_terms=None):
+        """vmap(compute_rollout) of GA:326-501.  Returns unsaturated costs (N,) f32.
+        cost_terms: the build's opt-in terms (srbd_oracle.extra_cost), None for the reference's cost."""
         params = np.asarray(params, dtype=f32)
         freqs = np.asarray(freqs, dtype=f32)
         N, PL = params.shape[0], self.PL
@@ -135,6 +136,7 @@ class GaitAdaptiveOracle(SamplingMPCOracle):
         cost = np.zeros(N, dtype=f32)
         rx = f32(MAX_SAMPLING_FORCES_Z / MAX_SAMPLING_FORCES_X)
         ry = f32(MAX_SAMPLING_FORCES_Z / MAX_SAMPLING_FORCES_Y)
+        Fprev = None
         with np.errstate(over="ignore", invalid="ignore", divide="ignore"):
             for n in range(self.horizon):
                 c = cs[:, :, n]
@@ -152,6 +154,7 @@ class GaitAdaptiveOracle(SamplingMPCOracle):
                     fx[leg] = (fx[leg] * c[:, leg] / rx).astype(f32)
                     fy[leg] = (fy[leg] * c[:, leg] / ry).astype(f32)
                     fz[leg] = (fz[leg] * c[:, leg]).astype(f32)
+                pre = np.stack([v for leg in range(4) for v in (fx[leg], fy[leg])], -1).astype(f32)
                 fx, fy, fz = self.enforce_force_constraints(fx, fy, fz)   # GA:410-414
                 F = np.stack([v for leg in range(4) for v in (fx[leg], fy[leg], fz[leg])], -1).astype(f32)
                 x = self.robot.integrate(x, F, c, n)                     # GA:447-451
@@ -161,6 +164,9 @@ class GaitAdaptiveOracle(SamplingMPCOracle):
                 for i in range(1, 24):
                     acc = acc + qe[:, i] * e[:, i]
                 cost = (cost + acc).astype(f32)
+                if cost_terms:
+                    cost = (cost + extra_cost(F, pre, c, fref, Fprev, f32(self.mu), cost_terms)).astype(f32)
+                Fprev = F
             d = (freqs - f32(GA_FREQ_CENTER)).astype(f32)                 # GA:500
             cost = (cost + ((d * f32(GA_FREQ_WEIGHT)).astype(f32) * d)).astype(f32)
         return cost

@@ -276,8 +276,9 @@ class SamplingMPCOracle:
             oz.append(z)
         return ox, oy, oz
 
-    def _forces_at(self, params, contact, n, step, horizon_leg):
-        """Decode + gravity compensation + contact mask + clip (NMPC:364-420 and :706-750)."""
+    def _forces_at(self, params, contact, n, step, horizon_leg, with_pre=False):
+        """Decode + gravity compensation + contact mask + clip (NMPC:364-420 and :706-750).
+        with_pre: also the masked x / y before the clip (N, 8) and fref (the opt-in cone term)."""
         PL = self.PL
         fx, fy, fz = [], [], []
         for leg in range(4):
@@ -296,21 +297,26 @@ class SamplingMPCOracle:
                 fx[leg] = fx[leg] * cs[leg] / rx
                 fy[leg] = fy[leg] * cs[leg] / ry
                 fz[leg] = fz[leg] * cs[leg]
+            pre = np.stack([v for leg in range(4) for v in (fx[leg], fy[leg])], -1).astype(f32)
             fx, fy, fz = self.enforce_force_constraints(fx, fy, fz)
         F = np.stack([v for leg in range(4) for v in (fx[leg], fy[leg], fz[leg])], -1).astype(f32)
+        if with_pre:
+            return F, np.array(cs, dtype=f32), pre, f32(fref)
         return F, np.array(cs, dtype=f32)
 
     # ------------------------------------------------------------- rollout
-    def rollout_costs(self, state, reference, params, contact):
-        """vmap(compute_rollout), NMPC:316-496.  params (N,P) f32 -> costs (N,) f32 (unsaturated)."""
+    def rollout_costs(self, state, reference, params, contact, cost_terms=None):
+        """vmap(compute_rollout), NMPC:316-496.  params (N,P) f32 -> costs (N,) f32 (unsaturated).
+        cost_terms: None, or dict(r_force, w_smooth, w_cone) of the build's opt-in terms (extra_cost)."""
         params = np.asarray(params, dtype=f32)
         N = params.shape[0]
         x = np.broadcast_to(np.asarray(state, dtype=f32), (N, 24)).copy()
         ref = np.asarray(reference, dtype=f32)
         cost = np.zeros(N, dtype=f32)
+        Fprev = None
         with np.errstate(over="ignore", invalid="ignore", divide="ignore"):
             for n in range(self.horizon):
-                F, cs = self._forces_at(params, contact, n, n, self.horizon)
+                F, cs, pre, fref = self._forces_at(params, contact, n, n, self.horizon, with_pre=True)
                 x = self.robot.integrate(x, F, cs, n)
                 e = (x - ref).astype(f32)
                 # e^T Q e with diagonal Q, accumulated i = 0..23
@@ -319,6 +325,9 @@ class SamplingMPCOracle:
                 for i in range(1, 24):
                     acc = acc + qe[:, i] * e[:, i]
                 cost = cost + acc
+                if cost_terms:
+                    cost = (cost + extra_cost(F, pre, cs, fref, Fprev, f32(self.mu), cost_terms)).astype(f32)
+                Fprev = F
         return cost.astype(f32)
 
     @staticmethod
@@ -404,6 +413,39 @@ class SamplingMPCOracle:
             out["sigma"] = s
             out["elite"] = idx
         return out
+
+
+def extra_cost(F, pre, cs, fref, Fprev, mu, terms):
+    """The build's opt-in cost terms of one step (include/srbd_mpc.h srbd_set_cost_terms; not in the
+    reference, whose R input cost is commented out at NMPC:453-484).  F (N,12) clipped forces, pre (N,8)
+    masked x / y before the clip, cs (4,) or (N,4) contact, fref the gravity share, Fprev the previous
+    step's F (None at n = 0).  Returns (N,) f32: per component, leg by leg, r_q u^2 + w_smooth d^2 +
+    w_cone v^2 (kernel order: srbd_core.h extra_cost_step)."""
+    r = np.asarray(terms.get("r_force", (0.0, 0.0, 0.0)), dtype=f32)
+    ws, wc = f32(terms.get("w_smooth", 0.0)), f32(terms.get("w_cone", 0.0))
+    cs = np.asarray(cs, dtype=f32)
+    N = F.shape[0]
+    total = np.zeros(N, dtype=f32)
+    for q in range(3):
+        e = np.zeros(N, dtype=f32)
+        for leg in range(4):
+            f = F[:, 3 * leg + q]
+            c = cs[..., leg]
+            if q == 2:
+                u = (f - np.where(c != 0, fref, f32(0))).astype(f32)
+            else:
+                u = f
+            term = ((u * r[q]).astype(f32) * u).astype(f32)
+            if Fprev is not None:
+                d = (f - Fprev[:, 3 * leg + q]).astype(f32)
+                term = (term + (d * ws).astype(f32) * d).astype(f32)
+            if q < 2:
+                v = (np.abs(pre[:, 2 * leg + q]) - (mu * F[:, 3 * leg + 2]).astype(f32)).astype(f32)
+                v = np.where(v > 0, v, f32(0)).astype(f32)
+                term = (term + (v * wc).astype(f32) * v).astype(f32)
+            e = (e + term).astype(f32)
+        total = (total + e).astype(f32)
+    return total
 
 
 def prepare_state_and_reference(state_current, reference_state, current_contact, previous_contact, best, PL):

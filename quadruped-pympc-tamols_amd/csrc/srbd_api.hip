@@ -708,6 +708,26 @@ extern "C" int srbd_clear_gait(srbd_ctx* c) {
     return SRBD_OK;
 }
 
+extern "C" int srbd_set_cost_terms(srbd_ctx* c, const float* r_force, float w_smooth, float w_cone) {
+    if (!c || !r_force) return SRBD_E_INVALID;
+    const float w[5] = {r_force[0], r_force[1], r_force[2], w_smooth, w_cone};
+    for (float x : w)
+        if (!(x >= 0.0f && x < INFINITY)) return fail(c, SRBD_E_INVALID, "cost weights must be finite and >= 0");
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    ModelConst& mc = c->mc;
+    const int on = (w[0] != 0.0f || w[1] != 0.0f || w[2] != 0.0f || w_smooth != 0.0f || w_cone != 0.0f) ? 1 : 0;
+    if (on != mc.cost_on || memcmp(mc.cost_r, r_force, sizeof(mc.cost_r)) || mc.cost_smooth != w_smooth ||
+        mc.cost_cone != w_cone) {
+        mc.cost_on = on;
+        memcpy(mc.cost_r, r_force, sizeof(mc.cost_r));
+        mc.cost_smooth = w_smooth;
+        mc.cost_cone = w_cone;
+        drop_graphs(c);  // kernels take ModelConst by value: recapture
+    }
+    return SRBD_OK;
+}
+
 // ------------------------------------------------------------------ host merge (no device)
 static uint64_t host_rec_key(const float* R, int P, int q) {
     return ((uint64_t)f2u(R[REC_HDR + P + 2 * q + 1]) << 32) | (uint64_t)f2u(R[REC_HDR + P + 2 * q]);

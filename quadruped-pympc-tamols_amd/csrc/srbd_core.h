@@ -49,6 +49,9 @@ struct ModelConst {
     int ntail;
     short tailc[MAX_TAIL];
     uint32_t tailmask[MAXP / 32];
+    // opt-in cost terms (srbd_set_cost_terms); cost_on == 0: the reference's cost, terms skipped
+    int cost_on;
+    float cost_r[3], cost_smooth, cost_cone;
 };
 SRBD_HD bool is_tail_col(const ModelConst& mc, int j) { return (mc.tailmask[j >> 5] >> (j & 31)) & 1u; }
 
@@ -280,6 +283,39 @@ SRBD_HD void shape_leg(const ModelConst& mc, float fref, float c, float& fx, flo
     fy = div3(fy * c);
     fz = fz * c;
     clip_leg(mc, fx, fy, fz);
+}
+
+// Opt-in cost terms of one step n (srbd_set_cost_terms), thread-per-sample layout: per component q
+// (x, y, z), leg by leg in order, (u r_q) u + (d w_smooth) d [n >= 1] + (v w_cone) v [q = x, y] with
+// u = f_q (z: f_z - fref for a stance leg), d = f_q - f_q(step n-1), v = max(0, |f_q before the
+// clip| - mu f_z); the component's sum joins cost3[q] after its tracking term.  F: clipped forces,
+// RX / RY: each leg's decoded x / y.  The four-lane kernel forms the same terms in the same order.
+SRBD_HD void extra_cost_step(const ModelConst& mc, int n, const float F[12], const float RX[4], const float RY[4],
+                             const float c[4], float fref, float Fprev[12], float cost3[3]) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        float e = 0.0f;
+#pragma unroll
+        for (int leg = 0; leg < 4; ++leg) {
+            const float f = F[3 * leg + q];
+            const float u = q == 2 ? f - (c[leg] != 0.0f ? fref : 0.0f) : f;
+            float term = (u * mc.cost_r[q]) * u;
+            if (n > 0) {
+                const float d = f - Fprev[3 * leg + q];
+                term = term + (d * mc.cost_smooth) * d;
+            }
+            if (q < 2) {
+                const float pre = div3((q == 0 ? RX[leg] : RY[leg]) * c[leg]);
+                float v = fabsf(pre) - mc.mu * F[3 * leg + 2];
+                v = v > 0.0f ? v : 0.0f;
+                term = term + (v * mc.cost_cone) * v;
+            }
+            e = e + term;
+        }
+        cost3[q] = cost3[q] + e;
+    }
+#pragma unroll
+    for (int i = 0; i < 12; ++i) Fprev[i] = F[i];
 }
 
 // Spline decode of one leg (NMPC:181-268) with precomputed per-step coefficients.

@@ -283,7 +283,7 @@ __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepI
 }
 
 // One thread per sample.  Best throughput when samples fill the GPU (>= ~1 wave per SIMD).
-template <int KIND, int HT, int ST, bool CEMT>
+template <int KIND, int HT, int ST, bool CEMT, bool EXT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == SRBD_ZERO_ORDER ? 2 : 1))) rollout_kernel(const ModelConst mc, const StepInput* __restrict__ in,
                                                       const float* __restrict__ noise, float* __restrict__ costs,
                                                       float* __restrict__ recs, int rec_stride,
@@ -318,12 +318,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
         feet[i] = in->state[12 + i];
     }
     float cost3[3] = {0.0f, 0.0f, 0.0f};
-
-    auto step = [&](const int n) __attribute__((always_inline)) {
+    float Fprev[12];  // EXT: opt-in cost terms (srbd_set_cost_terms), a separate instantiation so the
+                      // default horizon carries none of their code (a runtime test cost C3 17 %)
+    auto step = [&](const int n, auto EX) __attribute__((always_inline)) {
         const float c[4] = {in->contact[0][n], in->contact[1][n], in->contact[2][n], in->contact[3][n]};
         const float fref = in->fzref[n];
         const int idx = CT && KIND != SRBD_ZERO_ORDER ? chunk_index(n, HT, ST) : mc.sidx[n];
-        float F[12];
+        float F[12], RX[4], RY[4];
 #pragma unroll
         for (int leg = 0; leg < 4; ++leg) {
             const int base = leg * PL;
@@ -334,6 +335,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
             float fx, fy, fz;
             decode_leg(KIND, H, S, idx, mc.sq[n], mc.somq[n], mc.sa[n], mc.sb[n], mc.sc[n], mc.sd[n], n, acc, fx,
                        fy, fz);
+            RX[leg] = fx;
+            RY[leg] = fy;
             shape_leg(mc, fref, c[leg], fx, fy, fz);
             F[3 * leg] = fx;
             F[3 * leg + 1] = fy;
@@ -349,12 +352,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
         }
 #pragma unroll
         for (int q = 0; q < 3; ++q) cost3[q] = cost3[q] + (((t[q] + t[3 + q]) + t[6 + q]) + t[9 + q]);
+        if constexpr (decltype(EX)::value) extra_cost_step(mc, n, F, RX, RY, c, fref, Fprev, cost3);
     };
-    if constexpr (CT) {
-        unroll_seq([&](auto nc) { step(decltype(nc)::value); }, std::make_integer_sequence<int, (CT ? HT : 1)>{});
-    } else {
-        for (int n = 0; n < H; ++n) step(n);
-    }
+    auto horizon = [&](auto EX) __attribute__((always_inline)) {
+        if constexpr (CT) {
+            unroll_seq([&](auto nc) { step(decltype(nc)::value, EX); },
+                       std::make_integer_sequence<int, (CT ? HT : 1)>{});
+        } else {
+            for (int n = 0; n < H; ++n) step(n, EX);
+        }
+    };
+    horizon(std::bool_constant<EXT>{});
     float cost = (cost3[0] + cost3[1]) + cost3[2];
     cost = cost + in->cost_feet;  // 0, or NaN when a foot term is non-finite (Q_feet = 0)
     // NMPC:686-687
@@ -437,6 +445,8 @@ __global__ void __launch_bounds__(256) rollout_ga_kernel(const ModelConst mc, co
         feet[i] = in->state[12 + i];
     }
     float cost3[3] = {0.0f, 0.0f, 0.0f};
+    const bool extra = mc.cost_on != 0;  // opt-in cost terms (srbd_set_cost_terms)
+    float Fprev[12];
     for (int n = 0; n < H; ++n) {
         float c[4];
 #pragma unroll
@@ -447,7 +457,7 @@ __global__ void __launch_bounds__(256) rollout_ga_kernel(const ModelConst mc, co
         }
         const float ns = ((c[0] + c[1]) + c[2]) + c[3];
         const float fref = mc.fz_ns[(int)ns];
-        float F[12];
+        float F[12], RX[4], RY[4];
 #pragma unroll
         for (int leg = 0; leg < 4; ++leg) {
             const int base = leg * PL;
@@ -472,6 +482,8 @@ __global__ void __launch_bounds__(256) rollout_ga_kernel(const ModelConst mc, co
             }
             float fx, fy, fz;
             decode_leg(KIND, H, S, idx, q, omq, a, bb, cc, d, st, acc, fx, fy, fz);
+            RX[leg] = fx;
+            RY[leg] = fy;
             shape_leg(mc, fref, c[leg], fx, fy, fz);
             F[3 * leg] = fx;
             F[3 * leg + 1] = fy;
@@ -486,6 +498,7 @@ __global__ void __launch_bounds__(256) rollout_ga_kernel(const ModelConst mc, co
         }
 #pragma unroll
         for (int q = 0; q < 3; ++q) cost3[q] = cost3[q] + (((t[q] + t[3 + q]) + t[6 + q]) + t[9 + q]);
+        if (extra) extra_cost_step(mc, n, F, RX, RY, c, fref, Fprev, cost3);
     }
     float cost = (cost3[0] + cost3[1]) + cost3[2];
     cost = cost + in->cost_feet;
@@ -582,7 +595,7 @@ __device__ __forceinline__ float quad_cross(float vl, float fl) {
     return (-vn2) * fn1 + vn1 * fn2;
 }
 
-template <int KIND, int HT, int ST, bool CEMT>
+template <int KIND, int HT, int ST, bool CEMT, bool EXT>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) rollout_quad_kernel(const ModelConst mc, const StepInput* __restrict__ in,
                                                            const float* __restrict__ noise, float* __restrict__ costs,
                                                            float* __restrict__ recs, int rec_stride,
@@ -630,6 +643,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
     float p = sel3(c, st[0], st[1], st[2]), v = sel3(c, st[3], st[4], st[5]);
     float r = sel3(c, st[6], st[7], st[8]), w = sel3(c, st[9], st[10], st[11]);
     float cost = 0.0f;
+    // EXT: opt-in cost terms (srbd_set_cost_terms), this lane's component of extra_cost_step
+    const float rwc = sel3(c, mc.cost_r[0], mc.cost_r[1], mc.cost_r[2]);
+    float fprev[4];
 
     // Specialised shapes: every parameter this lane reads over the horizon (its component's block
     // of each leg) is loaded before the first step, so the horizon chain pays one memory round trip
@@ -657,14 +673,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
             }
     }
 
-    auto step = [&](const int n) __attribute__((always_inline)) {
+    auto step = [&](const int n, auto EX) __attribute__((always_inline)) {  // EX: as rollout_kernel
         const float cl[4] = {in->contact[0][n], in->contact[1][n], in->contact[2][n], in->contact[3][n]};
         const float fref = in->fzref[n];
         const int idx = CT && KIND != SRBD_ZERO_ORDER ? chunk_index(n, HT, ST) : mc.sidx[n];
         // force and torque sums in leg order (integrate(): temp = sum_i f_i c_i, temp2 = sum_i t_i c_i;
         // 0 + x == x).  No per-leg branch on the contact flags: the straight-line horizon schedules
         // better than it saves (measured 15.9 -> 17.1 us at C2 with the branches)
-        float temp = 0.0f, temp2 = 0.0f;
+        float temp = 0.0f, temp2 = 0.0f, ex = 0.0f;
 #pragma unroll
         for (int l = 0; l < 4; ++l) {
             const int base = l * PL;
@@ -699,6 +715,21 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
             const float f = c == 2 ? fz : clamp_cs(xy, mc.neg_mu * fz, mc.mu * fz);
             temp = temp + f * cl[l];
             temp2 = temp2 + quad_cross(feet[l] - p, f) * cl[l];
+            if constexpr (decltype(EX)::value) {
+                const float u = c == 2 ? f - (cl[l] != 0.0f ? fref : 0.0f) : f;
+                float term = (u * rwc) * u;
+                if (n > 0) {
+                    const float d = f - fprev[l];
+                    term = term + (d * mc.cost_smooth) * d;
+                }
+                if (c < 2) {
+                    float vv = fabsf(xy) - mc.mu * fz;
+                    vv = vv > 0.0f ? vv : 0.0f;
+                    term = term + (vv * mc.cost_cone) * vv;
+                }
+                ex = ex + term;
+                fprev[l] = f;
+            }
         }
         quad_rigid_body(mc, L, temp, temp2, mc.dts[n], p, v, r, w);
         // tracking cost (NMPC:451), accumulated per component lane: cost_c += ((tp + tv) + tr) + tw,
@@ -706,12 +737,17 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
         const float ep = p - rp, ev = v - rv, er_ = r - rr, ew = w - rw;
         const float tp = (ep * Qp) * ep, tv = (ev * Qv) * ev, tr = (er_ * Qr) * er_, tw = (ew * Qw) * ew;
         cost = cost + (((tp + tv) + tr) + tw);
+        if constexpr (decltype(EX)::value) cost = cost + ex;
     };
-    if constexpr (CT) {
-        unroll_seq([&](auto nc) { step(decltype(nc)::value); }, std::make_integer_sequence<int, (CT ? HT : 1)>{});
-    } else {
-        for (int n = 0; n < H; ++n) step(n);
-    }
+    auto horizon = [&](auto EX) __attribute__((always_inline)) {
+        if constexpr (CT) {
+            unroll_seq([&](auto nc) { step(decltype(nc)::value, EX); },
+                       std::make_integer_sequence<int, (CT ? HT : 1)>{});
+        } else {
+            for (int n = 0; n < H; ++n) step(n, EX);
+        }
+    };
+    horizon(std::bool_constant<EXT>{});
     SRBD_RSTAMP(2);
     cost = (qp<QP_B0>(cost) + qp<QP_B1>(cost)) + qp<QP_B2>(cost);
     cost = cost + in->cost_feet;  // 0, or NaN when a foot term is non-finite (Q_feet = 0)
@@ -1193,7 +1229,7 @@ __global__ void div_selftest_kernel(const float* a, const float* b, int n, float
 }
 
 // ------------------------------------------------------------------ launchers
-template <int KIND, int HT, int ST>
+template <int KIND, int HT, int ST, bool EXT = false>
 static void launch_rollout_t(const ModelConst& mc, const StepInput* in, const float* noise, float* costs,
                              float* recs, int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next) {
     const RngJob job = next ? *next : RngJob{nullptr, 0, 0, 0, 0};
@@ -1204,19 +1240,19 @@ static void launch_rollout_t(const ModelConst& mc, const StepInput* in, const fl
         const int blocks = (mc.n_local + spb - 1) / spb;
         const dim3 grid(blocks + extra * 256 / threads);
         if (cem)
-            hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, true>), grid, dim3(threads), 0, s, mc, in, noise,
+            hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, true, EXT>), grid, dim3(threads), 0, s, mc, in, noise,
                                costs, recs, rec_stride, job, blocks);
         else
-            hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false>), grid, dim3(threads), 0, s, mc, in, noise,
+            hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, EXT>), grid, dim3(threads), 0, s, mc, in, noise,
                                costs, recs, rec_stride, job, blocks);
     } else {
         const int blocks = (mc.n_local + threads - 1) / threads;
         const dim3 grid(blocks + extra * (256 / threads));
         if (cem)
-            hipLaunchKernelGGL((rollout_kernel<KIND, HT, ST, true>), grid, dim3(threads), 0, s, mc, in, noise, costs,
+            hipLaunchKernelGGL((rollout_kernel<KIND, HT, ST, true, EXT>), grid, dim3(threads), 0, s, mc, in, noise, costs,
                                recs, rec_stride, job, blocks);
         else
-            hipLaunchKernelGGL((rollout_kernel<KIND, HT, ST, false>), grid, dim3(threads), 0, s, mc, in, noise, costs,
+            hipLaunchKernelGGL((rollout_kernel<KIND, HT, ST, false, EXT>), grid, dim3(threads), 0, s, mc, in, noise, costs,
                                recs, rec_stride, job, blocks);
     }
 }
@@ -1249,6 +1285,16 @@ void launch_rollout(const ModelConst& mc, const StepInput* in, const float* nois
                     int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next) {
     if (mc.ga) return launch_rollout_ga(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next);
     const int H = mc.H, S = mc.S;
+    if (mc.cost_on) {  // the opt-in cost terms run on the runtime-shape kernels only
+        if (mc.kind == SRBD_ZERO_ORDER)
+            return launch_rollout_t<SRBD_ZERO_ORDER, 0, 0, true>(mc, in, noise, costs, recs, rec_stride, mode,
+                                                                 threads, s, next);
+        if (mc.kind == SRBD_LINEAR_SPLINE)
+            return launch_rollout_t<SRBD_LINEAR_SPLINE, 0, 0, true>(mc, in, noise, costs, recs, rec_stride, mode,
+                                                                    threads, s, next);
+        return launch_rollout_t<SRBD_CUBIC_SPLINE, 0, 0, true>(mc, in, noise, costs, recs, rec_stride, mode,
+                                                               threads, s, next);
+    }
 #define SRBD_LR(K, HH, SS) \
     return launch_rollout_t<K, HH, SS>(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next)
     switch (mc.kind) {

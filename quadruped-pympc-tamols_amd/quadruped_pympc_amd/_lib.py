@@ -74,6 +74,7 @@ SIGNATURES = {
     "srbd_step": (_I, [_P, _P, _P, _P, _I, _P, _P, _P, C.c_uint64, C.c_uint64, C.POINTER(SrbdResult), _P]),
     "srbd_set_gait": (_I, [_P, _FP, _F, _F, _FP, _I, _FP]),
     "srbd_clear_gait": (_I, [_P]),
+    "srbd_set_cost_terms": (_I, [_P, _FP, _F, _F]),
     "srbd_record_floats": (_I, [_P]),
     "srbd_step_local": (_I, [_P, _FP, _FP, _FP, _I, _FP, _FP, _FP, C.c_uint64, C.c_uint64, _P]),
     "srbd_step_finish": (_I, [_P, _P, _I, _FP, _FP, C.POINTER(SrbdResult), _FP]),
@@ -414,6 +415,12 @@ class Context:
 
     def clear_gait(self):
         self.check(lib.srbd_clear_gait(self.h), "srbd_clear_gait")
+
+    def set_cost_terms(self, r_force=(0.0, 0.0, 0.0), w_smooth: float = 0.0, w_cone: float = 0.0):
+        """srbd_set_cost_terms: opt-in force regularisation / GRF smoothing / cone-violation terms (all 0: the
+        reference's cost)."""
+        r = np.ascontiguousarray(np.asarray(r_force, np.float32).reshape(3))
+        self.check(lib.srbd_set_cost_terms(self.h, fptr(r), float(w_smooth), float(w_cone)), "srbd_set_cost_terms")
 
     def set_stream(self, stream_handle: int | None):
         """Launch on a caller-owned hipStream_t; None (or 0, the legacy null stream) -> the context's own."""

@@ -156,6 +156,12 @@ class Sampling_MPC:
     def context(self) -> "_lib.Context":
         if self._ctx is None:
             self._ctx = _lib.Context(self._srbd_config())
+            # optional extension (not in the reference): mpc_params['cost_terms'] = {'r_force': (rx, ry, rz),
+            # 'w_smooth': w, 'w_cone': w}; absent or zero = the reference's cost (include/srbd_mpc.h)
+            terms = self._cfg.mpc_params.get("cost_terms")
+            if terms:
+                self._ctx.set_cost_terms(terms.get("r_force", (0.0, 0.0, 0.0)), terms.get("w_smooth", 0.0),
+                                         terms.get("w_cone", 0.0))
         return self._ctx
 
     def _run(self, state, reference, contact_sequence, best_control_parameters, key, sigma, noise):
