@@ -758,6 +758,128 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
     SRBD_RSTAMP(5);
 }
 
+// ---- gait-adaptive rollout in the four-lane layout (rollout_ga_kernel's float operations, in its
+// order, component-wise as rollout_quad_kernel does): the sample's step frequency, contact masks,
+// stance counters and per-leg spline coefficients are formed on each of its four lanes (the same
+// values), the decode reads this lane's component.  Costs are rollout_ga_kernel's bit for bit.
+// The opt-in cost terms run on rollout_ga_kernel (launch_rollout_ga).
+template <int KIND, int HT>
+__global__ void __launch_bounds__(512) rollout_ga_quad_kernel(const ModelConst mc, const StepInput* __restrict__ in,
+                                                              const float* __restrict__ noise,
+                                                              float* __restrict__ costs, float* __restrict__ recs,
+                                                              int rec_stride, const RngJob next_rng, int nroll) {
+    if ((int)blockIdx.x >= nroll) {
+        rng_items(mc, in, next_rng, ((int)blockIdx.x - nroll) * (int)blockDim.x + (int)threadIdx.x,
+                  ((int)gridDim.x - nroll) * (int)blockDim.x);
+        return;
+    }
+    __shared__ float e_sh[128];
+    __shared__ uint64_t red[8];
+    __shared__ uint64_t elite_sh[MAXK];
+    const int H = HT > 0 ? HT : mc.H, S = mc.S, PL = mc.PL;  // HT: horizon fixed at compile time
+    const int tid = threadIdx.x;
+    const int q4 = tid & 3;
+    const int c = q4 < 3 ? q4 : 2;
+    const int sib = tid >> 2;
+    const int SPB = (int)blockDim.x >> 2;
+    const int k = blockIdx.x * SPB + sib;
+    const bool valid = k < mc.n_local;
+    const size_t ldn = (size_t)mc.ldn;
+    const float* __restrict__ nz = noise + k;
+    const float* __restrict__ best = in->best;
+
+    const float f = ga_sample_freq(mc, in, k);
+    uint32_t mask[4];
+    ga_contact_masks(in, H, f, mask);
+    float seg[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) seg[l] = ((float)__popc(mask[l]) + 1.0f) / (float)S;
+    int cnt[4] = {-1, -1, -1, -1};
+
+    const QuadLane L = quad_lane(mc, c);
+    const float Qp = sel3(c, mc.Q[0], mc.Q[1], mc.Q[2]), Qv = sel3(c, mc.Q[3], mc.Q[4], mc.Q[5]);
+    const float Qr = sel3(c, mc.Q[6], mc.Q[7], mc.Q[8]), Qw = sel3(c, mc.Q[9], mc.Q[10], mc.Q[11]);
+    const float* st_ = in->state;
+    const float* rf = in->ref;
+    const float rp = sel3(c, rf[0], rf[1], rf[2]), rv = sel3(c, rf[3], rf[4], rf[5]);
+    const float rr = sel3(c, rf[6], rf[7], rf[8]), rw = sel3(c, rf[9], rf[10], rf[11]);
+    float feet[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) feet[l] = sel3(c, st_[12 + 3 * l], st_[13 + 3 * l], st_[14 + 3 * l]);
+    float p = sel3(c, st_[0], st_[1], st_[2]), v = sel3(c, st_[3], st_[4], st_[5]);
+    float r = sel3(c, st_[6], st_[7], st_[8]), w = sel3(c, st_[9], st_[10], st_[11]);
+    float cost = 0.0f;
+    // unrolled when HT > 0: every step's parameter loads depend only on the contact masks, so they
+    // issue ahead of the physics chain
+    constexpr int UNR = HT > 0 ? HT : 1;
+#pragma unroll UNR
+    for (int n = 0; n < H; ++n) {
+        float cl[4];
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            const uint32_t b = (mask[l] >> n) & 1u;
+            cl[l] = b ? 1.0f : 0.0f;
+            cnt[l] += (int)b;
+        }
+        const float ns = ((cl[0] + cl[1]) + cl[2]) + cl[3];
+        const float fref = mc.fz_ns[(int)ns];
+        float temp = 0.0f, temp2 = 0.0f;
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            const int base = l * PL;
+            auto acc = [&](int j) {
+                j = j < 0 ? j + PL : j;
+                return best[base + j] + nz[(size_t)(base + j) * ldn];
+            };
+            const int stc = cnt[l];
+            float raw;
+            if (KIND == SRBD_ZERO_ORDER) {
+                raw = acc(stc + c * H);
+            } else {
+                int idx = 0;
+                for (int i = 0; i <= S; ++i)
+                    if (stc >= in->ga_cb[i]) idx = i;
+                float tau = (float)stc / seg[l];
+                tau = tau - (float)idx;
+                const float q = tau / 1.0f;
+                if (KIND == SRBD_LINEAR_SPLINE) {
+                    const float omq = 1.0f - q;
+                    const int o = idx + c * (S + 1);
+                    raw = omq * acc(o) + q * acc(o + 1);
+                } else {
+                    const float a = 2.0f * q * q * q - 3.0f * q * q + 1.0f;
+                    const float bb = (q * q * q - 2.0f * q * q + q) * 1.0f;
+                    const float cc = -2.0f * q * q * q + 3.0f * q * q;
+                    const float d = (q * q * q - q * q) * 1.0f;
+                    const int o = 10 * idx + 4 * c;
+                    const float p0 = acc(o), p1 = acc(o + 1), p2 = acc(o + 2), p3 = acc(o + 3);
+                    const float phi = 0.5f * ((p2 - p1) + (p1 - p0));
+                    const float phin = 0.5f * ((p3 - p2) + (p2 - p1));
+                    raw = a * p1 + bb * phi + cc * p2 + d * phin;
+                }
+            }
+            const float zp = clamp_cs((fref + raw) * cl[l], mc.grf_min, mc.grf_max);
+            const float xy = div3(raw * cl[l]);
+            const float fz = qp<QP_B2>(c == 2 ? zp : xy);
+            const float fo = c == 2 ? fz : clamp_cs(xy, mc.neg_mu * fz, mc.mu * fz);
+            temp = temp + fo * cl[l];
+            temp2 = temp2 + quad_cross(feet[l] - p, fo) * cl[l];
+        }
+        quad_rigid_body(mc, L, temp, temp2, mc.dts[n], p, v, r, w);
+        const float ep = p - rp, ev = v - rv, er_ = r - rr, ew = w - rw;
+        const float tp = (ep * Qp) * ep, tv = (ev * Qv) * ev, tr = (er_ * Qr) * er_, tw = (ew * Qw) * ew;
+        cost = cost + (((tp + tv) + tr) + tw);
+    }
+    cost = (qp<QP_B0>(cost) + qp<QP_B1>(cost)) + qp<QP_B2>(cost);
+    cost = cost + in->cost_feet;
+    const float df = f - 1.3f;
+    cost = cost + (df * 100.0f) * df;  // GA:500
+    if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
+    if (valid && q4 == 0 && costs) costs[k] = cost;
+    block_epilogue(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh,
+                   false, f);
+}
+
 // ------------------------------------------------------------------ merge
 __device__ __forceinline__ uint64_t rec_key(const float* R, int P, int q) {
     return ((uint64_t)f2u(R[REC_HDR + P + 2 * q + 1]) << 32) | (uint64_t)f2u(R[REC_HDR + P + 2 * q]);
@@ -1269,6 +1391,32 @@ static void launch_rollout_ga(const ModelConst& mc, const StepInput* in, const f
     const int extra = next ? (rng_grid(mc) < 1024 ? rng_grid(mc) : 1024) : 0;
     const int spb = mode == ROLLOUT_QUAD ? threads / 4 : threads;
     const int blocks = (mc.n_local + spb - 1) / spb;
+    if (mode == ROLLOUT_QUAD && !mc.cost_on) {  // four lanes per sample, `threads` per block
+        const dim3 grid(blocks + extra * 256 / threads), block(threads);
+#define SRBD_GQ(K, HH)                                                                                            \
+    {                                                                                                              \
+        hipLaunchKernelGGL((rollout_ga_quad_kernel<K, HH>), grid, block, 0, s, mc, in, noise, costs, recs, rec_stride, \
+                           job, blocks);                                                                           \
+        return;                                                                                                    \
+    }
+        const int H = mc.H;
+        switch (mc.kind) {
+            case SRBD_ZERO_ORDER:
+                if (H == 10) SRBD_GQ(SRBD_ZERO_ORDER, 10);
+                if (H == 12) SRBD_GQ(SRBD_ZERO_ORDER, 12);
+                if (H == 16) SRBD_GQ(SRBD_ZERO_ORDER, 16);
+                SRBD_GQ(SRBD_ZERO_ORDER, 0);
+            case SRBD_LINEAR_SPLINE:
+                if (H == 12) SRBD_GQ(SRBD_LINEAR_SPLINE, 12);
+                if (H == 16) SRBD_GQ(SRBD_LINEAR_SPLINE, 16);
+                SRBD_GQ(SRBD_LINEAR_SPLINE, 0);
+            default:
+                if (H == 12) SRBD_GQ(SRBD_CUBIC_SPLINE, 12);
+                if (H == 16) SRBD_GQ(SRBD_CUBIC_SPLINE, 16);
+                SRBD_GQ(SRBD_CUBIC_SPLINE, 0);
+        }
+#undef SRBD_GQ
+    }
     const dim3 grid(blocks + extra * 256 / spb), block(spb);
     if (mc.kind == SRBD_ZERO_ORDER)
         hipLaunchKernelGGL((rollout_ga_kernel<SRBD_ZERO_ORDER>), grid, block, 0, s, mc, in, noise, costs, recs,

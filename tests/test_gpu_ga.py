@@ -168,3 +168,22 @@ def test_interface_gait_adaptive_mppi(lib):
     out = itf.compute_control(sc, rs, contact, None, np.array([0.1, 0.6, 0.6, 0.1]), 1.65, 1)
     assert out[5] in np.array(cfg.mpc_params["step_freq_available"], f32)
     itf.controller.close()
+
+
+@pytest.mark.parametrize("par,H", [("zero_order", 12), ("linear_spline", 12), ("cubic_spline", 16),
+                                   ("zero_order", 10)])
+@pytest.mark.parametrize("method", ["mppi", "random_sampling"])
+@pytest.mark.parametrize("device_freqs", [False, True])
+def test_ga_rollout_variants_bitwise(lib, monkeypatch, par, H, method, device_freqs):
+    """rollout_ga_quad_kernel (four lanes per sample) gives rollout_ga_kernel's costs bit for bit."""
+    case = make_case("c2", N=1000, method=method, par=par, H=H, seed=21)
+    o = ga_oracle(case)
+    fs = freq_set(o.method, AVAIL, 1.65, 1)
+    freqs = None if device_freqs else np.random.default_rng(5).choice(fs, o.N).astype(f32)
+    out = {}
+    for mode in ("thread", "quad"):
+        monkeypatch.setenv("SRBD_ROLLOUT", mode)
+        _, res, costs = run(lib, case, TIMINGS[1], fs, freqs)
+        out[mode] = (costs, res.best_index, res.best_freq)
+    np.testing.assert_array_equal(out["thread"][0], out["quad"][0])
+    assert out["thread"][1:] == out["quad"][1:]
