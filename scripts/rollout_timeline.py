@@ -67,6 +67,8 @@ def main():
         R = rel[roll]
         G = rel[~roll]
         for i in range(NS):
+            if i == 1:  # stamp 1 is not recorded (the prefetch overlaps the horizon)
+                continue
             agg.setdefault(f"roll_s{i}", []).append(pct(R[:, i]))
         for i, j, nm in ((0, 2, "prefetch_horizon"), (2, 3, "min"), (3, 4, "wsum"), (4, 5, "tail")):
             agg.setdefault(f"phase_{nm}", []).append(float(np.mean(R[:, j] - R[:, i])))

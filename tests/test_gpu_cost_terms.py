@@ -101,3 +101,28 @@ def test_gait_adaptive_cost_terms_match_oracle(lib):
     params = (case["best"][None, :] + case["noise"]).astype(f32)
     ref = o.saturate(o.rollout_costs_ga(case["state"], case["ref"], params, timing, freqs, cost_terms=TERMS))
     np.testing.assert_allclose(costs, ref, rtol=2e-5, atol=1e-3)
+
+
+def test_cost_terms_toggle_with_graphs(lib):
+    """Setting or clearing the terms on a context whose step graph is already captured re-captures it:
+    the next step prices the new cost (oracle), and clearing restores the plain cost bit for bit."""
+    case = make_case("c2", N=1200, method="mppi", seed=17)
+    o = case["orc"]
+    params = (case["best"][None, :] + case["noise"]).astype(f32)
+    ctx = lib.Context(product_cfg(case, use_graph=True))
+    try:
+        def step():
+            return ctx.step(case["state"], case["ref"], case["contact"], case["best"], noise=case["noise"], seed=1,
+                            counter=2, want_costs=True)[3]
+        plain = step()
+        plain2 = step()  # graph replay
+        ctx.set_cost_terms(TERMS["r_force"], TERMS["w_smooth"], TERMS["w_cone"])
+        with_terms = step()
+        ctx.set_cost_terms((0.0, 0.0, 0.0), 0.0, 0.0)
+        cleared = step()
+    finally:
+        ctx.close()
+    np.testing.assert_array_equal(plain, plain2)
+    ref = o.saturate(o.rollout_costs(case["state"], case["ref"], params, case["contact"], cost_terms=TERMS))
+    np.testing.assert_allclose(with_terms, ref, rtol=2e-5, atol=1e-3)
+    np.testing.assert_array_equal(cleared, plain)
