@@ -2,69 +2,135 @@
 """Benchmark of the MI355X sampling SRBD MPC step (BASELINE.json metric).
 
 metric : "SRBD rollouts/sec + p50 MPC-step ms at N=10k H=12; 1/2/4/8 GPU"
-workload (N=1): BASELINE configs[1] = C2, Go2 trot flat, MPPI, N=10 000, H=12, zero-order control.
-A step = one full sampling-MPC iteration over one batch of N rollouts: device Philox RNG ->
-fused rollout + cost + block softmax partials -> merge (argmin, MPPI update, GRFs, predicted
-state) -> warm start of the next step written back on the device.  Inputs are resident in
-HBM when the timed region starts; `value` = rollouts of all ranks / max-over-ranks wall time.
-`p50_step_ms` / `p99_step_ms` are the host-to-host latency of one `srbd_step` call (state,
-reference, contact and parameters in; GRFs, predicted state, parameters out; PCIe included).
+workload (N=1 default): BASELINE configs[1] = C2, Go2 trot flat, MPPI, N=10 000, H=12, zero-order.
 
-N>1 GPUs (torchrun, one rank per GPU): weak scaling, N = 10 000 rows per GPU of ONE MPC problem;
-each step ends in one RCCL all-gather of the per-rank partial records (the path's only exchange),
-issued by the library on its own stream between the rollout and the merge (torch.distributed only
-carries the RCCL unique id and the timing barrier / max-over-ranks).
+A step = one host-to-host MPC iteration as the controller interface issues it: state,
+reference, contact sequence and warm-start parameters in (a few KB), device Philox noise (the
+O(N*P) input is generated and kept in HBM), fused rollout + cost + block softmax partials, merge
+(argmin, MPPI/CEM update, GRFs, predicted state), outputs back on the host.  The timed region is
+exactly K such steps (`srbd_step` / `srbd_step_sharded`), bracketed by a barrier and a device
+synchronisation; `value` = rollouts of all ranks x K / max-over-ranks wall time.  `p50_step_ms` /
+`p99_step_ms` are per-step host-to-host latencies (>= 1000 steps).  `device_chain` is the same
+step replayed device-resident (warm start kept on the device, hipGraph chain): the bound the host
+round trip sits on.
+
+--gpus N > 1 without a torchrun environment: this script starts torchrun itself as a CHILD
+process (before torch or the HIP library is loaded), relays rank 0's line and exits with the
+child's status.  One rank per GPU; each rank holds its rows of ONE MPC problem; the rank records
+are exchanged by the merge kernel over xGMI (IPC-mapped mailboxes; RCCL all-gather fallback).
+  --scaling weak   (default for c1-c4): num_samples rows per GPU, N_total = num_samples x N;
+  --scaling strong (default for c5)   : N_total = num_samples split over the N GPUs
+                                        (C5: 524 288 = 65 536 per GPU at N=8).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(ROOT, "quadruped-pympc-tamols_amd"))
-if int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--force-sharded" in sys.argv:
-    import torch  # noqa: F401  -- before libsrbd_hip.so: one HIP runtime per process (see _lib.py)
-
-from quadruped_pympc_amd import _lib  # noqa: E402
-from quadruped_pympc_amd.synthetic import CONFIGS, Workload, inputs  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 METRIC = "SRBD rollouts/sec + p50 MPC-step ms at N=10k H=12; 1/2/4/8 GPU"
 
 
-def make_cfg(w: Workload, n_total: int, rank: int, world: int, device: int):
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
+                    help="multi-GPU: rows per GPU fixed (weak) or total rows fixed (strong); default strong for c5")
+    ap.add_argument("--transport", default="auto", choices=["auto", "xgmi", "rccl"])
+    ap.add_argument("--latency-steps", type=int, default=1000)
+    ap.add_argument("--device-steps", type=int, default=2000, help="steps of the device-resident chain figure")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--extras", type=int, default=200,
+                    help="steps of the supplementary interface / TAMOLS latency probes (0: skip)")
+    return ap.parse_args(argv)
+
+
+def spawn_ranks(args, argv) -> int:
+    """torchrun as a child process (never exec): one rank per GPU on this node."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (xGMI mailboxes, RCCL)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------------------------------------- helpers
+def host_cores() -> dict:
+    """CPUs this process may use: the affinity set, capped by a cgroup CPU quota when one is set."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    usable = min(aff, quota) if quota else aff
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "usable": usable}
+
+
+def step_inputs(w, count):
+    """`count` distinct synthetic steps: state from default_rng(1234 + k), the PGG contact
+    sequence advanced 5 sim steps per MPC step."""
+    import numpy as np
+
+    from quadruped_pympc_amd.synthetic import contact_sequences, reference, robot_state
+
+    cs = contact_sequences(w.gait, w.horizon, count)
+    out = []
+    for k in range(count):
+        s = robot_state(w.robot, k)
+        out.append((s.astype(np.float32), reference(w.robot, s).astype(np.float32), cs[k].astype(np.float32)))
+    return out
+
+
+def make_cfg(_lib, w, n_total: int, rank: int, world: int, device: int):
+    import numpy as np
+
     return _lib.make_config(num_samples=n_total, horizon=w.horizon, method=w.method,
                             parametrization=w.parametrization, num_splines=w.num_splines, mass=w.mass,
                             inertia=w.inertia, dts=np.full(w.horizon, w.dt, np.float32), device_id=device,
                             rank=rank, world_size=world, use_graph=True, sigma_mppi=w.sigma)
 
 
-def roofline(w: Workload, n_local: int, kern: dict, traffic):
-    """Dominant kernel = the rollout launch as the timed chain runs it.
+def roofline(w, n_local: int, kern: dict, traffic):
+    """Dominant kernel = the rollout launch the step runs (with the next step's Philox blocks when fused).
 
-    Algorithmic bytes (SURVEY 8(d)): each noise row read once and one cost written, N*(4P+4);
-    when the launch also draws the next step's noise (fused), + N*4P written.
-    Duration: HIP events around each launch on the context stream (kernel_us).  This agrees with
-    rocprofv3's kernel-trace average for the same kernel (profiles/).  event_floor_us (the same event
-    pair around an empty kernel) is reported beside it for reference and is NOT subtracted: it holds a
-    minimal kernel's own duration as well as dispatch.
+    achieved = ALGORITHMIC bytes (each noise row read once + one cost written, 4P+4 per
+    rollout, x the rows one launch processes) / the launch's average duration (srbd_time_kernels: one
+    hipEvent pair on the context stream around back-to-back launches; agrees with rocprofv3's
+    kernel-trace average, profiles/).  The fused next-step draws (N*4P stored) are work the launch
+    also does but not algorithmic bytes of the rollout: reported as launch_bytes beside it.
+    traffic = HBM bytes per launch from the rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE).
     """
     P = w.num_params()
-    fused = "fused_rollout_us" in kern
+    fused = kern.get("fused_rollout_us", 0.0) > 0
     us = kern["fused_rollout_us"] if fused else kern["rollout_us"]
-    floor = kern.get("event_floor_us", 0.0)
-    algo = n_local * (4 * P + 4) + (n_local * 4 * P if fused else 0)
+    algo = n_local * (4 * P + 4)
     achieved = algo / (us * 1e-6) / 1e9
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-            "kernel": "rollout_quad_kernel" + (" (+ next-step Philox blocks)" if fused else ""),
-            "kernel_us": round(us, 3), "event_floor_us": round(floor, 3),
-            "algorithmic_bytes_per_launch": algo}
+            "kernel": "rollout_quad_kernel / rollout_kernel" + (" (+ next-step Philox blocks)" if fused else ""),
+            "kernel_us": round(us, 3), "algorithmic_bytes_per_launch": algo,
+            "launch_bytes": algo + (n_local * 4 * P if fused else 0), "bytes_per_rollout": 4 * P + 4}
 
 
 def pmc_traffic(workload_name: str):
@@ -78,30 +144,42 @@ def pmc_traffic(workload_name: str):
         return None
 
 
-def cpu_baseline(w: Workload, seconds: float):
-    """The C oracle (OpenMP, all host threads offered) on bounded full C2 steps."""
+def cpu_baseline(w, seconds: float):
+    """The C port of the step (oracle/srbd_oracle.c, OpenMP over samples) on every usable host core, on
+    a bounded sample of full steps of the same workload (the JAX-CPU reference cannot run: JAX absent)."""
+    import numpy as np
+
     sys.path.insert(0, ROOT)
     from oracle import c_oracle as co  # test-infrastructure CPU port, used only as this baseline
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
-    cfg = co.make_cfg(N=w.num_samples, H=w.horizon, method=1 if w.method == "mppi" else 0, param_kind=0,
+    cores = host_cores()
+    threads = cores["usable"]
+    method = {"random_sampling": 0, "mppi": 1, "cem_mppi": 2}[w.method]
+    kind = {"zero_order": 0, "linear_spline": 1, "cubic_spline": 2}[w.parametrization]
+    cfg = co.make_cfg(N=w.num_samples, H=w.horizon, method=method, param_kind=kind, num_splines=w.num_splines,
                       mass=w.mass, inertia=w.inertia, sigma_mppi=w.sigma)
-    s, r, c = inputs(w, 0)
-    best = np.zeros(w.num_params(), np.float32)
-    co.step(cfg, s, r, c, best, seed=42, counter=0, nthreads=threads)  # warm-up
+    ins = step_inputs(w, 8)
+    P = co.num_params(cfg)
+    best = np.zeros(P, np.float32)
+    sigma = np.full(P, 3.0, np.float32) if w.method == "cem_mppi" else None
+    s, r, c = ins[0]
+    co.step(cfg, s, r, c, best, sigma=sigma, seed=42, counter=0, nthreads=threads)  # warm-up
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds and n < 2000:
-        best, *_ = co.step(cfg, s, r, c, best, seed=42, counter=n + 1, nthreads=threads)
+        s, r, c = ins[n % len(ins)]
+        best, sig, *_ = co.step(cfg, s, r, c, best, sigma=sigma, seed=42, counter=n + 1, nthreads=threads)
+        sigma = sig if sigma is not None else None
         n += 1
     dt = time.perf_counter() - t0
     return {"value": round(w.num_samples * n / dt, 1), "unit": "rollouts/s", "cores": threads, "kind": "port",
-            "sample": f"{n} full MPPI steps of C2 (N={w.num_samples}, H={w.horizon}; Philox noise, rollouts, "
-                      f"softmax update, GRFs) in {dt:.1f} s, oracle/srbd_oracle.c OpenMP",
+            "nproc": cores["nproc"], "affinity_cpus": cores["affinity"], "cgroup_quota_cpus": cores["cgroup_quota_cpus"],
+            "sample": f"{n} full {w.method} steps of {w.name} (N={w.num_samples}, H={w.horizon}; Philox noise, "
+                      f"rollouts, update, GRFs) in {dt:.1f} s, oracle/srbd_oracle.c OpenMP on {threads} threads "
+                      f"(all usable host CPUs: affinity {cores['affinity']}, nproc {cores['nproc']})",
             "ms_per_step": round(1e3 * dt / max(n, 1), 3)}
 
 
-def interface_latency(w: Workload, steps: int):
+def interface_latency(w, steps: int):
     """p50 / p99 ms of one MPC step through the reference's Python plugin API at the workload's shape:
     PeriodicGaitGenerator.compute_contact_sequence (C++ host producer) + SRBDControllerInterface.
     compute_control (prepare_state_and_reference, with_newkey, jitted_compute_control, LegsAttr masking),
@@ -109,11 +187,13 @@ def interface_latency(w: Workload, steps: int):
     import copy
     import types
 
+    import numpy as np
+
     from quadruped_pympc_amd import config as base
     from quadruped_pympc_amd.config import ROBOTS
     from quadruped_pympc_amd.helpers.periodic_gait_generator import PeriodicGaitGenerator
     from quadruped_pympc_amd.interfaces.srbd_controller_interface import SRBDControllerInterface
-    from quadruped_pympc_amd.synthetic import GAITS
+    from quadruped_pympc_amd.synthetic import GAITS, inputs
 
     cfg = types.SimpleNamespace(**{k: copy.deepcopy(getattr(base, k)) for k in
                                    ("robot", "mass", "inertia", "hip_height", "gravity_constant", "mpc_params",
@@ -121,7 +201,7 @@ def interface_latency(w: Workload, steps: int):
     cfg.robot, cfg.mass, cfg.inertia = w.robot, ROBOTS[w.robot][0], np.array(ROBOTS[w.robot][1])
     cfg.mpc_params.update(horizon=w.horizon, sampling_method=w.method, control_parametrization=w.parametrization,
                           num_splines=w.num_splines, num_parallel_computations=w.num_samples, sigma_mppi=w.sigma,
-                          grf_max=cfg.mass * 9.81)
+                          grf_max=cfg.mass * 9.81, device_id=0)
     iface = SRBDControllerInterface(cfg)
     gtype, freq, duty = GAITS[w.gait]
     pgg = PeriodicGaitGenerator(duty, freq, gtype, w.horizon)
@@ -153,6 +233,8 @@ def tamols_latency(calls: int):
     """p50 / p99 ms of one TAMOLS foothold adaptation for the four legs on stepping_stones_medium (C4):
     13 x 7 patches raycast on the GPU from the device-resident scene + the TAMOLS search, one call
     (srbd_tamols_run_terrain), Go2 trot stance feet."""
+    import numpy as np
+
     from quadruped_pympc_amd import config
     from quadruped_pympc_amd.helpers.terrain import GpuTerrain
     from quadruped_pympc_amd.helpers.visual_foothold_adaptation import TamolsSearch, tamols_params_struct
@@ -181,29 +263,60 @@ def tamols_latency(calls: int):
             "path": "srbd_tamols_run_terrain: 4 x 13 x 7 raycast patches + TAMOLS, stepping_stones_medium"}
 
 
-def bench_single(w, args):
-    ctx = _lib.Context(make_cfg(w, w.num_samples, 0, 1, 0))
-    s, r, c = inputs(w, 0)
-    best = np.zeros(ctx.P, np.float32)
-    for k in range(max(1, args.warmup)):
-        best, _, res, _ = ctx.step(s, r, c, best, seed=42, counter=k)
-    # host-to-host latency of one MPC step
-    lat = []
-    for k in range(args.latency_steps):
+# ---------------------------------------------------------------------------------------------- runs
+def run_steps(step_fn, ins, best, first_counter, count, lat=None):
+    """`count` host-to-host steps, counters consecutive (the fused next-step draws are used)."""
+    for i in range(count):
+        s, r, c = ins[(first_counter + i) % len(ins)]
         t0 = time.perf_counter()
-        best, _, res, _ = ctx.step(s, r, c, best, seed=42, counter=1000 + k)
-        lat.append(time.perf_counter() - t0)
-    # throughput: K device-resident steps, warm-started on the device
-    ctx.bench_device_steps(max(1, args.warmup))
+        best = step_fn(s, r, c, best, first_counter + i)
+        if lat is not None:
+            lat.append(time.perf_counter() - t0)
+    return best
+
+
+def bench_single(_lib, w, args):
+    import numpy as np
+
+    ctx = _lib.Context(make_cfg(_lib, w, w.num_samples, 0, 1, 0))
+    ins = step_inputs(w, 32)
+    best = np.zeros(ctx.P, np.float32)
+    sigma = np.full(ctx.P, 3.0, np.float32) if w.method == "cem_mppi" else None
+    state = {"sigma": sigma}
+
+    def step(s, r, c, b, k):
+        b, sg, _, _ = ctx.step(s, r, c, b, sigma=state["sigma"], seed=42, counter=k)
+        if sg is not None:
+            state["sigma"] = sg
+        return b
+
+    k = 0
+    best = run_steps(step, ins, best, k, max(1, args.warmup))
+    k += max(1, args.warmup)
+    lat = []
+    if args.steps < args.latency_steps:  # latency sample of >= latency_steps steps besides the timed region
+        best = run_steps(step, ins, best, k, args.latency_steps, lat)
+        k += args.latency_steps
+    timed = []
     t0 = time.perf_counter()
-    ms_dev = ctx.bench_device_steps(args.steps)
+    best = run_steps(step, ins, best, k, args.steps, timed)  # srbd_step returns with outputs on the host
     wall = time.perf_counter() - t0
-    kern = ctx.time_kernels(50)
+    if not lat:
+        lat = timed
+    dev = None
+    if args.device_steps > 0:
+        ctx.bench_device_steps(max(1, args.warmup))
+        ms = ctx.bench_device_steps(args.device_steps)
+        dev = {"value": round(w.num_samples * args.device_steps / (ms * 1e-3), 1),
+               "ms_per_step": round(ms / args.device_steps, 5), "steps": args.device_steps}
+    kern = ctx.time_kernels(200)
     ctx.close()
-    return dict(n_total=w.num_samples, n_local=w.num_samples, wall=wall, ms_dev=ms_dev, lat=lat, kern=kern)
+    return dict(n_total=w.num_samples, n_local=w.num_samples, wall=wall, lat=lat, kern=kern, dev=dev,
+                transport=None)
 
 
-def bench_multi(w, args, rank, world, local_rank):
+def bench_multi(_lib, w, args, rank, world, local_rank, scaling):
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -211,89 +324,119 @@ def bench_multi(w, args, rank, world, local_rank):
 
     torch.cuda.set_device(local_rank)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    n_total = w.num_samples * world  # weak scaling: N rows per GPU of one MPC problem
-    mpc = ShardedSamplingMPC(make_cfg(w, n_total, rank, world, local_rank), rank, world, local_rank)
-    s, r, c = inputs(w, 0)
+    n_total = w.num_samples if scaling == "strong" else w.num_samples * world
+    mpc = ShardedSamplingMPC(make_cfg(_lib, w, n_total, rank, world, local_rank), rank, world, local_rank,
+                             transport=args.transport)
+    ins = step_inputs(w, 32)
     best = np.zeros(mpc.P, np.float32)
-    for k in range(max(1, args.warmup)):
-        best, _, _ = mpc.step(s, r, c, best, seed=42, counter=k)
+    sigma = np.full(mpc.P, 3.0, np.float32) if w.method == "cem_mppi" else None
+    state = {"sigma": sigma}
+
+    def step(s, r, c, b, k):
+        b, sg, _ = mpc.step(s, r, c, b, sigma=state["sigma"], seed=42, counter=k)
+        if sg is not None:
+            state["sigma"] = sg
+        return b
+
+    k = 0
+    best = run_steps(step, ins, best, k, max(1, args.warmup))
+    k += max(1, args.warmup)
     lat = []
-    for k in range(args.latency_steps):
+    if args.steps < args.latency_steps:
         dist.barrier()
-        t0 = time.perf_counter()
-        best, _, _ = mpc.step(s, r, c, best, seed=42, counter=1000 + k)
-        lat.append(time.perf_counter() - t0)
-    mpc.device_steps(max(1, args.warmup))
+        best = run_steps(step, ins, best, k, args.latency_steps, lat)
+        k += args.latency_steps
     dist.barrier()
     torch.cuda.synchronize()
+    timed = []
     t0 = time.perf_counter()
-    mpc.device_steps(args.steps)  # rollout -> ncclAllGather -> merge per step, driven from C++
+    best = run_steps(step, ins, best, k, args.steps, timed)  # rollout -> xGMI record exchange -> merge
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    dist.barrier()
     t = torch.tensor([wall], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall = float(t.item())
+    if not lat:
+        lat = timed
+    dev = None
+    if args.device_steps > 0:
+        mpc.device_steps(max(1, args.warmup))
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        mpc.device_steps(args.device_steps)
+        torch.cuda.synchronize()
+        dwall = time.perf_counter() - t0
+        t = torch.tensor([dwall], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dwall = float(t.item())
+        dev = {"value": round(n_total * args.device_steps / dwall, 1),
+               "ms_per_step": round(1e3 * dwall / args.device_steps, 5), "steps": args.device_steps}
     n_local = mpc.ctx.n_local
-    kern = mpc.ctx.time_kernels(20)
+    kern = mpc.ctx.time_kernels(100)
+    transport = mpc.transport
     mpc.close()
     dist.destroy_process_group()
-    return dict(n_total=n_total, n_local=n_local, wall=wall, ms_dev=None, lat=lat, kern=kern)
+    return dict(n_total=n_total, n_local=n_local, wall=wall, lat=lat, kern=kern, dev=dev, transport=transport)
 
 
-def main():
-    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--latency-steps", type=int, default=500)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--extras", type=int, default=200,
-                    help="steps of the supplementary interface / TAMOLS latency probes (0: skip)")
-    ap.add_argument("--force-sharded", action="store_true", help=argparse.SUPPRESS)  # 1-GPU rehearsal
-    args = ap.parse_args()
-    rank = int(os.environ.get("RANK", "0"))
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args, argv))  # before torch / the HIP library are loaded
+    rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    sys.path.insert(0, os.path.join(ROOT, "quadruped-pympc-tamols_amd"))
+    if world > 1:
+        import torch  # noqa: F401  -- before libsrbd_hip.so: one HIP runtime per process (see _lib.py)
+    import numpy as np
+
+    from quadruped_pympc_amd import _lib
+    from quadruped_pympc_amd.synthetic import CONFIGS
+
     w = CONFIGS[args.config]
-    if world > 1 or args.force_sharded:
-        out = bench_multi(w, args, rank, world, local_rank)
+    scaling = args.scaling or ("strong" if args.config == "c5" else "weak")
+    if world > 1:
+        out = bench_multi(_lib, w, args, rank, world, local_rank, scaling)
     else:
-        out = bench_single(w, args)
+        out = bench_single(_lib, w, args)
     if rank != 0:
         return
     lat = np.array(out["lat"]) * 1e3
-    ms_per_step = 1e3 * out["wall"] / args.steps
-    value = out["n_total"] * args.steps / out["wall"]
     line = {
         "metric": METRIC,
-        "value": round(value, 1),
+        "value": round(out["n_total"] * args.steps / out["wall"], 1),
         "unit": "rollouts/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 5),
+        "ms_per_step": round(1e3 * out["wall"] / args.steps, 5),
         "p50_step_ms": round(float(np.percentile(lat, 50)), 4),
         "p99_step_ms": round(float(np.percentile(lat, 99)), 4),
+        "latency_steps": int(lat.size),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (fixed-seed Go2 state/reference, PGG trot contact sequence, device Philox noise)",
-        "config": {"workload": w.name, "num_samples": out["n_total"], "horizon": w.horizon, "method": w.method,
-                   "parametrization": w.parametrization, "robot": w.robot, "gait": w.gait,
-                   "parallelism": f"rows sharded over {world} GPU(s)" if world > 1 else "single GPU"},
+        "data": "synthetic (fixed-seed robot states / references, PGG contact sequences, device Philox noise)",
+        "config": {"workload": w.name, "num_samples": out["n_total"], "rows_per_gpu": out["n_local"],
+                   "horizon": w.horizon, "method": w.method, "parametrization": w.parametrization,
+                   "robot": w.robot, "gait": w.gait,
+                   "parallelism": (f"rows sharded over {world} GPUs ({scaling} scaling), record exchange: "
+                                   f"{out['transport']}") if world > 1 else "single GPU"},
+        "step": "host-to-host srbd_step (state/ref/contact/params in, GRFs/pred/params out; noise device-resident)",
+        "device_chain": out["dev"],
         "kernels_us": {k: round(v, 3) for k, v in out["kern"].items()},
         "roofline": roofline(w, out["n_local"], out["kern"], pmc_traffic(w.name)),
     }
-    if out["ms_dev"] is not None:
-        line["device_ms_per_step"] = round(out["ms_dev"] / args.steps, 5)
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
     else:
         line["cpu_baseline"] = None
-    if world == 1 and args.extras:  # supplementary latencies of the callers either side of the path
+    if world == 1 and args.extras and args.config in ("c2", "c4"):  # the callers either side of the path
         line["interface_step"] = interface_latency(w, args.extras)
         line["tamols_c4"] = tamols_latency(args.extras)
     print(json.dumps(line), flush=True)

@@ -172,11 +172,11 @@ int srbd_make_record_host(const srbd_config* cfg, int32_t rank, int32_t world_si
 /* Measurement: replay `steps` device-resident steps (RNG -> rollout -> reduction -> warm start
  * written back on device) back to back; returns elapsed ms (hipEvents on the context stream). */
 int srbd_bench_device_steps(srbd_ctx* ctx, int32_t steps, float* elapsed_ms);
-/* Average per-launch duration (us) of each kernel of one step, hipEvents around every launch.
- * fused_rollout_us: the rollout launch that also draws the next step's noise (the form the step
- * chain runs when fusion applies; 0 otherwise).  event_floor_us: the same event pair around an
- * empty kernel (dispatch + kernel boundary; rocprof's kernel durations exclude it).  Any out
- * pointer may be NULL. */
+/* Average per-launch duration (us) of each kernel of one step: one hipEvent pair on the context
+ * stream around `iters` back-to-back launches of that kernel (agrees with rocprofv3's kernel-trace
+ * average).  fused_rollout_us: the rollout launch that also draws the next step's noise (the form
+ * the step runs when fusion applies; 0 otherwise).  event_floor_us: the same measurement of an
+ * empty kernel (launch-to-launch spacing).  Any out pointer may be NULL. */
 int srbd_time_kernels(srbd_ctx* ctx, int32_t iters, float* rollout_us, float* rng_us, float* reduce_us,
                       float* fused_rollout_us, float* event_floor_us);
 

@@ -1279,10 +1279,14 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_xchg_kernel(const ModelCo
     float* mine = x.stage + (size_t)x.rank * stride;
     merge_body(mc, in, recs, nrec, rec_stride, 0, noise, mine, nullptr, 0, 0, nullptr, nullptr, 0);
     __syncthreads();
+    // slot parity: epoch & 1.  A peer can run at most one exchange ahead of this rank (it cannot pass
+    // its next wait before this rank has published that epoch, i.e. finished copying this one), so
+    // its epoch+1 record lands in the other half and never overwrites a slot still being copied.
+    const size_t half = (size_t)(epoch & 1u) * x.world * stride;
     for (int i = tid; i < (x.world - 1) * stride; i += T) {
         const int q = i / stride, k = i - q * stride;
         const int p = q < x.rank ? q : q + 1;
-        __hip_atomic_store(reinterpret_cast<uint32_t*>(x.peer_mailbox[p]) + (size_t)x.rank * stride + k,
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(x.peer_mailbox[p]) + half + (size_t)x.rank * stride + k,
                            __float_as_uint(mine[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1297,7 +1301,8 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_xchg_kernel(const ModelCo
     __syncthreads();
     if (tid < x.world && tid != x.rank) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(x.flags + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+        // >= (wrap-safe): a peer one exchange ahead has already moved its flag on to epoch + 1
+        while ((int32_t)(__hip_atomic_load(x.flags + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
             __builtin_amdgcn_s_sleep(2);
             if (__builtin_amdgcn_s_memrealtime() - t0 > XCHG_TIMEOUT_TICKS) {
                 timed_out = 1;
@@ -1319,7 +1324,7 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_xchg_kernel(const ModelCo
     for (int i = tid; i < (x.world - 1) * stride; i += T) {
         const int q = i / stride, k = i - q * stride;
         const size_t o = (size_t)(q < x.rank ? q : q + 1) * stride + k;
-        x.stage[o] = __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(x.mailbox) + o,
+        x.stage[o] = __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(x.mailbox) + half + o,
                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     }
     __syncthreads();
@@ -1515,7 +1520,8 @@ int launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nre
 __global__ void xchg_probe_kernel(XchgArgs x, int* ok) {
     const int tid = threadIdx.x;
     const uint32_t epoch = *x.epoch + 1;
-    if (tid < x.world) x.peer_mailbox[tid][(size_t)x.rank * x.stride] = (float)x.rank;
+    const size_t half = (size_t)(epoch & 1u) * x.world * x.stride;
+    if (tid < x.world) x.peer_mailbox[tid][half + (size_t)x.rank * x.stride] = (float)x.rank;
     __threadfence_system();
     __syncthreads();
     if (tid < x.world)
@@ -1526,12 +1532,13 @@ __global__ void xchg_probe_kernel(XchgArgs x, int* ok) {
     if (tid < x.world) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         bool seen = false;
-        while (!(seen = __hip_atomic_load(x.flags + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == epoch)) {
+        while (!(seen = (int32_t)(__hip_atomic_load(x.flags + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) -
+                                  epoch) >= 0)) {
             __builtin_amdgcn_s_sleep(2);
             if (__builtin_amdgcn_s_memrealtime() - t0 > XCHG_TIMEOUT_TICKS) break;
         }
         __atomic_thread_fence(__ATOMIC_ACQUIRE);
-        if (!seen || x.mailbox[(size_t)tid * x.stride] != (float)tid) bad = 1;
+        if (!seen || x.mailbox[half + (size_t)tid * x.stride] != (float)tid) bad = 1;
     }
     __syncthreads();
     if (tid == 0) {

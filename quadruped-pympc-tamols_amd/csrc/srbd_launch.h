@@ -59,8 +59,9 @@ constexpr int MERGE_PER_BLOCK = 32;
 constexpr int MERGE_MAX_PARTIALS = 64;
 // to_outputs: the merge produces step outputs (column-split final level), else a rank record.
 int merge_partials(int nrec, bool to_outputs);
-// xGMI exchange of rank records (merge_xchg_kernel).  mailbox: this rank's W slots of one rank
-// record each; flags: W epochs (slot r written by rank r); peer_*: every rank's mailbox / flags as
+// xGMI exchange of rank records (merge_xchg_kernel).  mailbox: this rank's 2 x W slots of one rank
+// record each (half epoch & 1, slot r of a half written by rank r); flags: W epochs (word r written
+// by rank r; waits accept >= epoch); peer_*: every rank's mailbox / flags as
 // this GPU addresses them (IPC-mapped; entry `rank` is the local one).  epoch: this rank's exchange
 // counter in device memory, advanced by every exchange kernel (so the chain can be a replayed graph).
 constexpr int XCHG_MAX_WORLD = 16;

@@ -10,62 +10,17 @@
 
 #include <string>
 
-#include "srbd_launch.h"
+#include "terrain_ray.h"
 
 namespace srbd {
-
-__device__ __forceinline__ void consider(double top, double ray_z, double& best, int& hit) {
-    if (top <= ray_z && top > best) {
-        best = top;
-        hit = 1;
-    }
-}
 
 __global__ void __launch_bounds__(256) terrain_patch_kernel(const TerrainDev t, const PatchJob j) {
     const int per = j.rows * j.cols;
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= j.npatch * per) return;
     const int p = g / per, r = g % per, i = r / j.cols, k = r % j.cols;
-    const double c = j.cs_yaw[2 * p], s = j.cs_yaw[2 * p + 1];
-    const double dx = ((double)i - (double)(j.rows - 1) / 2.0) * j.dist_x;
-    const double dy = ((double)k - (double)(j.cols - 1) / 2.0) * j.dist_y;
-    const double x = j.centers[3 * p] + c * dx - s * dy;
-    const double y = j.centers[3 * p + 1] + s * dx + c * dy;
-    double best = -INFINITY;
-    int hit = 0;
-    if (t.has_ground) consider(t.ground_z, j.ray_z, best, hit);
-    // unrolled so several primitives' (wave-uniform, scalar) loads are in flight per round trip
-#pragma unroll 4
-    for (int q = 0; q < t.nprims; ++q) {
-        const srbd_terrain_prim& pr = t.prims[q];
-        const double ux = x - pr.cx, uy = y - pr.cy;
-        bool in;
-        if (pr.type == SRBD_PRIM_BOX) {
-            const double cb = t.cs[2 * q], sb = t.cs[2 * q + 1];
-            const double u = cb * ux + sb * uy, v = cb * uy - sb * ux;
-            in = fabs(u) <= pr.a && fabs(v) <= pr.b;
-        } else {
-            in = ux * ux + uy * uy <= pr.a * pr.a;
-        }
-        if (in) consider(pr.cz + pr.c, j.ray_z, best, hit);
-    }
-    if (t.hf) {
-        const double fx = (x - t.hf_x0) / t.hf_dx, fy = (y - t.hf_y0) / t.hf_dy;
-        if (fx >= 0.0 && fy >= 0.0 && fx <= (double)(t.hf_nx - 1) && fy <= (double)(t.hf_ny - 1)) {
-            int i0 = (int)floor(fx), j0 = (int)floor(fy);
-            i0 = i0 > t.hf_nx - 2 ? t.hf_nx - 2 : i0;
-            j0 = j0 > t.hf_ny - 2 ? t.hf_ny - 2 : j0;
-            const double tx = fx - (double)i0, ty = fy - (double)j0;
-            const double z00 = t.hf[i0 * t.hf_ny + j0], z10 = t.hf[(i0 + 1) * t.hf_ny + j0];
-            const double z01 = t.hf[i0 * t.hf_ny + j0 + 1], z11 = t.hf[(i0 + 1) * t.hf_ny + j0 + 1];
-            const double z = tx >= ty ? z00 + tx * (z10 - z00) + ty * (z11 - z10) : z00 + ty * (z01 - z00) + tx * (z11 - z01);
-            consider(z, j.ray_z, best, hit);
-        }
-    }
-    double* o = j.out + 3 * (size_t)g;
-    o[0] = x;
-    o[1] = y;
-    o[2] = hit ? best : t.miss_z;
+    terrain_ray_point(t, j.centers[3 * p], j.centers[3 * p + 1], j.cs_yaw[2 * p], j.cs_yaw[2 * p + 1], j.rows, j.cols,
+                      i, k, j.dist_x, j.dist_y, j.ray_z, j.out + 3 * (size_t)g);
 }
 
 void launch_terrain_patches(const TerrainDev& t, const PatchJob& j, hipStream_t s) {

@@ -11,7 +11,8 @@ code written against the reference reads them unchanged.  Differences:
   as ``ref_z``);
 * ``mpc_params['type']`` defaults to ``'sampling'`` (the only controller this
   package provides; gradient/acados controllers are out of scope);
-* optional keys ``device_id`` (HIP ordinal) and ``num_elite`` (CEM elite size,
+* optional keys ``device_id`` (HIP ordinal, or ``'auto'``: replica i -> GPU i mod G, see
+  ``runtime.py``) and ``num_elite`` (CEM elite size,
   reference hard-codes 10) and ``use_hip_graph``.
 
 Use :func:`set_robot` to switch robot (the reference edits ``robot`` in-file).
@@ -85,7 +86,7 @@ mpc_params = {
     "sigma_random_sampling": [0.2, 3, 10],
     "shift_solution": False,
     # extensions (this package)
-    "device_id": 0,
+    "device_id": "auto",
     "num_elite": 10,
     "use_hip_graph": True,
 }

@@ -31,8 +31,8 @@ import sys
 
 import numpy as np
 
-from ... import config as default_config
 from ... import _lib
+from ...runtime import active_config, resolve_device_id
 
 f32 = np.float32
 
@@ -69,7 +69,7 @@ class Sampling_MPC:
     """This is a small class that implements a sampling based control law (MI355X HIP backend)."""
 
     def __init__(self, config_module=None):
-        cfg = config_module if config_module is not None else default_config
+        cfg = active_config(config_module)  # the reference's quadruped_pympc.config when installed
         mp = cfg.mpc_params
         self._cfg = cfg
         device = mp["device"]
@@ -87,7 +87,8 @@ class Sampling_MPC:
         self.max_sampling_forces_z = 30
         if device != "gpu":
             raise RuntimeError("Sampling_MPC (HIP) runs on the GPU only; mpc_params['device'] must be 'gpu'")
-        self.device_id = int(mp.get("device_id", 0))
+        # ordinal or 'auto' (default): replica process i -> GPU i mod G, resolved at context creation
+        self.device_id = mp.get("device_id", "auto")
 
         # centroidal_nmpc_jax.py:52-93
         if self.control_parametrization == "linear_spline":
@@ -144,6 +145,7 @@ class Sampling_MPC:
     # ------------------------------------------------------------------ device
     def _srbd_config(self) -> "_lib.SrbdConfig":
         mp = self._cfg.mpc_params
+        self.device_id = resolve_device_id(self.device_id)
         return _lib.make_config(
             num_samples=self.num_parallel_computations, horizon=self.horizon, method=self.sampling_method,
             parametrization=self.control_parametrization, num_splines=self.num_spline,

@@ -22,7 +22,7 @@ import ctypes as C
 import numpy as np
 
 from .. import _lib
-from .. import config as default_config
+from ..runtime import active_config, resolve_device_id
 from .legs_attr import LegsAttr
 
 LEGS = ("FL", "FR", "RL", "RR")
@@ -130,7 +130,7 @@ class TamolsSearch:
 
 class VisualFootholdAdaptation:
     def __init__(self, legs_order, adaptation_strategy="height", config_module=None, device_id=None):
-        cfg = config_module if config_module is not None else default_config
+        cfg = active_config(config_module)  # the reference's quadruped_pympc.config when installed
         self.footholds_adaptation = LegsAttr(FL=np.array([0, 0, 0]), FR=np.array([0, 0, 0]), RL=np.array([0, 0, 0]),
                                              RR=np.array([0, 0, 0]))
         self.footholds_constraints = LegsAttr(FL=None, FR=None, RL=None, RR=None)
@@ -140,7 +140,7 @@ class VisualFootholdAdaptation:
         if adaptation_strategy == "vfa":
             raise ImportError("VFA strategy requested but VFA module could not be imported.")
         self._search = None
-        self._device_id = cfg.mpc_params.get("device_id", 0) if device_id is None else device_id
+        self._device_id = cfg.mpc_params.get("device_id", "auto") if device_id is None else device_id
         if adaptation_strategy == "tamols":
             self.tamols_params = cfg.simulation_params.get("tamols_params", {})
             self.robot_name = cfg.robot
@@ -162,6 +162,7 @@ class VisualFootholdAdaptation:
     @property
     def search(self) -> TamolsSearch:
         if self._search is None:
+            self._device_id = resolve_device_id(self._device_id)
             self._search = TamolsSearch(self._device_id)
         return self._search
 

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .. import config as default_config
+from ..runtime import active_config
 from ..helpers.legs_attr import LegsAttr
 
 
@@ -18,7 +18,7 @@ class SRBDControllerInterface:
     """This is an interface for a controller that uses the SRBD method to optimize the gait"""
 
     def __init__(self, config_module=None):
-        cfg = config_module if config_module is not None else default_config
+        cfg = active_config(config_module)  # the reference's quadruped_pympc.config when installed
         self._cfg = cfg
         self.type = cfg.mpc_params["type"]
         self.mpc_dt = cfg.mpc_params["dt"]

@@ -20,12 +20,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 @pytest.fixture(scope="module")
 def worker_results():
+    # one hardware queue per rank stream (8 ranks in the C5 case; HIP's default is 4 queues)
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
     p = subprocess.run([sys.executable, os.path.join(HERE, "xgmi_worker.py")], capture_output=True, text=True,
-                       timeout=240)
+                       timeout=240, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     return json.loads(p.stdout.strip().splitlines()[-1])
 
 
-@pytest.mark.parametrize("case", ["mppi", "cem_mppi", "random_sampling", "mppi_w3", "mppi_ga_w3", "timeout"])
+@pytest.mark.parametrize("case", ["mppi", "cem_mppi", "random_sampling", "mppi_w3", "mppi_ga_w3", "c5_w8", "timeout"])
 def test_xgmi_exchange_in_process(worker_results, case):
     assert worker_results[case] == "ok", worker_results[case]

@@ -3,8 +3,9 @@
 W ranks as W contexts on the one GPU of the box, mailboxes connected in-process
 (srbd_xgmi_connect_local), each rank's blocking call in its own thread (ctypes releases the GIL), so
 the W exchange kernels wait for each other exactly as W GPUs do.  A fresh process holds only these
-contexts' streams, so each rank's stream gets its own hardware queue (GPU_MAX_HW_QUEUES=4): two
-ranks' kernels sharing one queue would serialise and the first would time out waiting for the other.
+contexts' streams, so each rank's stream gets its own hardware queue (the test starts this worker
+with GPU_MAX_HW_QUEUES=16 for the 8-rank case; HIP's default is 4): two ranks' kernels sharing one
+queue would serialise and the first would time out waiting for the other.
 
 Prints one JSON object: {case: "ok" | error text}.
 """
@@ -59,8 +60,8 @@ def probe(cx):
     return r.value
 
 
-def exchange_case(method, W=2, N=4000, ga=False):
-    case = make_case("c2", N=N, method=method, seed=23)
+def exchange_case(method, W=2, N=4000, ga=False, wkey="c2"):
+    case = make_case(wkey, N=N, method=method, seed=23)
     freqs = np.random.default_rng(1).choice(np.array([1.4, 2.0, 2.4], f32), N).astype(f32) if ga else None
     full = _lib.Context(product_cfg(case))
     if ga:
@@ -99,8 +100,21 @@ def exchange_case(method, W=2, N=4000, ga=False):
         cx.check(_lib.lib.srbd_sharded_device_steps(cx.h, n, C.byref(ms)), "srbd_sharded_device_steps")
         return ms.value
 
+    def synced(cx):
+        b = np.zeros(cx.P, f32)
+        sg = np.zeros(cx.P, f32)
+        res = _lib.SrbdResult()
+        cx.check(_lib.lib.srbd_sync_result(cx.h, _lib.fptr(b), _lib.fptr(sg), C.byref(res)), "srbd_sync_result")
+        return b, sg, np.array(res.grf, f32), res.best_index
+
     for n in (6, 7):  # two-step graphs, then the odd tail
         assert all(ms > 0 for ms in run_threads([lambda cx=cx: chain(cx, n) for cx in ctxs]))
+        # back-to-back replayed exchanges (one rank may run an exchange ahead of another, the
+        # mailbox halves alternate by epoch): every rank ends on bit-identical outputs
+        fin = [synced(cx) for cx in ctxs]
+        for o in fin[1:]:
+            for a, b in zip(fin[0], o):
+                np.testing.assert_array_equal(a, b)
     outs = run_threads([lambda cx=cx: host_step(cx) for cx in ctxs])
     for b, _, res, _ in outs:
         assert res.best_index == r0.best_index
@@ -130,7 +144,9 @@ def main():
     cases = [("mppi", lambda: exchange_case("mppi")), ("cem_mppi", lambda: exchange_case("cem_mppi")),
              ("random_sampling", lambda: exchange_case("random_sampling")),
              ("mppi_w3", lambda: exchange_case("mppi", W=3, N=3001)),
-             ("mppi_ga_w3", lambda: exchange_case("mppi", W=3, N=3001, ga=True)), ("timeout", timeout_case)]
+             ("mppi_ga_w3", lambda: exchange_case("mppi", W=3, N=3001, ga=True)),
+             # C5 (HyQReal bound MPPI, N=524 288) over 8 ranks of 65 536 rows: needs 8 hardware queues
+             ("c5_w8", lambda: exchange_case("mppi", W=8, N=524288, wkey="c5")), ("timeout", timeout_case)]
     for name, fn in cases:
         try:
             fn()
