@@ -253,7 +253,7 @@ def tamols_latency(calls: int):
         t0 = time.perf_counter()
         out = srch.run_terrain(ter, 0.0, seeds, hips, ps, forward_vel=np.array([0.5, 0.0, 0.0]),
                                base_position=np.array([1.03, 0.0, 0.35]), current_contact=contact,
-                               current_feet_pos=feet)
+                               current_feet_pos=feet, want_scores=False, want_heightmaps=False)
         lat.append(time.perf_counter() - t0)
     srch.close()
     ter.close()

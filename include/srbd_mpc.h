@@ -294,14 +294,21 @@ const char* srbd_terrain_last_error(const srbd_terrain* terrain);
 int srbd_terrain_patches(srbd_terrain* terrain, const double* centers, const double* yaws, int32_t npatch,
                          int32_t rows, int32_t cols, double dist_x, double dist_y, double ray_z, double* out);
 /* srbd_tamols_run with the four patches raycast on the device from `terrain` (centres = the seeds,
- * one yaw) in the same stream: no host round trip of the patch.  out_heightmaps (4 x rows x cols x 3)
- * may be NULL. */
+ * one yaw) in the same launch (the heightmap sensor fused into the search): no host round trip of the
+ * patch.  out_heightmaps (4 x rows x cols x 3) and out_scores may be NULL (then only the footholds,
+ * boxes, validity and seed heights cross PCIe). */
 int srbd_tamols_run_terrain(srbd_tamols_ctx* ctx, srbd_terrain* terrain, double yaw, int32_t rows, int32_t cols,
                             double dist_x, double dist_y, double ray_z, const double* seeds, const double* hips,
                             const double* forward_vel, const double* base_pos, const int32_t* contact,
                             const double* feet, const srbd_tamols_params* params, double* out_footholds,
                             double* out_boxes, int32_t* out_valid, double* out_scores, double* out_seed_heights,
                             double* out_heightmaps);
+/* Diagnostic: enable != 0 stamps the phases of the following TAMOLS calls; out_us[5] (may be NULL)
+ * receives the last call's mean per-block durations of (patch, queries, scores, slice argmin + count)
+ * and the span from the first block's start to the last leg's end, in us.  enable == 0 turns it off. */
+int srbd_tamols_phases(srbd_tamols_ctx* ctx, int32_t enable, float* out_us);
+/* Diagnostic: the last call's raw stamps, 4 legs x 16 blocks x 8 uint64 (100 MHz). */
+int srbd_tamols_phases_raw(srbd_tamols_ctx* ctx, uint64_t* out);
 
 #ifdef __cplusplus
 }

@@ -1361,18 +1361,24 @@ extern "C" int srbd_selftest_div(const float* a, const float* b, int32_t n, floa
 }
 
 // ------------------------------------------------------------------ TAMOLS
+// One call = one launch (tamols_fused_kernel): the patches are raycast (or read from host-mapped
+// staging), scored and reduced on the device; the outputs land in host-mapped memory and the call
+// spins on a host-mapped sequence word, so there is no copy command and no stream synchronise.
 struct srbd_tamols_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    double* d_hm = nullptr;
-    // scores (4 nc) | footholds 12 | boxes 24 | seed heights 4 | valid (4 int32 in 2 doubles): one block,
-    // so the results come back in one D2H copy into pinned staging (h_out)
-    double* d_out = nullptr;
-    int* d_valid = nullptr;
+    // host-mapped output block [scores 4 nc | footholds 12 | boxes 24 | seed heights 4 | valid 4 x int32]
     double* h_out = nullptr;
-    double* h_hm = nullptr;  // pinned staging of heightmaps in (srbd_tamols_run) or out (run_terrain)
-    double* d_nn = nullptr;  // phase-A query heights, 4 x (nc * NQ + 1)
+    double* d_out_host = nullptr;
+    double* h_hm = nullptr;  // host-mapped heightmaps: in (srbd_tamols_run) or out (run_terrain)
+    double* d_hm_host = nullptr;
+    double* d_part = nullptr;  // per-block partials
+    unsigned* d_cnt = nullptr;  // block / leg counters (zero between calls)
+    uint32_t* h_flag = nullptr;
+    uint32_t* d_flag = nullptr;
+    uint32_t seq = 0;
     size_t cap_cand = 0;
+    uint64_t* d_dbg = nullptr;  // srbd_tamols_phases: stamps of the last call
     std::string err;
 };
 
@@ -1384,10 +1390,19 @@ extern "C" int srbd_tamols_create(int32_t device_id, srbd_tamols_ctx** out) {
         return fail(nullptr, SRBD_E_NODEVICE, "no HIP device visible (this library has no CPU fallback)");
     srbd_tamols_ctx* t = new srbd_tamols_ctx();
     t->device = device_id;
-    if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess) {
+    bool ok = hipSetDevice(device_id) == hipSuccess &&
+              hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipHostMalloc((void**)&t->h_flag, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) ==
+                  hipSuccess &&
+              hipHostGetDevicePointer((void**)&t->d_flag, t->h_flag, 0) == hipSuccess &&
+              hipMalloc((void**)&t->d_part, sizeof(double) * 4 * TAMOLS_BPL * 4) == hipSuccess &&
+              hipMalloc((void**)&t->d_cnt, sizeof(unsigned) * 8) == hipSuccess &&
+              hipMemset(t->d_cnt, 0, sizeof(unsigned) * 8) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+    if (!ok) {
         srbd_tamols_destroy(t);
         return fail(nullptr, SRBD_E_HIP, "TAMOLS context allocation failed");
     }
+    __atomic_store_n(t->h_flag, 0u, __ATOMIC_RELEASE);
     *out = t;
     return SRBD_OK;
 }
@@ -1396,11 +1411,12 @@ extern "C" void srbd_tamols_destroy(srbd_tamols_ctx* t) {
     if (!t) return;
     (void)hipSetDevice(t->device);
     if (t->stream) (void)hipStreamSynchronize(t->stream);
-    (void)hipFree(t->d_hm);
-    (void)hipFree(t->d_out);
-    (void)hipFree(t->d_nn);
+    (void)hipFree(t->d_part);
+    (void)hipFree(t->d_cnt);
+    (void)hipFree(t->d_dbg);
     if (t->h_out) (void)hipHostFree(t->h_out);
     if (t->h_hm) (void)hipHostFree(t->h_hm);
+    if (t->h_flag) (void)hipHostFree(t->h_flag);
     if (t->stream) (void)hipStreamDestroy(t->stream);
     delete t;
 }
@@ -1418,61 +1434,32 @@ extern "C" const char* srbd_tamols_last_error(const srbd_tamols_ctx* t) {
         }                                                                                           \
     } while (0)
 
-static int tamols_reserve(srbd_tamols_ctx* t, int nc);
-// The TAMOLS launch on a device heightmap buffer `d_hm` (4 x nc x 3) already ordered on t->stream.
-static int tamols_enqueue(srbd_tamols_ctx* t, const double* d_hm, int32_t rows, int32_t cols, const double* seeds,
-                          const double* hips, const double* vel, const double* base, const int32_t* contact,
-                          const double* feet, const srbd_tamols_params* p, double* out_fh, double* out_box,
-                          int32_t* out_valid, double* out_scores, double* out_seedh);
-
-extern "C" int srbd_tamols_run(srbd_tamols_ctx* t, const double* hm, int32_t rows, int32_t cols, const double* seeds,
-                               const double* hips, const double* vel, const double* base, const int32_t* contact,
-                               const double* feet, const srbd_tamols_params* p, double* out_fh, double* out_box,
-                               int32_t* out_valid, double* out_scores, double* out_seedh) {
-    if (!t || !hm || !seeds || !hips || !p || !out_fh || !out_box || !out_valid) return SRBD_E_INVALID;
-    const int nc = rows * cols;
-    if (rows < 1 || cols < 1 || nc > TAMOLS_MAXCAND) {
-        t->err = "patch must have 1..320 points";
-        return SRBD_E_INVALID;
-    }
-    TAM_TRY(t, hipSetDevice(t->device));
-    if (int rc = tamols_reserve(t, nc)) return rc;
-    memcpy(t->h_hm, hm, sizeof(double) * 12 * nc);
-    TAM_TRY(t, hipMemcpyAsync(t->d_hm, t->h_hm, sizeof(double) * 12 * nc, hipMemcpyHostToDevice, t->stream));
-    return tamols_enqueue(t, t->d_hm, rows, cols, seeds, hips, vel, base, contact, feet, p, out_fh, out_box,
-                          out_valid, out_scores, out_seedh);
-}
-
 static int tamols_reserve(srbd_tamols_ctx* t, int nc) {
     if (t->cap_cand < (size_t)nc) {
         TAM_TRY(t, hipStreamSynchronize(t->stream));
-        (void)hipFree(t->d_hm);
-        (void)hipFree(t->d_out);
-        (void)hipFree(t->d_nn);
         if (t->h_out) (void)hipHostFree(t->h_out);
         if (t->h_hm) (void)hipHostFree(t->h_hm);
-        t->d_hm = t->d_out = t->h_out = t->h_hm = t->d_nn = nullptr;
-        t->d_valid = nullptr;
+        t->h_out = t->h_hm = t->d_out_host = t->d_hm_host = nullptr;
         t->cap_cand = 0;
         const size_t out_doubles = 4 * (size_t)nc + 12 + 24 + 4 + 2;
-        TAM_TRY(t, hipMalloc((void**)&t->d_hm, sizeof(double) * 4 * 3 * nc));
-        TAM_TRY(t, hipMalloc((void**)&t->d_nn, sizeof(double) * 4 * ((size_t)nc * TAMOLS_NQ + 1)));
-        TAM_TRY(t, hipMalloc((void**)&t->d_out, sizeof(double) * out_doubles));
-        TAM_TRY(t, hipHostMalloc((void**)&t->h_out, sizeof(double) * out_doubles, hipHostMallocDefault));
-        TAM_TRY(t, hipHostMalloc((void**)&t->h_hm, sizeof(double) * 4 * 3 * nc, hipHostMallocDefault));
-        t->d_valid = reinterpret_cast<int*>(t->d_out + 4 * (size_t)nc + 40);
+        const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+        TAM_TRY(t, hipHostMalloc((void**)&t->h_out, sizeof(double) * out_doubles, fl));
+        TAM_TRY(t, hipHostGetDevicePointer((void**)&t->d_out_host, t->h_out, 0));
+        TAM_TRY(t, hipHostMalloc((void**)&t->h_hm, sizeof(double) * 4 * 3 * nc, fl));
+        TAM_TRY(t, hipHostGetDevicePointer((void**)&t->d_hm_host, t->h_hm, 0));
         t->cap_cand = nc;
     }
-    t->d_valid = reinterpret_cast<int*>(t->d_out + 4 * (size_t)nc + 40);  // this call's layout
     return SRBD_OK;
 }
 
-static int tamols_enqueue(srbd_tamols_ctx* t, const double* d_hm, int32_t rows, int32_t cols, const double* seeds,
-                          const double* hips, const double* vel, const double* base, const int32_t* contact,
-                          const double* feet, const srbd_tamols_params* p, double* out_fh, double* out_box,
-                          int32_t* out_valid, double* out_scores, double* out_seedh) {
+// Launch one call and wait for its published sequence number (bounded: the stream is polled now and
+// then, so a fault or a launch failure surfaces as an error instead of a hang).
+static int tamols_launch_wait(srbd_tamols_ctx* t, TamolsJob& j, const double* seeds, const double* hips,
+                              const double* vel, const double* base, const int32_t* contact, const double* feet,
+                              const srbd_tamols_params* p, int rows, int cols, double* out_fh, double* out_box,
+                              int32_t* out_valid, double* out_scores, double* out_seedh) {
     const int nc = rows * cols;
-    TamolsArgs a;
+    TamolsArgs& a = j.a;
     memset(&a, 0, sizeof(a));
     a.rows = rows;
     a.cols = cols;
@@ -1491,17 +1478,30 @@ static int tamols_enqueue(srbd_tamols_ctx* t, const double* d_hm, int32_t rows, 
         a.hips[i] = hips[i];
     }
     a.p = *p;
-    double* d_scores = t->d_out;
-    double* d_fh = d_scores + 4 * (size_t)nc;
-    double* d_box = d_fh + 12;
-    double* d_seedh = d_box + 24;
-    launch_tamols(a, d_hm, t->d_nn, d_scores, d_fh, d_box, t->d_valid, d_seedh, t->stream);
+    j.rows = rows;
+    j.cols = cols;
+    j.scores = out_scores ? t->d_out_host : nullptr;
+    j.out = t->d_out_host + 4 * (size_t)nc;
+    j.part = t->d_part;
+    j.cnt = t->d_cnt;
+    j.flag = t->d_flag;
+    j.seq = ++t->seq;
+    j.dbg = t->d_dbg;
+    launch_tamols_fused(j, t->stream);
     TAM_TRY(t, hipGetLastError());
-    // one D2H: the whole block when the scores are wanted, else its 42-double tail
-    const size_t first = out_scores ? 0 : 4 * (size_t)nc, total = 4 * (size_t)nc + 42;
-    TAM_TRY(t, hipMemcpyAsync(t->h_out + first, t->d_out + first, sizeof(double) * (total - first),
-                              hipMemcpyDeviceToHost, t->stream));
-    TAM_TRY(t, hipStreamSynchronize(t->stream));
+    for (uint64_t it = 1;; ++it) {
+        if (__atomic_load_n(t->h_flag, __ATOMIC_ACQUIRE) == j.seq) break;
+        if ((it & 4095) == 0) {
+            const hipError_t e = hipStreamQuery(t->stream);
+            if (e == hipSuccess) {
+                if (__atomic_load_n(t->h_flag, __ATOMIC_ACQUIRE) == j.seq) break;
+                t->err = "TAMOLS launch completed without publishing its outputs";
+                return SRBD_E_HIP;
+            }
+            if (e != hipErrorNotReady) TAM_TRY(t, e);
+        }
+        __builtin_ia32_pause();
+    }
     const double* h = t->h_out + 4 * (size_t)nc;
     memcpy(out_fh, h, sizeof(double) * 12);
     memcpy(out_box, h + 12, sizeof(double) * 24);
@@ -1511,7 +1511,28 @@ static int tamols_enqueue(srbd_tamols_ctx* t, const double* d_hm, int32_t rows, 
     return SRBD_OK;
 }
 
-// TAMOLS on patches raycast from a device terrain in the same stream (centres = the seeds).
+extern "C" int srbd_tamols_run(srbd_tamols_ctx* t, const double* hm, int32_t rows, int32_t cols, const double* seeds,
+                               const double* hips, const double* vel, const double* base, const int32_t* contact,
+                               const double* feet, const srbd_tamols_params* p, double* out_fh, double* out_box,
+                               int32_t* out_valid, double* out_scores, double* out_seedh) {
+    if (!t || !hm || !seeds || !hips || !p || !out_fh || !out_box || !out_valid) return SRBD_E_INVALID;
+    const int nc = rows * cols;
+    if (rows < 1 || cols < 1 || nc > TAMOLS_MAXCAND) {
+        t->err = "patch must have 1..320 points";
+        return SRBD_E_INVALID;
+    }
+    TAM_TRY(t, hipSetDevice(t->device));
+    if (int rc = tamols_reserve(t, nc)) return rc;
+    memcpy(t->h_hm, hm, sizeof(double) * 12 * nc);  // the previous call has completed (it was waited for)
+    TamolsJob j;
+    memset(&j, 0, sizeof(j));
+    j.use_terrain = 0;
+    j.hm = t->d_hm_host;
+    return tamols_launch_wait(t, j, seeds, hips, vel, base, contact, feet, p, rows, cols, out_fh, out_box, out_valid,
+                              out_scores, out_seedh);
+}
+
+// TAMOLS on patches raycast from a device terrain in the same launch (centres = the seeds).
 extern "C" int srbd_tamols_run_terrain(srbd_tamols_ctx* t, srbd_terrain* ter, double yaw, int32_t rows, int32_t cols,
                                        double dist_x, double dist_y, double ray_z, const double* seeds,
                                        const double* hips, const double* vel, const double* base,
@@ -1530,16 +1551,61 @@ extern "C" int srbd_tamols_run_terrain(srbd_tamols_ctx* t, srbd_terrain* ter, do
     }
     TAM_TRY(t, hipSetDevice(t->device));
     if (int rc = tamols_reserve(t, nc)) return rc;
-    const double yaws[4] = {yaw, yaw, yaw, yaw};
-    double* d_hm = nullptr;
-    if (terrain_enqueue(ter, seeds, yaws, 4, rows, cols, dist_x, dist_y, ray_z, t->stream, &d_hm)) {
-        t->err = ter->err;
-        return SRBD_E_HIP;
-    }
-    if (out_hm)
-        TAM_TRY(t, hipMemcpyAsync(t->h_hm, d_hm, sizeof(double) * 12 * nc, hipMemcpyDeviceToHost, t->stream));
-    const int rc = tamols_enqueue(t, d_hm, rows, cols, seeds, hips, vel, base, contact, feet, p, out_fh, out_box,
-                                  out_valid, out_scores, out_seedh);  // synchronises the stream
+    TamolsJob j;
+    memset(&j, 0, sizeof(j));
+    j.use_terrain = 1;
+    j.t = ter->dev;
+    j.yaw_c = cos(yaw);  // the same host cos / sin terrain_enqueue forms for a patch's yaw
+    j.yaw_s = sin(yaw);
+    j.dist_x = dist_x;
+    j.dist_y = dist_y;
+    j.ray_z = ray_z;
+    j.hm_out = out_hm ? t->d_hm_host : nullptr;
+    const int rc = tamols_launch_wait(t, j, seeds, hips, vel, base, contact, feet, p, rows, cols, out_fh, out_box,
+                                      out_valid, out_scores, out_seedh);
     if (!rc && out_hm) memcpy(out_hm, t->h_hm, sizeof(double) * 12 * nc);
     return rc;
+}
+
+// Diagnostic: stamp the phases of the following calls (enable != 0), or read the last call's stamps:
+// out_us[5] = the mean over blocks of (patch, queries, scores, count) durations and the span from the
+// first block's start to the last leg's end (us, 100 MHz s_memrealtime).
+extern "C" int srbd_tamols_phases(srbd_tamols_ctx* t, int32_t enable, float* out_us) {
+    if (!t) return SRBD_E_INVALID;
+    TAM_TRY(t, hipSetDevice(t->device));
+    const size_t n = 4 * TAMOLS_BPL * 8;
+    if (enable && !t->d_dbg) {
+        TAM_TRY(t, hipMalloc((void**)&t->d_dbg, sizeof(uint64_t) * n));
+        TAM_TRY(t, hipMemset(t->d_dbg, 0, sizeof(uint64_t) * n));
+    }
+    if (out_us && t->d_dbg) {
+        std::vector<uint64_t> h(n);
+        TAM_TRY(t, hipMemcpy(h.data(), t->d_dbg, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
+        double acc[4] = {0, 0, 0, 0};
+        uint64_t lo = ~0ull, hi = 0;
+        int nb = 0;
+        for (size_t blk = 0; blk < 4 * TAMOLS_BPL; ++blk) {
+            const uint64_t* s = h.data() + blk * 8;
+            if (!s[0]) continue;
+            ++nb;
+            for (int k = 0; k < 4; ++k) acc[k] += (double)(s[k + 1] - s[k]);
+            lo = std::min(lo, s[0]);
+            if (s[5]) hi = std::max(hi, s[5]);
+        }
+        for (int k = 0; k < 4; ++k) out_us[k] = nb ? (float)(acc[k] / nb * 0.01) : 0.0f;
+        out_us[4] = hi > lo ? (float)((double)(hi - lo) * 0.01) : 0.0f;
+    }
+    if (!enable && t->d_dbg) {
+        (void)hipFree(t->d_dbg);
+        t->d_dbg = nullptr;
+    }
+    return SRBD_OK;
+}
+
+// Diagnostic: the raw stamps of the last call (4 x TAMOLS_BPL x 8 uint64, 100 MHz ticks).
+extern "C" int srbd_tamols_phases_raw(srbd_tamols_ctx* t, uint64_t* out) {
+    if (!t || !out || !t->d_dbg) return SRBD_E_INVALID;
+    TAM_TRY(t, hipSetDevice(t->device));
+    TAM_TRY(t, hipMemcpy(out, t->d_dbg, sizeof(uint64_t) * 4 * TAMOLS_BPL * 8, hipMemcpyDeviceToHost));
+    return SRBD_OK;
 }

@@ -93,7 +93,7 @@ void launch_div_selftest(const float* a, const float* b, int n, float* o, hipStr
 
 // TAMOLS (tamols_kernel.hip)
 constexpr int TAMOLS_NQ = 19;        // nearest-neighbour queries per candidate
-constexpr int TAMOLS_MAXCAND = 320;  // rows * cols (LDS: 23 doubles per candidate)
+constexpr int TAMOLS_MAXCAND = 320;  // rows * cols
 
 struct TamolsArgs {
     int rows, cols, ncand;
@@ -148,9 +148,28 @@ namespace srbd {
 int terrain_enqueue(srbd_terrain* t, const double* centers, const double* yaws, int npatch, int rows, int cols,
                     double dist_x, double dist_y, double ray_z, hipStream_t s, double** d_out);
 
-size_t tamols_smem_bytes(int ncand);
-// nn: scratch of 4 x (ncand * TAMOLS_NQ + 1) doubles (the phase-A query heights)
-void launch_tamols(const TamolsArgs& a, const double* hm, double* nn, double* scores, double* footholds,
-                   double* boxes, int* valid, double* seedh, hipStream_t s);
+// One TAMOLS call as one launch (tamols_kernel.hip): TAMOLS_BPL blocks per leg, each raycasting (or
+// reading) the leg's patch and scoring its slice of the candidates; the leg's last block merges the
+// slices, the last leg publishes `seq` into `flag`.  Outputs are host-mapped pointers.
+constexpr int TAMOLS_BPL = 16;
+constexpr int TAMOLS_THREADS = 1024;
+constexpr int TAMOLS_LDS_PRIMS = 1024;  // scenes up to this many primitives are staged in LDS (80 KB)
+struct TamolsJob {
+    TamolsArgs a;
+    int use_terrain;     // 1: raycast the patches from `t` (centres = the seeds), 0: read `hm`
+    TerrainDev t;
+    double yaw_c, yaw_s, dist_x, dist_y, ray_z;
+    int rows, cols;
+    const double* hm;    // 4 x nc x 3 (device-visible) when !use_terrain
+    double* hm_out;      // 4 x nc x 3 raycast patches or NULL
+    double* scores;      // 4 x nc or NULL
+    double* out;         // fh 12 | boxes 24 | seed heights 4 | valid 4 x int32 (2 doubles)
+    double* part;        // 4 x TAMOLS_BPL x 4 partials (device)
+    unsigned* cnt;       // 4 per-leg block counters + 1 leg counter (device, zero between calls)
+    uint32_t* flag;      // host-mapped publish word
+    uint32_t seq;
+    uint64_t* dbg;       // diagnostic phase stamps (4 x TAMOLS_BPL x 8) or NULL
+};
+void launch_tamols_fused(const TamolsJob& j, hipStream_t s);
 
 }  // namespace srbd

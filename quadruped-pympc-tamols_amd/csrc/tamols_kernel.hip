@@ -2,15 +2,17 @@
 //
 // Restates VisualFootholdAdaptation.compute_adaptation, strategy 'tamols'
 // (quadruped_pympc/helpers/visual_foothold_adaptation.py:153-231, helpers :261-714).
-// Grid (TAMOLS_BPL blocks per leg, 4 legs), 256 threads.  Every block of a leg:
+// Grid (TAMOLS_BPL blocks per leg, 4 legs), TAMOLS_THREADS threads.  Every block of a leg:
 //   patch  : the leg's rows x cols heightmap into LDS -- raycast from the device terrain scene
-//            (terrain_ray.h, the heightmap sensor fused in) or read from the caller's patches;
+//            (terrain_ray.h, the heightmap sensor fused in; up to 8 lanes per ray, each walking a share
+//            of the scene staged in LDS) or read from the caller's patches;
 //   phase A: the nearest-neighbour height queries of ITS slice of the candidates (19 per candidate: the
 //            candidate, 5 leg-collision samples, 4 edge samples, 9 roughness samples; block 0 also the
-//            seed), one lane per query, brute force over the LDS patch (strict <: first nearest wins);
+//            seed), up to 4 lanes per query each scanning a part of the LDS patch (strict <: the first
+//            nearest point wins);
 //   phase B: one lane per candidate of the slice: hard constraints and soft costs -> score;
 //   phase C: strict-< argmin over the slice in candidate order -> (score, index, height) partial.
-// The last block of a leg to finish (agent-scope acq_rel counter) merges the leg's partials in block
+// The last block of a leg to finish (per-leg counter; partials stored write-through) merges them in block
 // order (strict <, so the first minimum over all candidates wins, VFA:185-190) and writes the leg's
 // foothold, box and validity; the last leg to finish publishes the call's sequence number to the host.
 // Outputs go straight to host-mapped memory; the host spins on the flag (no copy, no stream sync).
@@ -19,11 +21,11 @@
 
 namespace srbd {
 
-// Query t of a leg (0 <= t < nc * NQ: candidate t / NQ, sample t % NQ; t == nc * NQ: the seed) and its
-// nearest-neighbour height over the patch (strict <: the first nearest point wins), FastHeightMap.get_height
-// (VFA:31-35).
-__device__ __forceinline__ double tamols_query(const TamolsArgs& a, int leg, int t, const double* px, const double* py,
-                                               const double* pz) {
+// Query t of a leg (0 <= t < nc * NQ: candidate t / NQ, sample t % NQ; t == nc * NQ: the seed): its
+// point.  Its height is the nearest patch point's + 0.02 (strict <: the first nearest point wins),
+// FastHeightMap.get_height (VFA:31-35).
+__device__ __forceinline__ void tamols_query_point(const TamolsArgs& a, int leg, int t, const double* px,
+                                                   const double* py, double& qx_out, double& qy_out) {
     const int nc = a.ncand, nq = nc * TAMOLS_NQ + 1;
     const srbd_tamols_params& p = a.p;
     const double dl = p.gradient_delta;
@@ -53,8 +55,19 @@ __device__ __forceinline__ double tamols_query(const TamolsArgs& a, int leg, int
             qy = cy + (double)j * dl;
         }
     }
-    double bd = INFINITY, bh = 0.0;
-    for (int i = 0; i < nc; ++i) {
+    qx_out = qx;
+    qy_out = qy;
+}
+
+// The same query scanned over patch points [i0, i1) only: (squared distance, height) of its first nearest
+// point there (strict <), for splitting one query over several lanes.
+__device__ __forceinline__ void tamols_query_part(const TamolsArgs& a, int leg, int t, const double* px,
+                                                  const double* py, const double* pz, int i0, int i1, double& bd,
+                                                  double& bh) {
+    double qx, qy;
+    tamols_query_point(a, leg, t, px, py, qx, qy);
+#pragma unroll 4
+    for (int i = i0; i < i1; ++i) {
         const double dx = qx - px[i], dy = qy - py[i];
         const double d2 = dx * dx + dy * dy;
         if (d2 < bd) {
@@ -62,7 +75,6 @@ __device__ __forceinline__ double tamols_query(const TamolsArgs& a, int leg, int
             bh = pz[i];
         }
     }
-    return bh + 0.02;
 }
 
 // Score of candidate (cx, cy) with its query heights h[0..NQ) (VFA:192-222): INFINITY when a hard
@@ -165,45 +177,119 @@ __device__ __forceinline__ double tamols_score(const TamolsArgs& a, int leg, dou
 
 constexpr int TAMOLS_SLICE = (TAMOLS_MAXCAND + TAMOLS_BPL - 1) / TAMOLS_BPL;  // candidates per block, max
 
-__global__ void __launch_bounds__(256) tamols_fused_kernel(const TamolsJob j) {
+__global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const TamolsJob j) {
     __shared__ double px[TAMOLS_MAXCAND], py[TAMOLS_MAXCAND], pz[TAMOLS_MAXCAND];
     __shared__ double nn[TAMOLS_SLICE * TAMOLS_NQ + 1];
     __shared__ double sc[TAMOLS_SLICE];
+    __shared__ double rbest[TAMOLS_THREADS];
+    __shared__ int rhit[TAMOLS_THREADS];
     __shared__ int last;
+    extern __shared__ uint4 scene[];  // the terrain's primitives (+ box yaw cos / sin) when they fit
     const TamolsArgs& a = j.a;
     const int leg = blockIdx.y, b = blockIdx.x, NB = gridDim.x, tid = threadIdx.x, T = blockDim.x;
     const int nc = a.ncand;
+    // diagnostic stamps (srbd_tamols_phases): s_memrealtime (100 MHz) per block at the phase ends
+#define TAM_STAMP(k)                                                                                   \
+    if (j.dbg && tid == 0) {                                                                         \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                  \
+        j.dbg[((size_t)leg * NB + b) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                  \
+    }
+    TAM_STAMP(0);
 
     // ---- patch (raycast, or the caller's) -> LDS; block 0 also hands the raycast patch back
-    for (int i = tid; i < nc; i += T) {
-        double o[3];
-        if (j.use_terrain) {
-            terrain_ray_point(j.t, a.seeds[3 * leg], a.seeds[3 * leg + 1], j.yaw_c, j.yaw_s, j.rows, j.cols,
-                              i / j.cols, i % j.cols, j.dist_x, j.dist_y, j.ray_z, o);
-            if (b == 0 && j.hm_out) {
-                double* w = j.hm_out + 3 * ((size_t)leg * nc + i);
-                w[0] = o[0];
-                w[1] = o[1];
-                w[2] = o[2];
-            }
-        } else {
-            const double* hm = j.hm + 3 * ((size_t)leg * nc + i);
-            o[0] = hm[0];
-            o[1] = hm[1];
-            o[2] = hm[2];
+    if (j.use_terrain) {
+        const int np = j.t.nprims;
+        const bool staged = np > 0 && np <= TAMOLS_LDS_PRIMS;
+        const int w = np * (int)(sizeof(srbd_terrain_prim) / 16);
+        if (staged) {  // stage the scene: every ray re-reads every primitive
+            const uint4* src = reinterpret_cast<const uint4*>(j.t.prims);
+            const uint4* srcc = reinterpret_cast<const uint4*>(j.t.cs);
+            for (int i = tid; i < w + np; i += T) scene[i] = i < w ? src[i] : srcc[i - w];
+            __syncthreads();
+            TAM_STAMP(6);
         }
-        px[i] = o[0];
-        py[i] = o[1];
-        pz[i] = o[2];
+        // G lanes per ray, each walking a contiguous share of the primitives (the ray's result is a max).
+        // Lanes of one wave share the share (lane -> ray i = u mod ncp, share = u / ncp, ncp = nc rounded
+        // up to the wave): the primitive loads are LDS broadcasts and the box / cylinder branch is uniform.
+        const int ncp = (nc + 63) & ~63;
+        int G = 8;  // the most of 8, 4, 2 that fit the block, else 1 lane per ray in chunks
+        while (G > 1 && G * ncp > T) G >>= 1;
+        for (int u0 = 0; u0 < G * ncp; u0 += T) {
+            const int u = u0 + tid, part = u / ncp, i = u - part * ncp;
+            const bool on = part < G && i < nc;
+            double x, y, best = -INFINITY;
+            int hit = 0;
+            ray_xy(a.seeds[3 * leg], a.seeds[3 * leg + 1], j.yaw_c, j.yaw_s, j.rows, j.cols, i / j.cols, i % j.cols,
+                   j.dist_x, j.dist_y, x, y);
+            if (on) {
+                if (part == 0) ray_walk_fields(j.t, x, y, j.ray_z, best, hit);
+                // two call sites, so the staged walk reads through LDS-typed pointers (ds_read, not flat)
+                if (staged)
+                    ray_walk_prims(reinterpret_cast<const srbd_terrain_prim*>(scene),
+                                   reinterpret_cast<const double*>(scene + w), part * np / G, (part + 1) * np / G,
+                                   x, y, j.ray_z, best, hit);
+                else
+                    ray_walk_prims(j.t.prims, j.t.cs, part * np / G, (part + 1) * np / G, x, y, j.ray_z, best, hit);
+            }
+            rbest[tid] = best;
+            rhit[tid] = hit;
+            __syncthreads();
+            TAM_STAMP(7);
+            if (on && part == 0) {
+                for (int g = 1; g < G; ++g) ray_merge(rbest[tid + g * ncp], rhit[tid + g * ncp], best, hit);
+                const double z = hit ? best : j.t.miss_z;
+                px[i] = x;
+                py[i] = y;
+                pz[i] = z;
+                if (b == 0 && j.hm_out) {
+                    double* o = j.hm_out + 3 * ((size_t)leg * nc + i);
+                    o[0] = x;
+                    o[1] = y;
+                    o[2] = z;
+                }
+            }
+            __syncthreads();
+        }
+    } else {
+        for (int i = tid; i < nc; i += T) {
+            const double* hm = j.hm + 3 * ((size_t)leg * nc + i);
+            px[i] = hm[0];
+            py[i] = hm[1];
+            pz[i] = hm[2];
+        }
     }
     __syncthreads();
+    TAM_STAMP(1);
 
     // ---- phase A: this block's candidates [c0, c1), their queries (+ the seed on block 0)
     const int c0 = (int)((long)b * nc / NB), c1 = (int)((long)(b + 1) * nc / NB);
     const int nown = (c1 - c0) * TAMOLS_NQ, nloc = nown + (b == 0 ? 1 : 0);
-    for (int t = tid; t < nloc; t += T)
-        nn[t] = tamols_query(a, leg, t < nown ? c0 * TAMOLS_NQ + t : nc * TAMOLS_NQ, px, py, pz);
+    {
+        // Q lanes per query (aligned groups of Q consecutive lanes), each scanning a contiguous quarter of the
+        // patch; the groups' (d2, first index) minima combine lowest-part-first, so the first nearest point of
+        // the whole patch wins exactly as in one serial scan
+        int Q = 4;
+        while (Q > 1 && Q * nloc > T) Q >>= 1;
+        for (int u0 = 0; u0 < nloc * Q; u0 += T) {
+            const int u = u0 + tid, t = u / Q, part = u - t * Q;
+            const bool on = t < nloc;
+            double bd = INFINITY, bh = 0.0;
+            if (on)
+                tamols_query_part(a, leg, t < nown ? c0 * TAMOLS_NQ + t : nc * TAMOLS_NQ, px, py, pz, part * nc / Q,
+                                  (part + 1) * nc / Q, bd, bh);
+            for (int m = 1; m < Q; m <<= 1) {  // butterfly within the group; the lower part wins ties
+                const double od = __shfl_xor(bd, m, 64), oh = __shfl_xor(bh, m, 64);
+                const bool lower = (part & m) != 0;  // the partner holds the lower-index points
+                if (od < bd || (lower && od == bd)) {
+                    bd = od;
+                    bh = oh;
+                }
+            }
+            if (on && part == 0) nn[t] = bh + 0.02;
+        }
+    }
     __syncthreads();
+    TAM_STAMP(2);
 
     // ---- phase B
     for (int c = c0 + tid; c < c1; c += T) {
@@ -213,6 +299,7 @@ __global__ void __launch_bounds__(256) tamols_fused_kernel(const TamolsJob j) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's score / patch stores issued and done
     __syncthreads();
+    TAM_STAMP(3);
 
     // ---- phase C: the slice's strict-< argmin, then the leg's last block merges the slices in order
     if (tid == 0) {
@@ -223,18 +310,21 @@ __global__ void __launch_bounds__(256) tamols_fused_kernel(const TamolsJob j) {
                 bs = sc[c - c0];
                 bi = c;
             }
+        // partials as write-through (agent-scope) stores, drained before the count: the consumer reads them
+        // with agent-scope loads, so no L2 write-back / invalidate is needed (MI355X guide, valid forms)
         double* P = j.part + 4 * ((size_t)leg * NB + b);
-        P[0] = bs;
-        P[1] = (double)bi;
-        P[2] = bi >= 0 ? nn[(bi - c0) * TAMOLS_NQ] : 0.0;
-        P[3] = b == 0 ? nn[nloc - 1] : 0.0;  // the seed's height
-        __threadfence_system();               // partials (device) and scores / patch (host) before the count
-        const unsigned old = __hip_atomic_fetch_add(j.cnt + leg, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(P, bs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(P + 1, (double)bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(P + 2, bi >= 0 ? nn[(bi - c0) * TAMOLS_NQ] : 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(P + 3, b == 0 ? nn[nloc - 1] : 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // seed
+        if (j.scores || j.hm_out) __threadfence_system();  // this block's host-mapped scores / patch
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old = __hip_atomic_fetch_add(j.cnt + leg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last = old == (unsigned)(NB - 1);
     }
     __syncthreads();
+    TAM_STAMP(4);
     if (!last || tid != 0) return;
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);
     int bi = -1;
     double bs = INFINITY, bh = 0.0;
     for (int q = 0; q < NB; ++q) {
@@ -273,18 +363,21 @@ __global__ void __launch_bounds__(256) tamols_fused_kernel(const TamolsJob j) {
     }
     j.out[36 + leg] = seedh;
     __hip_atomic_store(j.cnt + leg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next call
-    __threadfence_system();
-    const unsigned done = __hip_atomic_fetch_add(j.cnt + 4, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (done == 3u) {  // the last leg: every leg's outputs are visible system-wide -> publish
+    __threadfence_system();  // this leg's host-mapped outputs
+    const unsigned done = __hip_atomic_fetch_add(j.cnt + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    TAM_STAMP(5);
+    if (done == 3u) {  // the last leg: every leg's outputs have reached the system -> publish
         __hip_atomic_store(j.cnt + 4, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __threadfence_system();
         __hip_atomic_store(j.flag, j.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+#undef TAM_STAMP
 }
 
 void launch_tamols_fused(const TamolsJob& j, hipStream_t s) {
     const int nb = j.a.ncand < TAMOLS_BPL ? j.a.ncand : TAMOLS_BPL;
-    hipLaunchKernelGGL(tamols_fused_kernel, dim3(nb, 4), dim3(256), 0, s, j);
+    const int np = j.use_terrain ? j.t.nprims : 0;
+    const size_t smem = (np > 0 && np <= TAMOLS_LDS_PRIMS) ? (sizeof(srbd_terrain_prim) + 2 * sizeof(double)) * np : 0;
+    hipLaunchKernelGGL(tamols_fused_kernel, dim3(nb, 4), dim3(TAMOLS_THREADS), smem, s, j);
 }
 
 }  // namespace srbd

@@ -100,8 +100,8 @@ SIGNATURES = {
     "srbd_tamols_create": (_I, [_I, C.POINTER(_P)]),
     "srbd_tamols_destroy": (None, [_P]),
     "srbd_tamols_last_error": (C.c_char_p, [_P]),
-    "srbd_tamols_run": (_I, [_P, _DP, _I, _I, _DP, _DP, _DP, _DP, _IP, _DP, C.POINTER(TamolsParams), _DP, _DP, _IP,
-                             _DP, _DP]),
+    # TAMOLS array pointers are plain addresses (TamolsSearch passes cached ints; ctypes pointers also work)
+    "srbd_tamols_run": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, C.POINTER(TamolsParams), _P, _P, _P, _P, _P]),
 }
 
 class SrbdPgg(C.Structure):
@@ -141,8 +141,10 @@ SIGNATURES.update({
     "srbd_terrain_destroy": (None, [_P]),
     "srbd_terrain_last_error": (C.c_char_p, [_P]),
     "srbd_terrain_patches": (_I, [_P, _DP, _DP, _I, _I, _I, _D, _D, _D, _DP]),
-    "srbd_tamols_run_terrain": (_I, [_P, _P, _D, _I, _I, _D, _D, _D, _DP, _DP, _DP, _DP, _IP, _DP,
-                                     C.POINTER(TamolsParams), _DP, _DP, _IP, _DP, _DP, _DP]),
+    "srbd_tamols_run_terrain": (_I, [_P, _P, _D, _I, _I, _D, _D, _D, _P, _P, _P, _P, _P, _P,
+                                     C.POINTER(TamolsParams), _P, _P, _P, _P, _P, _P]),
+    "srbd_tamols_phases": (_I, [_P, _I, _FP]),
+    "srbd_tamols_phases_raw": (_I, [_P, _P]),
 })
 
 LIB_NAME = "libsrbd_hip.so"

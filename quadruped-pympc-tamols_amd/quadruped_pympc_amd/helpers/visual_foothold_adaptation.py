@@ -54,7 +54,11 @@ def tamols_params_struct(tamols_params: dict, robot_name: str) -> "_lib.TamolsPa
 
 
 class TamolsSearch:
-    """Owns one ``srbd_tamols_ctx``; ``run`` evaluates all four legs in one kernel launch."""
+    """Owns one ``srbd_tamols_ctx``; ``run`` / ``run_terrain`` evaluate all four legs in one kernel launch.
+
+    Inputs are copied into persistent staging arrays whose addresses are cached, and the outputs come
+    back in persistent arrays (copied into the returned dict): a call costs a few slice copies plus the C
+    call (``ndarray.ctypes`` conversions cost ~2.5 us each, more than the kernel itself)."""
 
     def __init__(self, device_id: int = 0):
         h = C.c_void_p()
@@ -62,6 +66,24 @@ class TamolsSearch:
         if rc != _lib.OK:
             raise RuntimeError(f"srbd_tamols_create failed ({rc}): {_lib.last_error(None)}")
         self.h = h
+        self._shape = None
+        self._inp = np.zeros(42)  # seeds 0:12 | hips 12:24 | vel 24:27 | base 27:30 | feet 30:42
+        self._contact = np.zeros(4, dtype=np.int32)
+        self._res = np.zeros(40)  # footholds 0:12 | boxes 12:36 | seed heights 36:40
+        self._valid = np.zeros(4, dtype=np.int32)
+        a = self._inp.ctypes.data
+        self._a_seeds, self._a_hips, self._a_vel, self._a_base, self._a_feet = a, a + 96, a + 192, a + 216, a + 240
+        self._a_contact = self._contact.ctypes.data
+        r = self._res.ctypes.data
+        self._a_fh, self._a_box, self._a_seedh = r, r + 96, r + 288
+        self._a_valid = self._valid.ctypes.data
+
+    def _shape_bufs(self, rows, cols):
+        if self._shape != (rows, cols):
+            self._shape = (rows, cols)
+            self._scores = np.zeros(4 * rows * cols)
+            self._hm = np.zeros((4, rows, cols, 3))
+            self._a_scores, self._a_hm = self._scores.ctypes.data, self._hm.ctypes.data
 
     def close(self):
         if getattr(self, "h", None):
@@ -74,58 +96,75 @@ class TamolsSearch:
         except Exception:
             pass
 
+    def _stage(self, seeds, hips, forward_vel, base_position, current_contact, current_feet_pos):
+        inp = self._inp
+        inp[0:12] = np.reshape(seeds, 12)
+        inp[12:24] = np.reshape(hips, 12)
+        a_vel = a_base = a_contact = a_feet = None
+        if forward_vel is not None:
+            inp[24:27] = np.asarray(forward_vel, dtype=np.float64).reshape(-1)[:3]
+            a_vel = self._a_vel
+        if base_position is not None:
+            inp[27:30] = np.asarray(base_position, dtype=np.float64).reshape(-1)[:3]
+            a_base = self._a_base
+        if current_contact is not None:
+            self._contact[:] = np.reshape(current_contact, 4)
+            a_contact = self._a_contact
+        if current_feet_pos is not None:
+            inp[30:42] = np.reshape(current_feet_pos, 12)
+            a_feet = self._a_feet
+        return a_vel, a_base, a_contact, a_feet
+
+    def _result(self, rows, cols, with_hm, with_scores=True):
+        r = self._res
+        out = dict(footholds=r[0:12].reshape(4, 3).copy(), boxes=r[12:36].reshape(4, 2, 3).copy(),
+                   valid=self._valid.astype(bool), seed_heights=r[36:40].copy())
+        if with_scores:
+            out["scores"] = self._scores.reshape(4, rows * cols).copy()
+        if with_hm:
+            out["heightmaps"] = self._hm.copy()
+        return out
+
+    def _raise(self, name, rc):
+        msg = _lib.lib.srbd_tamols_last_error(self.h)
+        raise RuntimeError(f"{name} failed ({rc}): {msg.decode() if msg else ''}")
+
     def run(self, heightmaps, seeds, hips, params, forward_vel=None, base_position=None, current_contact=None,
-            current_feet_pos=None):
+            current_feet_pos=None, want_scores=True):
         """heightmaps (4, rows, cols, 3) or (4, rows, cols, 1, 3); seeds/hips (4, 3).
 
-        Returns dict(footholds (4,3), boxes (4,2,3), valid (4,) bool, scores (4, rows*cols), seed_heights (4,))."""
+        Returns dict(footholds (4,3), boxes (4,2,3), valid (4,) bool, scores (4, rows*cols) (when
+        want_scores), seed_heights (4,))."""
         hm = np.asarray(heightmaps, dtype=np.float64)
         rows, cols = hm.shape[1], hm.shape[2]
-        hm = np.ascontiguousarray(hm.reshape(4, rows * cols, 3))
-        seeds = np.ascontiguousarray(seeds, dtype=np.float64).reshape(12)
-        hips = np.ascontiguousarray(hips, dtype=np.float64).reshape(12)
-        vel = None if forward_vel is None else np.ascontiguousarray(np.asarray(forward_vel, np.float64)[:3])
-        base = None if base_position is None else np.ascontiguousarray(np.asarray(base_position, np.float64)[:3])
-        contact = None if current_contact is None else np.ascontiguousarray(current_contact, dtype=np.int32)
-        feet = None if current_feet_pos is None else np.ascontiguousarray(current_feet_pos, dtype=np.float64).reshape(12)
-        fh = np.zeros(12)
-        boxes = np.zeros(24)
-        valid = np.zeros(4, dtype=np.int32)
-        scores = np.zeros(4 * rows * cols)
-        seedh = np.zeros(4)
-        rc = _lib.lib.srbd_tamols_run(self.h, _lib.dptr(hm), rows, cols, _lib.dptr(seeds), _lib.dptr(hips),
-                                      _lib.dptr(vel), _lib.dptr(base), _lib.iptr(contact), _lib.dptr(feet),
-                                      C.byref(params), _lib.dptr(fh), _lib.dptr(boxes), _lib.iptr(valid),
-                                      _lib.dptr(scores), _lib.dptr(seedh))
+        self._shape_bufs(rows, cols)
+        self._hm[...] = hm.reshape(4, rows, cols, 3)
+        a_vel, a_base, a_contact, a_feet = self._stage(seeds, hips, forward_vel, base_position, current_contact,
+                                                       current_feet_pos)
+        rc = _lib.lib.srbd_tamols_run(self.h, self._a_hm, rows, cols, self._a_seeds, self._a_hips, a_vel, a_base,
+                                      a_contact, a_feet, C.byref(params), self._a_fh, self._a_box, self._a_valid,
+                                      self._a_scores if want_scores else None, self._a_seedh)
         if rc != _lib.OK:
-            msg = _lib.lib.srbd_tamols_last_error(self.h)
-            raise RuntimeError(f"srbd_tamols_run failed ({rc}): {msg.decode() if msg else ''}")
-        return dict(footholds=fh.reshape(4, 3), boxes=boxes.reshape(4, 2, 3), valid=valid.astype(bool),
-                    scores=scores.reshape(4, rows * cols), seed_heights=seedh)
-
+            self._raise("srbd_tamols_run", rc)
+        return self._result(rows, cols, False, want_scores)
 
     def run_terrain(self, terrain, yaw, seeds, hips, params, rows=13, cols=7, dist_x=0.04, dist_y=0.04, ray_z=10.0,
-                    forward_vel=None, base_position=None, current_contact=None, current_feet_pos=None):
-        """``run`` on patches raycast from a ``GpuTerrain`` around the seeds, in the same stream as the search
-        (``srbd_tamols_run_terrain``).  The result also holds the patches (``heightmaps``, (4, rows, cols, 3))."""
-        seeds = np.ascontiguousarray(seeds, dtype=np.float64).reshape(12)
-        hips = np.ascontiguousarray(hips, dtype=np.float64).reshape(12)
-        vel = None if forward_vel is None else np.ascontiguousarray(np.asarray(forward_vel, np.float64)[:3])
-        base = None if base_position is None else np.ascontiguousarray(np.asarray(base_position, np.float64)[:3])
-        contact = None if current_contact is None else np.ascontiguousarray(current_contact, dtype=np.int32)
-        feet = None if current_feet_pos is None else np.ascontiguousarray(current_feet_pos, dtype=np.float64).reshape(12)
-        fh, boxes, valid = np.zeros(12), np.zeros(24), np.zeros(4, dtype=np.int32)
-        scores, seedh, hm = np.zeros(4 * rows * cols), np.zeros(4), np.zeros((4, rows, cols, 3))
+                    forward_vel=None, base_position=None, current_contact=None, current_feet_pos=None,
+                    want_scores=True, want_heightmaps=True):
+        """``run`` on patches raycast from a ``GpuTerrain`` around the seeds, in the same launch as the search
+        (``srbd_tamols_run_terrain``).  The result also holds the patches (``heightmaps``, (4, rows, cols, 3))
+        when want_heightmaps; without scores and patches nothing but the footholds crosses PCIe."""
+        self._shape_bufs(rows, cols)
+        a_vel, a_base, a_contact, a_feet = self._stage(seeds, hips, forward_vel, base_position, current_contact,
+                                                       current_feet_pos)
         rc = _lib.lib.srbd_tamols_run_terrain(self.h, terrain.h, float(yaw), rows, cols, float(dist_x), float(dist_y),
-                                              float(ray_z), _lib.dptr(seeds), _lib.dptr(hips), _lib.dptr(vel),
-                                              _lib.dptr(base), _lib.iptr(contact), _lib.dptr(feet), C.byref(params),
-                                              _lib.dptr(fh), _lib.dptr(boxes), _lib.iptr(valid), _lib.dptr(scores),
-                                              _lib.dptr(seedh), _lib.dptr(hm))
+                                              float(ray_z), self._a_seeds, self._a_hips, a_vel, a_base, a_contact,
+                                              a_feet, C.byref(params), self._a_fh, self._a_box, self._a_valid,
+                                              self._a_scores if want_scores else None, self._a_seedh,
+                                              self._a_hm if want_heightmaps else None)
         if rc != _lib.OK:
-            msg = _lib.lib.srbd_tamols_last_error(self.h)
-            raise RuntimeError(f"srbd_tamols_run_terrain failed ({rc}): {msg.decode() if msg else ''}")
-        return dict(footholds=fh.reshape(4, 3), boxes=boxes.reshape(4, 2, 3), valid=valid.astype(bool),
-                    scores=scores.reshape(4, rows * cols), seed_heights=seedh, heightmaps=hm)
+            self._raise("srbd_tamols_run_terrain", rc)
+        return self._result(rows, cols, want_heightmaps, want_scores)
 
 
 class VisualFootholdAdaptation:
