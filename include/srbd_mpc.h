@@ -169,6 +169,18 @@ int srbd_finish_host(const srbd_config* cfg, const float* records, int32_t num_r
 int srbd_make_record_host(const srbd_config* cfg, int32_t rank, int32_t world_size, const float* costs,
                           const float* noise_rows, float* record);
 
+/*
+ * Checkpoint / restore (exact golden replays of device-resident chains).  The state is what the next
+ * device-resident step starts from: the warm start best_params (P floats), sigma (P floats, CEM
+ * only; may be NULL otherwise) and the device RNG key (seed, counter).  After a host srbd_step it is
+ * that step's inputs; every device-resident step (srbd_bench_device_steps, srbd_sharded_device_steps,
+ * srbd_device_step_local/finish) advances it on the device.  Host steps are stateless here: their
+ * state is their arguments (Sampling_MPC.get_state in the Python mirror).  Both calls block until the
+ * context stream is idle and need one srbd_step first (it sets the state / reference inputs).
+ */
+int srbd_get_state(srbd_ctx* ctx, float* best_params, float* sigma, uint64_t* seed, uint64_t* counter);
+int srbd_set_state(srbd_ctx* ctx, const float* best_params, const float* sigma, uint64_t seed, uint64_t counter);
+
 /* Measurement: replay `steps` device-resident steps (RNG -> rollout -> reduction -> warm start
  * written back on device) back to back; returns elapsed ms (hipEvents on the context stream). */
 int srbd_bench_device_steps(srbd_ctx* ctx, int32_t steps, float* elapsed_ms);
@@ -223,7 +235,9 @@ int srbd_xgmi_connect_local(srbd_ctx* const* ctxs, int32_t world);
 int srbd_xgmi_probe(srbd_ctx* ctx, int32_t* ok);
 int srbd_xgmi_disconnect(srbd_ctx* ctx);
 
-/* Diagnostic: mean duration (us) of the merge kernel's 5 phases (s_memrealtime stamps). */
+/* Diagnostic: mean duration (us) of the merge kernel's 5 phases (s_memrealtime stamps), then (staged merge)
+ * the times from its start at which the records were in LDS and the tail prep was done, then the
+ * shader clock in MHz over the kernel, then 16 finer marks (us from the start; 0 = unset): 24 floats. */
 int srbd_debug_merge_phases(srbd_ctx* ctx, int32_t iters, float* out_us);
 
 /* Self-test of the correctly rounded division used in the rollout (a/b; b == 3 uses the constant

@@ -318,6 +318,7 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     if ((e = hipSetDevice(cfg->device_id)) != hipSuccess) return cleanup_fail("hipSetDevice", e);
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return cleanup_fail("hipStreamCreate", e);
+    merge_prepare();
     if ((e = hipHostMalloc((void**)&c->h_in, sizeof(StepInput), hipHostMallocMapped)) != hipSuccess)
         return cleanup_fail("hipHostMalloc", e);
     if ((e = hipHostGetDevicePointer((void**)&c->d_in_host, c->h_in, 0)) != hipSuccess)
@@ -1208,6 +1209,47 @@ extern "C" int srbd_sharded_device_steps(srbd_ctx* c, int32_t steps, float* elap
     return rc;
 }
 
+// ------------------------------------------------------------------ checkpoint
+// The evolving state of a context is what its device-resident steps start from: the device copy of
+// the warm start (best[P]), sigma[P] (CEM) and the RNG key (seed, counter) in StepInput.  Host steps
+// take all of it as arguments (the Python Sampling_MPC keeps it: best_control_parameters,
+// sigma_cem_mppi, master_key), so a checkpoint of a host-driven controller is those arguments; this
+// pair covers the device-resident chains (srbd_bench_device_steps, srbd_sharded_device_steps,
+// srbd_device_step_local), whose warm start never leaves the device.
+extern "C" int srbd_get_state(srbd_ctx* c, float* best, float* sigma, uint64_t* seed, uint64_t* counter) {
+    if (!c || !best) return SRBD_E_INVALID;
+    if (!c->input_ready) return fail(c, SRBD_E_STATE, "no state yet: run srbd_step (or srbd_set_state) first");
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    StepInput* h = c->h_in;  // staging: overwritten by the next host step anyway
+    HIP_TRY(c, hipMemcpy(h, c->d_in, sizeof(StepInput), hipMemcpyDeviceToHost));
+    memcpy(best, h->best, sizeof(float) * c->mc.P);
+    if (sigma && c->mc.method == SRBD_CEM_MPPI) memcpy(sigma, h->sigma, sizeof(float) * c->mc.P);
+    if (seed) *seed = ((uint64_t)h->seed_hi << 32) | h->seed_lo;
+    if (counter) *counter = ((uint64_t)h->ctr_hi << 32) | h->ctr_lo;
+    return SRBD_OK;
+}
+
+extern "C" int srbd_set_state(srbd_ctx* c, const float* best, const float* sigma, uint64_t seed, uint64_t counter) {
+    if (!c || !best) return SRBD_E_INVALID;
+    if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step once first (it sets the state/reference inputs)");
+    if (c->mc.method == SRBD_CEM_MPPI && !sigma) return fail(c, SRBD_E_INVALID, "CEM: sigma is part of the state");
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    StepInput* h = c->h_in;
+    HIP_TRY(c, hipMemcpy(h, c->d_in, sizeof(StepInput), hipMemcpyDeviceToHost));
+    memcpy(h->best, best, sizeof(float) * c->mc.P);
+    if (c->mc.method == SRBD_CEM_MPPI) memcpy(h->sigma, sigma, sizeof(float) * c->mc.P);
+    h->seed_lo = (uint32_t)seed;
+    h->seed_hi = (uint32_t)(seed >> 32);
+    h->ctr_lo = (uint32_t)counter;
+    h->ctr_hi = (uint32_t)(counter >> 32);
+    h->noise_scaled = 0;  // device-resident steps draw on the device
+    HIP_TRY(c, hipMemcpy(c->d_in, h, sizeof(StepInput), hipMemcpyHostToDevice));
+    c->pref_valid = false;  // no prefetched draws belong to the restored key
+    return SRBD_OK;
+}
+
 // ------------------------------------------------------------------ measurement
 // Device-resident chain (benchmark): two steps per graph, each step's rollout launch also drawing
 // the next step's noise into the other buffer (device counter + 1), each merge writing the warm
@@ -1323,18 +1365,24 @@ extern "C" int srbd_debug_merge_phases(srbd_ctx* c, int32_t iters, float* out_us
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step once first");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     uint64_t* d = nullptr;
-    HIP_TRY(c, hipMalloc((void**)&d, 8 * sizeof(uint64_t)));
-    double acc[5] = {0, 0, 0, 0, 0};
+    HIP_TRY(c, hipMalloc((void**)&d, 32 * sizeof(uint64_t)));
+    HIP_TRY(c, hipMemsetAsync(d, 0, 32 * sizeof(uint64_t), c->stream));
+    double acc[24] = {};
     for (int i = 0; i < iters; ++i) {
         launch_merge(c->mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, 0, c->d_noise[c->cur], nullptr,
                      c->d_out, 0, c->stream, d);
-        uint64_t h[8];
+        uint64_t h[32];
         HIP_TRY(c, hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         for (int k = 0; k < 5; ++k) acc[k] += (double)(h[k + 1] - h[k]) * 0.01;  // 100 MHz ticks -> us
+        // staged merge: records in LDS, tail lanes' force-independent step done (from the start)
+        for (int k = 5; k < 7; ++k) acc[k] += h[k + 1] > h[0] ? (double)(h[k + 1] - h[0]) * 0.01 : 0.0;
+        // shader clock (MHz): s_memtime ticks over the same span as the 100 MHz s_memrealtime stamps
+        acc[7] += h[5] > h[0] ? (double)(h[9] - h[8]) / ((double)(h[5] - h[0]) * 0.01) : 0.0;
+        for (int k = 0; k < 16; ++k) acc[8 + k] += h[16 + k] > h[0] ? (double)(h[16 + k] - h[0]) * 0.01 : 0.0;
     }
     (void)hipFree(d);
-    for (int k = 0; k < 5; ++k) out_us[k] = (float)(acc[k] / iters);
+    for (int k = 0; k < 24; ++k) out_us[k] = (float)(acc[k] / iters);
     return SRBD_OK;
 }
 

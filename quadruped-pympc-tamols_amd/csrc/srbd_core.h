@@ -94,8 +94,11 @@ struct StepOutput {
     float best_freq;  // gait-adaptive: step frequency of the best row
 };
 
-SRBD_HD int rec_floats_wave(int P, int K) { return REC_HDR + P + 2 * K; }
-SRBD_HD int rec_floats_rank(int P, int K) { return REC_HDR + P + 2 * K + K * P; }
+// Record strides are padded to whole 16-byte words, so a merge block can stage a run of records into
+// LDS with dwordx4 loads (merge_body<true>); the padding floats are never read as values.
+SRBD_HD int rec_pad4(int n) { return (n + 3) & ~3; }
+SRBD_HD int rec_floats_wave(int P, int K) { return rec_pad4(REC_HDR + P + 2 * K); }
+SRBD_HD int rec_floats_rank(int P, int K) { return rec_pad4(REC_HDR + P + 2 * K + K * P); }
 SRBD_HD int num_elite(int method, int num_elite_cfg) { return method == SRBD_CEM_MPPI ? num_elite_cfg : 1; }
 
 SRBD_HD uint32_t f2u(float f) {

@@ -548,10 +548,14 @@ __device__ __forceinline__ QuadLane quad_lane(const ModelConst& mc, int c) {
 // `temp` = sum_i f_i c_i and torque sum `temp2` = sum_i (p_i - p_com) x f_i c_i.  The float ops and
 // their order are those of integrate() in srbd_core.h (rollout_kernel), so both layouts agree bit
 // for bit.  All four lanes of each quad must be active (DPP quad permutations).
-__device__ __forceinline__ void quad_rigid_body(const ModelConst& mc, const QuadLane& L, float temp, float temp2,
-                                                float dt, float& p, float& v, float& r, float& w) {
+// Split in two so the merge tail can form the state-only part (rotation, Euler rates, gyroscopic
+// term) while the weighted sums are still being reduced: quad_rb_prep needs only r and w,
+// quad_rb_apply adds the forces.  quad_rigid_body = apply(prep); the float ops are unchanged.
+struct QuadRB {
+    float er, R0, R1, R2, a1;
+};
+__device__ __forceinline__ QuadRB quad_rb_prep(const QuadLane& L, float r, float w) {
     const int c = L.c;
-    const float lin = mc.inv_m * temp + L.g;
     float sn, cs;
     sincosf(r, &sn, &cs);
     const float sr = qp<QP_B0>(sn), cr = qp<QP_B0>(cs);
@@ -575,17 +579,26 @@ __device__ __forceinline__ void quad_rigid_body(const ModelConst& mc, const Quad
     const float R0 = c == 0 ? r0a : r0b;
     const float R1 = c == 0 ? r1a : r1b;
     const float R2 = c == 0 ? -sp : r2b;
-    const float Rt = R0 * qp<QP_B0>(temp2) + R1 * qp<QP_B1>(temp2) + R2 * qp<QP_B2>(temp2);
     const float Iw = L.Ir0 * w0 + L.Ir1 * w1 + L.Ir2 * w2;
     const float wx = (-qp<QP_NEXT2>(w)) * qp<QP_NEXT>(Iw) + qp<QP_NEXT>(w) * qp<QP_NEXT2>(Iw);
     const float a1 = L.Ii0 * qp<QP_B0>(wx) + L.Ii1 * qp<QP_B1>(wx) + L.Ii2 * qp<QP_B2>(wx);
+    return QuadRB{er, R0, R1, R2, a1};
+}
+__device__ __forceinline__ void quad_rb_apply(const ModelConst& mc, const QuadLane& L, const QuadRB& q, float temp,
+                                              float temp2, float dt, float& p, float& v, float& r, float& w) {
+    const float lin = mc.inv_m * temp + L.g;
+    const float Rt = q.R0 * qp<QP_B0>(temp2) + q.R1 * qp<QP_B1>(temp2) + q.R2 * qp<QP_B2>(temp2);
     const float a2 = L.Ii0 * qp<QP_B0>(Rt) + L.Ii1 * qp<QP_B1>(Rt) + L.Ii2 * qp<QP_B2>(Rt);
-    const float aa = -a1 + a2;
-    const float pn = p + v * dt, vn = v + lin * dt, rn = r + er * dt, wn = w + aa * dt;
+    const float aa = -q.a1 + a2;
+    const float pn = p + v * dt, vn = v + lin * dt, rn = r + q.er * dt, wn = w + aa * dt;
     p = pn;
     v = vn;
     r = rn;
     w = wn;
+}
+__device__ __forceinline__ void quad_rigid_body(const ModelConst& mc, const QuadLane& L, float temp, float temp2,
+                                                float dt, float& p, float& v, float& r, float& w) {
+    quad_rb_apply(mc, L, quad_rb_prep(L, r, w), temp, temp2, dt, p, v, r, w);
 }
 
 // This lane's component of (p_i - p_com) x f_i (jnp.dot(skew(v), f), CMJ:100-101, zero terms dropped).
@@ -889,6 +902,12 @@ constexpr int MERGE_THREADS = 1024;
 constexpr int MERGE_WAVES = MERGE_THREADS / 64;
 constexpr int MERGE_PREF = 24;  // record values of the weighted sums loaded per thread before beta is known
 constexpr int MERGE_RPT = 8;    // record headers per thread (nrec <= MERGE_RPT * MERGE_THREADS)
+// The LDS-staged merge runs two waves per SIMD: its phases are short dependent chains that every
+// wave repeats (index math, the beta reduction), so 16 waves pay ~2x the issue of 8, while fewer
+// waves stage the records more slowly (C2 merge 9.0 / 8.4 / 9.8 us at 1024 / 512 / 256 threads).
+#ifndef MERGE_STAGE_THREADS
+#define MERGE_STAGE_THREADS 512
+#endif
 constexpr uint64_t KEY_NONE = ~0ull;
 
 // Sorted (ascending) per-lane candidate list of at most KM keys; fully unrolled (registers only).
@@ -914,7 +933,7 @@ __device__ __forceinline__ void wave_topk(uint64_t (&lk)[KM], int K, uint64_t* o
 // Block-wide K smallest record keys (ascending) into `elite`, K <= KM: every thread's list starts as
 // its first record's keys (a record's keys ascend already), later records insert; per-wave K-round
 // minima; then one wave over the MERGE_WAVES wave lists.  Caller syncs afterwards.
-template <int KM>
+template <int KM, int NW = MERGE_WAVES>
 __device__ __forceinline__ void block_topk(const float* __restrict__ recs, int nrec, int rec_stride, int P, int K,
                                            uint64_t (*wlist)[MAXK], uint64_t* elite) {
     const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wv = tid >> 6;
@@ -939,7 +958,7 @@ __device__ __forceinline__ void block_topk(const float* __restrict__ recs, int n
     __syncthreads();
     if (wv == 0) {
 #pragma unroll
-        for (int i = 0; i < KM; ++i) lk[i] = (lane < MERGE_WAVES && i < K) ? wlist[lane][i] : KEY_NONE;
+        for (int i = 0; i < KM; ++i) lk[i] = (lane < NW && i < K) ? wlist[lane][i] : KEY_NONE;
         wave_topk(lk, K, elite);
     }
 }
@@ -959,32 +978,63 @@ __device__ __forceinline__ void block_topk(const float* __restrict__ recs, int n
 // the GRFs, the predicted state and the step scalars; block b >= 1 the columns [(b-1)cs, b cs) -- it
 // writes the other parameters and sigma.  Each block publishes flag[blockIdx.x] = seq.  This spreads
 // the record reads over CUs and drops the single block's serial column loop (C2: 8.8 -> see DESIGN).
+// STAGE: the block first copies its records into LDS with 16-byte loads (one memory round trip,
+// a quarter of the load instructions of dword column reads; the whole per-block record array at C2 is
+// 157 x 152 floats = 95 KB) and every later phase reads them from LDS.
+// Host-published outputs (flag != NULL) are stored system-scope (write-through to the mapped host
+// buffer); after every wave's vmcnt(0) and a barrier the flag store follows them, so the system-wide
+// L2 write-back of __threadfence_system is not needed for them (fence_sys = 1 keeps it).
+template <int NT, bool STAGE>
 __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __restrict__ in,
                                            const float* __restrict__ recs, int nrec, int rec_stride, int rows_in_rec,
                                            const float* __restrict__ noise, float* __restrict__ rank_out,
                                            StepOutput* __restrict__ out, int chain, int ctr_inc,
                                            uint64_t* __restrict__ dbg, uint32_t* __restrict__ flag, uint32_t seq,
-                                           int split_cs = 0) {
-    extern __shared__ float smem[];  // scale[nrec_pad] | part[G*(ncol+1)] | erow[K*ncol]
-    __shared__ uint64_t red[MERGE_WAVES];
-    __shared__ uint64_t wlist[MERGE_WAVES][MAXK];
+                                           int split_cs = 0, int fence_sys = 1) {
+    extern __shared__ float smem[];  // [STAGE: records] | scale[nrec_pad] | part[G*(ncol+1)] | erow[K*ncol]
+    constexpr int NW = NT / 64;
+    __shared__ uint64_t red[NW];
+    __shared__ uint64_t wlist[NW][MAXK];
     __shared__ uint64_t elite[MAXK];
     __shared__ int elite_src[MAXK];
     __shared__ float Vs[MAXP + 1];
     __shared__ float nb[MAXP];
-    __shared__ float grf_sh[12];
     __shared__ float tag_sh;  // header tag (gait-adaptive step frequency) of the record holding beta's row
+    // tail lanes: StepInput fields (13), the force-independent step (5), the ModelConst values the tail
+    // uses (16) -- read back in one batch (kernarg fields re-read lazily are serial scalar loads)
+    __shared__ float tail_sh[4][40];
 #define MERGE_STAMP(i) \
     if (dbg && threadIdx.x == 0 && blockIdx.x == 0) dbg[i] = __builtin_amdgcn_s_memrealtime()
+    // finer marks (diagnostic build of the phases call only: dbg[16 + i])
+#define MERGE_MARK(i) MERGE_STAMP(16 + (i))
     MERGE_STAMP(0);
+    if (dbg && threadIdx.x == 0 && blockIdx.x == 0) dbg[8] = __builtin_amdgcn_s_memtime();  // shader clock
 
-    const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wv = tid >> 6;
+    // T: the launch's block size, a template constant (blockDim.x is a dependent load)
+    const int tid = threadIdx.x, T = NT, lane = tid & 63, wv = tid >> 6;
     const int P = mc.P, K = mc.K;
     const bool rs = mc.method == SRBD_RANDOM_SAMPLING, cem = mc.method == SRBD_CEM_MPPI;
     const bool split = split_cs > 0;
     const bool tailblk = split && blockIdx.x == 0;
+    const bool sysout = flag != nullptr;  // outputs read by the host after the flag
+    // Unsplit: the step outputs are assembled in LDS and written out in one burst at the end, so no
+    // wave waits for a host store's completion mid-merge (a wave overwriting a register of a pending
+    // store waits vmcnt(0), ~1 us for a PCIe write) and the publish waits for one round of them.
+    __shared__ float osh[sizeof(StepOutput) / sizeof(float)];
+    const bool shadow = !split;
+    auto ostore = [&](void* dst, float v) {
+        if (shadow)
+            osh[reinterpret_cast<float*>(dst) - reinterpret_cast<float*>(out)] = v;
+        else if (sysout)
+            __hip_atomic_store(reinterpret_cast<uint32_t*>(dst), __float_as_uint(v), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        else
+            *reinterpret_cast<float*>(dst) = v;
+    };
     if (!split && gridDim.x > 1) {  // first level of a two-level merge: block b reduces its slice into rank_out[b]
-        const int b0 = (int)((long)blockIdx.x * nrec / gridDim.x), b1 = (int)((long)(blockIdx.x + 1) * nrec / gridDim.x);
+        // 32-bit: blockIdx.x * nrec < 64 * MAX_RECORDS (a 64-bit division is a ~100-instruction sequence)
+        const int b0 = (int)(blockIdx.x * (uint32_t)nrec / gridDim.x),
+                  b1 = (int)((blockIdx.x + 1) * (uint32_t)nrec / gridDim.x);
         recs += (size_t)b0 * rec_stride;
         nrec = b1 - b0;
         rank_out += (size_t)blockIdx.x * rec_floats_rank(P, K);
@@ -1000,16 +1050,18 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     int G = T / cols;
     G = G < 1 ? 1 : (G > nrec ? nrec : G);
     const int nrec_pad = (nrec + 3) & ~3;
-    float* scale = smem;
-    float* part = smem + nrec_pad;
+    float* stage = smem;
+    float* scale = STAGE ? smem + (size_t)nrec * rec_stride : smem;
+    float* part = scale + nrec_pad;
     float* erow = part + ((G * cols + 3) & ~3);
 
-    // ---- L: loads.  The StepInput fields the output phases need are fetched here too, so their
-    // latency hides under the record loads instead of stalling the tail.
+    // ---- L: loads.  The StepInput fields the output phases need are fetched first, so their latency
+    // hides under the record loads instead of stalling the tail.
     const float best_pre = (out && tid < ncol && owns(jc(tid))) ? in->best[jc(tid)] : 0.0f;
     const int qc = tid < 3 ? tid : 2;  // tail lanes 0..3: component of the four-lane layout
-    float tail_pre[13];
-    if (do_tail && tid < 4) {
+    const bool tail_lane = do_tail && tid < 4;
+    float tail_pre[13];  // kept in tail_sh across the merge (register pressure: 1024-thread block)
+    if (tail_lane) {
         tail_pre[0] = in->fzref[0];
 #pragma unroll
         for (int l = 0; l < 4; ++l) tail_pre[1 + l] = in->contact[l][0];
@@ -1019,37 +1071,102 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         for (int l = 0; l < 4; ++l) tail_pre[9 + l] = in->state[12 + 3 * l + qc];  // feet
     }
     const float state_hi = (do_tail && tid >= 12 && tid < 24) ? in->state[tid] : 0.0f;
-    float mr[MERGE_RPT];
+    // the predicted state's force-independent part (NMPC:752-784 via CMJ:93-174), formed while the
+    // record loads are in flight
+    auto tail_prep = [&]() {
+        if (tail_lane) {
+            const QuadLane L = quad_lane(mc, qc);
+            const QuadRB rb = quad_rb_prep(L, tail_pre[7], tail_pre[8]);
+            tail_sh[tid][36] = L.Ii0;
+            tail_sh[tid][37] = L.Ii1;
+            tail_sh[tid][38] = L.Ii2;
+            tail_sh[tid][39] = L.g;
+#pragma unroll
+            for (int i = 0; i < 13; ++i) tail_sh[tid][i] = tail_pre[i];
+            tail_sh[tid][13] = rb.er;
+            tail_sh[tid][14] = rb.R0;
+            tail_sh[tid][15] = rb.R1;
+            tail_sh[tid][16] = rb.R2;
+            tail_sh[tid][17] = rb.a1;
+            const int iv[5] = {mc.kind, mc.H, mc.PL, mc.S, mc.fidx};
+#pragma unroll
+            for (int i = 0; i < 5; ++i) tail_sh[tid][18 + i] = __int_as_float(iv[i]);
+            const float fv[13] = {mc.fq, mc.fomq, mc.fa, mc.fb, mc.fc, mc.fd, mc.grf_min,
+                                  mc.grf_max, mc.mu, mc.neg_mu, mc.inv_m, mc.dts[0], 0.0f};
+#pragma unroll
+            for (int i = 0; i < 13; ++i) tail_sh[tid][23 + i] = fv[i];
+        }
+    };
+    if constexpr (STAGE) {
+        constexpr int U = 8;
+        const int n4 = (nrec * rec_stride) >> 2;
+        const float4* __restrict__ src = reinterpret_cast<const float4*>(recs);
+        float4* dst = reinterpret_cast<float4*>(stage);
+        auto chunk = [&](int base, bool first) __attribute__((always_inline)) {
+            float4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = base + u * T + tid;
+                v[u] = i < n4 ? src[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
+            if (first) {
+                tail_prep();
+                MERGE_STAMP(7);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = base + u * T + tid;
+                if (i < n4) dst[i] = v[u];
+            }
+        };
+        chunk(0, true);
+        for (int base = U * T; base < n4; base += U * T) chunk(base, false);
+        __syncthreads();
+        MERGE_STAMP(6);
+        recs = stage;
+    }
+    // ---- 1. beta.  Staged: only the waves holding a record scan and reduce (nrec <= RPT * T, but a
+    // step's few hundred records sit in the first waves), and the block minimum is over those waves.
+    float mr[STAGE ? 1 : MERGE_RPT];  // staged: re-read from LDS when scaling
     uint64_t mine = KEY_NONE;
     float mtag = 0.0f;
+    const int nhw = STAGE ? (nrec + 63) >> 6 : NW;  // waves that hold a record (staged: <= RPT * NW)
+    if (!STAGE || wv < nhw) {
 #pragma unroll
-    for (int i = 0; i < MERGE_RPT; ++i) {
-        const int r = tid + i * T;
-        mr[i] = 0.0f;
-        if (r < nrec) {
-            const float* R = recs + (size_t)r * rec_stride;
-            mr[i] = R[0];
-            const uint64_t kk = ((uint64_t)f2u(mr[i]) << 32) | (uint64_t)f2u(R[2]);
-            const float tg = R[3];
-            mtag = kk < mine ? tg : mtag;
-            mine = umin64(mine, kk);
+        for (int i = 0; i < (STAGE ? MERGE_RPT : MERGE_RPT); ++i) {
+            const int r = tid + i * T;
+            if (!STAGE) mr[i] = 0.0f;
+            if (r < nrec) {
+                const float* R = recs + (size_t)r * rec_stride;
+                const float m_r = R[0];
+                if (!STAGE) mr[i] = m_r;
+                const uint64_t kk = ((uint64_t)f2u(m_r) << 32) | (uint64_t)f2u(R[2]);
+                const float tg = R[3];
+                mtag = kk < mine ? tg : mtag;
+                mine = umin64(mine, kk);
+            }
         }
+        const uint64_t wmin = wave_min_u64(mine);
+        if (lane == 0 && wv < NW) red[wv] = wmin;
     }
-    const int j = tid % cols, g = tid / cols;
+    MERGE_MARK(0);
+    const int j = (int)((uint32_t)tid % (uint32_t)cols), g = (int)((uint32_t)tid / (uint32_t)cols);
     const bool summer = !rs && tid < G * cols;
-    const int r0 = summer ? (int)((long)g * nrec / G) : 0, r1 = summer ? (int)((long)(g + 1) * nrec / G) : 0;
+    const int r0 = summer ? (int)((uint32_t)(g * nrec) / (uint32_t)G) : 0,
+              r1 = summer ? (int)((uint32_t)((g + 1) * nrec) / (uint32_t)G) : 0;
     const int off = j < ncol ? REC_HDR + jc(j) : 1;
-    float pv[MERGE_PREF];
+    constexpr int NPV = STAGE ? 1 : MERGE_PREF;  // staged: the sums read LDS directly
+    float pv[NPV];
+    if constexpr (!STAGE) {
 #pragma unroll
-    for (int i = 0; i < MERGE_PREF; ++i) pv[i] = (r0 + i < r1) ? recs[(size_t)(r0 + i) * rec_stride + off] : 0.0f;
-
-    // ---- 1. beta
-    const uint64_t wmin = wave_min_u64(mine);
-    if (lane == 0) red[wv] = wmin;
+        for (int i = 0; i < MERGE_PREF; ++i) pv[i] = (r0 + i < r1) ? recs[(size_t)(r0 + i) * rec_stride + off] : 0.0f;
+        tail_prep();
+    }
+    MERGE_MARK(1);
     __syncthreads();
+    MERGE_MARK(2);
     uint64_t bkey = red[0];
-#pragma unroll
-    for (int i = 1; i < MERGE_WAVES; ++i) bkey = umin64(bkey, red[i]);
+    for (int i = 1; i < (STAGE ? (nhw < NW ? nhw : NW) : NW); ++i) bkey = umin64(bkey, red[i]);
     const float beta = u2f((uint32_t)(bkey >> 32));
     if (mine == bkey && mine != KEY_NONE) tag_sh = mtag;  // keys are unique: one writer
     MERGE_STAMP(1);
@@ -1059,25 +1176,50 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
 #pragma unroll
         for (int i = 0; i < MERGE_RPT; ++i) {
             const int r = tid + i * T;
-            if (r < nrec) scale[r] = expf(-1.0f * (mr[i] - beta));
+            if (r < nrec) scale[r] = expf(-1.0f * ((STAGE ? recs[(size_t)r * rec_stride] : mr[i]) - beta));
         }
+        MERGE_MARK(3);
         __syncthreads();
-        if (summer) {
+        MERGE_MARK(4);
+        if constexpr (STAGE) {  // (group, column) items; more columns than threads loop (G = 1)
+            for (int q = tid; !rs && q < G * cols; q += T) {
+                const int jq = (int)((uint32_t)q % (uint32_t)cols), gq = (int)((uint32_t)q / (uint32_t)cols);
+                const int q0 = (int)((uint32_t)(gq * nrec) / (uint32_t)G), q1 = (int)((uint32_t)((gq + 1) * nrec) / (uint32_t)G);
+                const int oq = jq < ncol ? REC_HDR + jc(jq) : 1;
+                // batches of 8 LDS reads in flight, then the fixed-order sum
+                float a = 0.0f;
+                int r = q0;
+                for (; r + 8 <= q1; r += 8) {
+                    float sv[8], xv[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        sv[u] = scale[r + u];
+                        xv[u] = recs[(size_t)(r + u) * rec_stride + oq];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) a = a + sv[u] * xv[u];
+                }
+                for (; r < q1; ++r) a = a + scale[r] * recs[(size_t)r * rec_stride + oq];
+                part[gq * cols + jq] = a;
+            }
+            MERGE_MARK(5);
+        } else if (summer) {
             float a = 0.0f;
 #pragma unroll
             for (int i = 0; i < MERGE_PREF; ++i)
                 if (r0 + i < r1) a = a + scale[r0 + i] * pv[i];
-            for (int rb = r0 + MERGE_PREF; rb < r1; rb += MERGE_PREF) {
+            for (int rb0 = r0 + MERGE_PREF; rb0 < r1; rb0 += MERGE_PREF) {
 #pragma unroll
                 for (int i = 0; i < MERGE_PREF; ++i)
-                    pv[i] = (rb + i < r1) ? recs[(size_t)(rb + i) * rec_stride + off] : 0.0f;
+                    pv[i] = (rb0 + i < r1) ? recs[(size_t)(rb0 + i) * rec_stride + off] : 0.0f;
 #pragma unroll
                 for (int i = 0; i < MERGE_PREF; ++i)
-                    if (rb + i < r1) a = a + scale[rb + i] * pv[i];
+                    if (rb0 + i < r1) a = a + scale[rb0 + i] * pv[i];
             }
             part[g * cols + j] = a;
         }
         __syncthreads();
+        MERGE_MARK(6);
         for (int jj = tid; jj < cols; jj += T) {
             float a = 0.0f;
             for (int gg = 0; gg < G; ++gg) a = a + part[gg * cols + jj];
@@ -1094,9 +1236,9 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         for (int e = 1 + tid; e < K; e += T) elite[e] = KEY_NONE;
     } else {
         if (K <= 10)
-            block_topk<10>(recs, nrec, rec_stride, P, K, wlist, elite);
+            block_topk<10, NW>(recs, nrec, rec_stride, P, K, wlist, elite);
         else
-            block_topk<MAXK>(recs, nrec, rec_stride, P, K, wlist, elite);
+            block_topk<MAXK, NW>(recs, nrec, rec_stride, P, K, wlist, elite);
     }
     __syncthreads();
     // record slot of every elite key (needed when rows travel inside the records)
@@ -1154,7 +1296,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
                 const float b0 = i == tid ? best_pre : in->best[jj];
                 const float v = rs ? b0 + erow[i] : b0 + Vs[i] / Vs[ncol];
                 nb[jj] = v;
-                out->best[jj] = v;
+                ostore(&out->best[jj], v);
             }
             if (cem && !tailblk) {  // NMPC:1075-1081
                 float s = 0.0f;
@@ -1169,51 +1311,99 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
                 float sg = sqrtf(var + 1e-8f);
                 sg = sg > 5.0f ? 5.0f : sg;
                 sg = sg < 0.2f ? 0.2f : sg;
-                out->sigma[jj] = sg;
+                ostore(&out->sigma[jj], sg);
                 if (chain) in->sigma[jj] = sg;
             }
         }
         __syncthreads();
         MERGE_STAMP(4);
-        if (do_tail && tid < 4) {  // final GRFs, one thread per leg (NMPC:695-750)
-            const int leg = tid;
-            const float* pl = nb + leg * mc.PL;
-            auto acc = [pl](int jj) { return pl[jj]; };
-            float fx, fy, fz;
-            decode_leg(mc.kind, mc.H, mc.S, mc.fidx, mc.fq, mc.fomq, mc.fa, mc.fb, mc.fc, mc.fd, 0, acc, fx, fy,
-                       fz);
-            shape_leg(mc, tail_pre[0], tail_pre[1 + leg], fx, fy, fz);
-            grf_sh[3 * leg] = fx;
-            grf_sh[3 * leg + 1] = fy;
-            grf_sh[3 * leg + 2] = fz;
-        }
-        __syncthreads();
-        if (do_tail && tid < 12) out->grf[tid] = grf_sh[tid];
-        if (do_tail && tid < 4) {  // predicted state (NMPC:752-784): one Euler step in the four-lane layout
+        if (tail_lane) {
+            float ts[40];  // one batch of LDS reads
+#pragma unroll
+            for (int i = 0; i < 40; ++i) ts[i] = tail_sh[tid][i];
+            const float* tail_pre = ts;
+            const QuadRB rb{ts[13], ts[14], ts[15], ts[16], ts[17]};
+            const int kind = __float_as_int(ts[18]), H = __float_as_int(ts[19]), PL = __float_as_int(ts[20]),
+                      S = __float_as_int(ts[21]), fidx = __float_as_int(ts[22]);
+            const float fq = ts[23], fomq = ts[24], fa = ts[25], fb = ts[26], fc = ts[27], fd = ts[28];
+            const float gmin = ts[29], gmax = ts[30], mu = ts[31], neg_mu = ts[32];
+            // final GRFs (NMPC:695-750) and the predicted state (NMPC:752-784), four-lane layout: lane c
+            // decodes component c of every leg (decode_leg at step 0.0, horizon_leg 1), shapes and clips it
+            // as shape_leg does (the rollout's component form), then one Euler step from rb.  One
+            // straight-line read of the legs' parameters per kind, so the LDS reads issue together.
             const int c = qc;
-            const QuadLane L = quad_lane(mc, c);
+            float raw[4];
+            if (kind == SRBD_ZERO_ORDER) {
+#pragma unroll
+                for (int l = 0; l < 4; ++l) raw[l] = nb[l * PL + c * H];
+            } else if (kind == SRBD_LINEAR_SPLINE) {
+                float x0[4], x1[4];
+                const int o = fidx + c * (S + 1);
+#pragma unroll
+                for (int l = 0; l < 4; ++l) {
+                    x0[l] = nb[l * PL + o];
+                    x1[l] = nb[l * PL + o + 1];
+                }
+#pragma unroll
+                for (int l = 0; l < 4; ++l) raw[l] = fomq * x0[l] + fq * x1[l];
+            } else {
+                float x[4][4];
+                const int o = 10 * fidx + 4 * c;
+#pragma unroll
+                for (int l = 0; l < 4; ++l)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) x[l][k] = nb[l * PL + o + k];
+#pragma unroll
+                for (int l = 0; l < 4; ++l) {
+                    const float p0 = x[l][0], p1 = x[l][1], p2 = x[l][2], p3 = x[l][3];
+                    const float phi = 0.5f * ((p2 - p1) + (p1 - p0));
+                    const float phin = 0.5f * ((p3 - p2) + (p2 - p1));
+                    raw[l] = fa * p1 + fb * phi + fc * p2 + fd * phin;
+                }
+            }
+            float f[4];
+#pragma unroll
+            for (int l = 0; l < 4; ++l) {
+                const float cl = tail_pre[1 + l];
+                const float zp = clamp_cs((tail_pre[0] + raw[l]) * cl, gmin, gmax);
+                const float xy = div3(raw[l] * cl);
+                const float fz = qp<QP_B2>(c == 2 ? zp : xy);
+                f[l] = c == 2 ? fz : clamp_cs(xy, neg_mu * fz, mu * fz);
+            }
             float p = tail_pre[5], v = tail_pre[6], r = tail_pre[7], w = tail_pre[8];
             const float c0 = tail_pre[1], c1 = tail_pre[2], c2 = tail_pre[3], c3 = tail_pre[4];
-            const float f0 = grf_sh[c], f1 = grf_sh[3 + c], f2 = grf_sh[6 + c], f3 = grf_sh[9 + c];
-            const float temp = f0 * c0 + f1 * c1 + f2 * c2 + f3 * c3;  // integrate()'s order
-            float temp2 = quad_cross(tail_pre[9] - p, f0) * c0;
-            temp2 = temp2 + quad_cross(tail_pre[10] - p, f1) * c1;
-            temp2 = temp2 + quad_cross(tail_pre[11] - p, f2) * c2;
-            temp2 = temp2 + quad_cross(tail_pre[12] - p, f3) * c3;
-            quad_rigid_body(mc, L, temp, temp2, mc.dts[0], p, v, r, w);
+            const float temp = f[0] * c0 + f[1] * c1 + f[2] * c2 + f[3] * c3;  // integrate()'s order
+            float temp2 = quad_cross(tail_pre[9] - p, f[0]) * c0;
+            temp2 = temp2 + quad_cross(tail_pre[10] - p, f[1]) * c1;
+            temp2 = temp2 + quad_cross(tail_pre[11] - p, f[2]) * c2;
+            temp2 = temp2 + quad_cross(tail_pre[12] - p, f[3]) * c3;
+            {  // quad_rb_apply with the LDS copies of inv_m / dt and this lane's constants
+                const float lin = ts[33] * temp + ts[39];
+                const float Rt = rb.R0 * qp<QP_B0>(temp2) + rb.R1 * qp<QP_B1>(temp2) + rb.R2 * qp<QP_B2>(temp2);
+                const float a2 = ts[36] * qp<QP_B0>(Rt) + ts[37] * qp<QP_B1>(Rt) + ts[38] * qp<QP_B2>(Rt);
+                const float aa = -rb.a1 + a2;
+                const float dt = ts[34];
+                const float pn = p + v * dt, vn = v + lin * dt, rn = r + rb.er * dt, wn = w + aa * dt;
+                p = pn;
+                v = vn;
+                r = rn;
+                w = wn;
+            }
             if (tid < 3) {
-                out->pred[c] = p;
-                out->pred[3 + c] = v;
-                out->pred[6 + c] = r;
-                out->pred[9 + c] = w;
+#pragma unroll
+                for (int l = 0; l < 4; ++l) ostore(&out->grf[3 * l + c], f[l]);
+                ostore(&out->pred[c], p);
+                ostore(&out->pred[3 + c], v);
+                ostore(&out->pred[6 + c], r);
+                ostore(&out->pred[9 + c], w);
             }
         }
-        if (do_tail && tid >= 12 && tid < 24) out->pred[tid] = state_hi;
+        if (do_tail && tid >= 12 && tid < 24) ostore(&out->pred[tid], state_hi);
         if (do_tail && tid == 0) {
-            out->best_cost = beta;
-            out->best_index = (int32_t)(uint32_t)bkey;
-            out->best_freq = tag_sh;
-            out->status = 0;
+            ostore(&out->best_cost, beta);
+            ostore(&out->best_index, __uint_as_float((uint32_t)bkey));
+            ostore(&out->best_freq, tag_sh);
+            ostore(&out->status, __int_as_float(0));
             // chain: the next draws come from the device RNG.  (Split: slices read noise_scaled too, but a
             // chain's steps all run with it 0 already -- reset_noise_scaled -- so this store never changes it.)
             if (chain) in->noise_scaled = 0;
@@ -1229,20 +1419,42 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
                 if (owns(jj)) in->best[jj] = nb[jj];
             }
     }
+    if (out && shadow) {  // the burst: best[P] | sigma[P] (CEM) | grf, pred, scalars
+        __syncthreads();
+        constexpr int TAILF = (int)((sizeof(StepOutput) - offsetof(StepOutput, grf)) / sizeof(float));
+        constexpr int TAIL0 = (int)(offsetof(StepOutput, grf) / sizeof(float));
+        constexpr int SIG0 = (int)(offsetof(StepOutput, sigma) / sizeof(float));
+        const int nsig = cem ? P : 0;
+        float* o = reinterpret_cast<float*>(out);
+        for (int t = tid; t < P + nsig + TAILF; t += T) {
+            const int k = t < P ? t : (t < P + nsig ? SIG0 + (t - P) : TAIL0 + (t - P - nsig));
+            if (sysout)
+                __hip_atomic_store(reinterpret_cast<uint32_t*>(o + k), __float_as_uint(osh[k]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            else
+                o[k] = osh[k];
+        }
+    }
     MERGE_STAMP(5);
+    MERGE_MARK(8);
+    if (dbg && threadIdx.x == 0 && blockIdx.x == 0) dbg[9] = __builtin_amdgcn_s_memtime();
 #undef MERGE_STAMP
-    if (flag) {  // every thread's output writes reach the system before thread 0 publishes `seq`
+#undef MERGE_MARK
+    if (flag) {  // every thread's output writes have completed before thread 0 publishes `seq`
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
-            __threadfence_system();
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (fence_sys) {
+                __threadfence_system();
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             __hip_atomic_store(flag + (split ? blockIdx.x : 0), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
 
-__global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst mc, StepInput* __restrict__ in,
+template <int NT, bool STAGE>
+__global__ void __launch_bounds__(NT) merge_kernel(const ModelConst mc, StepInput* __restrict__ in,
                                                               const float* __restrict__ recs, int nrec,
                                                               int rec_stride, int rows_in_rec,
                                                               const float* __restrict__ noise,
@@ -1250,9 +1462,9 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_kernel(const ModelConst m
                                                               StepOutput* __restrict__ out, int chain,
                                                               int ctr_inc, uint64_t* __restrict__ dbg,
                                                               uint32_t* __restrict__ flag, uint32_t seq,
-                                                              int split_cs) {
-    merge_body(mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag, seq,
-               split_cs);
+                                                              int split_cs, int fence_sys) {
+    merge_body<NT, STAGE>(mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag,
+                      seq, split_cs, fence_sys);
 }
 
 // Sharded step without a collective launch (xGMI exchange).
@@ -1277,7 +1489,7 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_xchg_kernel(const ModelCo
     const int stride = rec_floats_rank(mc.P, mc.K);
     const uint32_t epoch = *x.epoch + 1;
     float* mine = x.stage + (size_t)x.rank * stride;
-    merge_body(mc, in, recs, nrec, rec_stride, 0, noise, mine, nullptr, 0, 0, nullptr, nullptr, 0);
+    merge_body<MERGE_THREADS, false>(mc, in, recs, nrec, rec_stride, 0, noise, mine, nullptr, 0, 0, nullptr, nullptr, 0);
     __syncthreads();
     // slot parity: epoch & 1.  A peer can run at most one exchange ahead of this rank (it cannot pass
     // its next wait before this rank has published that epoch, i.e. finished copying this one), so
@@ -1328,7 +1540,7 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_xchg_kernel(const ModelCo
                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     }
     __syncthreads();
-    merge_body(mc, in, x.stage, x.world, stride, 1, noise, nullptr, out, chain, ctr_inc, nullptr, flag, seq);
+    merge_body<MERGE_THREADS, false>(mc, in, x.stage, x.world, stride, 1, noise, nullptr, out, chain, ctr_inc, nullptr, flag, seq);
 }
 
 __global__ void advance_kernel(const ModelConst mc, StepInput* __restrict__ in, const StepOutput* __restrict__ out) {
@@ -1485,7 +1697,7 @@ void launch_transpose(const float* src, int n, int P, int ldn, float* dst, hipSt
 
 size_t merge_smem_bytes(int nrec, int P, int K) {
     const int nrec_pad = (nrec + 3) & ~3;
-    return sizeof(float) * ((size_t)nrec_pad + MERGE_THREADS + 4 + (size_t)K * P);
+    return sizeof(float) * ((size_t)nrec_pad + MERGE_THREADS + 4 + (size_t)K * P);  // part: <= T + cols
 }
 
 int merge_split_cols(const ModelConst& mc) {
@@ -1500,6 +1712,48 @@ int merge_blocks(const ModelConst& mc) {
     return cs ? 1 + (mc.P + cs - 1) / cs : 1;
 }
 
+// LDS staging of the records (merge_body<true>): when the block's records fit beside the merge's own
+// dynamic LDS.  SRBD_MERGE_STAGE=2 turns it off (measurement), SRBD_MERGE_FENCE=2 drops the system
+// fence before the publish flag (outputs are system-scope stores; 1 keeps it).
+constexpr size_t MERGE_LDS_DYN_MAX = 150 * 1024;
+static bool merge_stage_fits(int nrec_block, int rec_stride, int P, int K, size_t* smem) {
+    static const int knob = tune_knob("SRBD_MERGE_STAGE", 1);
+    const size_t base = merge_smem_bytes(nrec_block, P, K);
+    const size_t st = sizeof(float) * (size_t)nrec_block * rec_stride;
+    if (knob == 1 && (rec_stride & 3) == 0 && base + st <= MERGE_LDS_DYN_MAX &&
+        nrec_block <= MERGE_RPT * MERGE_STAGE_THREADS) {
+        *smem = base + st;
+        return true;
+    }
+    *smem = base;
+    return false;
+}
+// Called once per context before any launch (not during a graph capture).
+void merge_prepare() {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&merge_kernel<MERGE_STAGE_THREADS, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)MERGE_LDS_DYN_MAX);
+}
+static int merge_fence_sys() {
+    static const int knob = tune_knob("SRBD_MERGE_FENCE", 2);
+    return knob == 1 ? 1 : 0;
+}
+static void launch_merge_kernel(bool stage, dim3 grid, size_t smem, hipStream_t s, const ModelConst& mc,
+                                StepInput* in, const float* recs, int nrec, int rec_stride, int rows_in_rec,
+                                const float* noise, float* rank_out, StepOutput* out, int chain, int ctr_inc,
+                                uint64_t* dbg, uint32_t* flag, uint32_t seq, int split_cs) {
+    if (stage) {
+        hipLaunchKernelGGL((merge_kernel<MERGE_STAGE_THREADS, true>), grid, dim3(MERGE_STAGE_THREADS), smem, s, mc, in,
+                           recs, nrec, rec_stride,
+                           rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag, seq, split_cs,
+                           merge_fence_sys());
+    } else {
+        hipLaunchKernelGGL((merge_kernel<MERGE_THREADS, false>), grid, dim3(MERGE_THREADS), smem, s, mc, in, recs, nrec,
+                           rec_stride,
+                           rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag, seq, split_cs,
+                           merge_fence_sys());
+    }
+}
+
 int launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                  int rows_in_rec, const float* noise, float* rank_out, StepOutput* out, int chain, hipStream_t s,
                  uint64_t* dbg, int ctr_inc, Publish pub) {
@@ -1509,9 +1763,11 @@ int launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nre
     const bool split = out && !rank_out && (nrec > MERGE_SPLIT_MIN_RECS || mc.method == SRBD_CEM_MPPI);
     const int cs = split ? merge_split_cols(mc) : 0;
     const int nb = cs ? merge_blocks(mc) : 1;
-    hipLaunchKernelGGL(merge_kernel, dim3(nb), dim3(MERGE_THREADS), merge_smem_bytes(nrec, mc.P, mc.K), s, mc, in,
-                       recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, chain ? ctr_inc : 0, dbg,
-                       pub.flag, pub.seq, cs);
+    size_t smem = 0;
+    const bool stage = !cs && merge_stage_fits(nrec, rec_stride, mc.P, mc.K, &smem);
+    if (cs) smem = merge_smem_bytes(nrec, mc.P, mc.K);
+    launch_merge_kernel(stage, dim3(nb), smem, s, mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out,
+                        chain, chain ? ctr_inc : 0, dbg, pub.flag, pub.seq, cs);
     return nb;
 }
 
@@ -1580,9 +1836,10 @@ int launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, in
     const int m = merge_partials(nrec, out && !rank_out);
     if (m == 0) return launch_merge(mc, in, recs, nrec, rec_stride, 0, noise, rank_out, out, chain, s, nullptr, ctr_inc, pub);
     const int per = (nrec + m - 1) / m;
-    hipLaunchKernelGGL(merge_kernel, dim3(m), dim3(MERGE_THREADS), merge_smem_bytes(per, mc.P, mc.K), s, mc, in, recs,
-                       nrec, rec_stride, 0, noise, partials, (StepOutput*)nullptr, 0, 0, (uint64_t*)nullptr,
-                       (uint32_t*)nullptr, 0u, 0);
+    size_t smem = 0;
+    const bool stage = merge_stage_fits(per, rec_stride, mc.P, mc.K, &smem);
+    launch_merge_kernel(stage, dim3(m), smem, s, mc, in, recs, nrec, rec_stride, 0, noise, partials, nullptr, 0, 0,
+                        nullptr, nullptr, 0u, 0);
     return launch_merge(mc, in, partials, m, rec_floats_rank(mc.P, mc.K), 1, noise, rank_out, out, chain, s, nullptr,
                         ctr_inc, pub);
 }

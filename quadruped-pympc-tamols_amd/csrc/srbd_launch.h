@@ -43,6 +43,7 @@ constexpr int MERGE_SPLIT_COLS = 16;  // parameter columns per slice block (SRBD
 constexpr int MERGE_MAX_BLOCKS = 64;  // publish flags the host context holds
 constexpr int MERGE_SPLIT_MIN_RECS = 256;
 int merge_split_cols(const ModelConst& mc);
+void merge_prepare();  // once per context: the LDS-staged merge's dynamic LDS limit
 int merge_blocks(const ModelConst& mc);
 int launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                   int rows_in_rec, const float* noise, float* rank_out, StepOutput* out, int chain, hipStream_t s,

@@ -86,6 +86,8 @@ SIGNATURES = {
     "srbd_device_step_finish": (_I, [_P, _P, _I]),
     "srbd_sync_result": (_I, [_P, _FP, _FP, C.POINTER(SrbdResult)]),
     "srbd_copy_costs": (_I, [_P, _FP]),
+    "srbd_get_state": (_I, [_P, _FP, _FP, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "srbd_set_state": (_I, [_P, _FP, _FP, C.c_uint64, C.c_uint64]),
     "srbd_selftest_div": (_I, [_FP, _FP, _I, _FP, _FP]),
     "srbd_debug_merge_phases": (_I, [_P, _I, _FP]),
     "srbd_comm_get_unique_id": (_I, [C.c_char_p, _P]),
@@ -267,7 +269,7 @@ def record_floats_host(cfg: SrbdConfig) -> int:
     """Floats per rank record (== srbd_record_floats of a context of this configuration)."""
     K = cfg.num_elite if cfg.method == CEM_MPPI else 1
     P = num_params(cfg)
-    return REC_HDR + P + 2 * K + K * P
+    return (REC_HDR + P + 2 * K + K * P + 3) // 4 * 4  # padded to 16-byte words (srbd_core.h rec_pad4)
 
 
 def make_record_host(cfg: SrbdConfig, rank: int, world: int, costs: np.ndarray, noise_rows: np.ndarray) -> np.ndarray:
@@ -386,6 +388,21 @@ class Context:
         self.check(lib.srbd_copy_costs(self.h, fptr(out)), "srbd_copy_costs")
         return out
 
+    def get_state(self):
+        """srbd_get_state: (best, sigma or None, seed, counter) the next device-resident step starts from."""
+        best = np.zeros(self.P, np.float32)
+        sigma = np.zeros(self.P, np.float32) if self.cfg.method == CEM_MPPI else None
+        seed, ctr = C.c_uint64(0), C.c_uint64(0)
+        self.check(lib.srbd_get_state(self.h, fptr(best), fptr(sigma), C.byref(seed), C.byref(ctr)), "srbd_get_state")
+        return best, sigma, int(seed.value), int(ctr.value)
+
+    def set_state(self, best, sigma, seed: int, counter: int):
+        """srbd_set_state: restore a get_state checkpoint for the following device-resident steps."""
+        best = np.ascontiguousarray(np.asarray(best, np.float32).reshape(self.P))
+        sig = None if sigma is None else np.ascontiguousarray(
+            np.broadcast_to(np.asarray(sigma, np.float32), (self.P,)))
+        self.check(lib.srbd_set_state(self.h, fptr(best), fptr(sig), int(seed), int(counter)), "srbd_set_state")
+
     def bench_device_steps(self, steps: int) -> float:
         ms = _F(0)
         self.check(lib.srbd_bench_device_steps(self.h, int(steps), C.byref(ms)), "srbd_bench_device_steps")
@@ -401,9 +418,12 @@ class Context:
         return out
 
     def merge_phases(self, iters: int = 50):
-        out = np.zeros(5, np.float32)
+        out = np.zeros(24, np.float32)
         self.check(lib.srbd_debug_merge_phases(self.h, int(iters), fptr(out)), "srbd_debug_merge_phases")
-        return dict(zip(("min_key", "weighted_sums", "elite", "outputs", "tail"), (round(float(x), 3) for x in out)))
+        d = dict(zip(("min_key", "weighted_sums", "elite", "outputs", "tail", "staged_at", "tail_prep_at",
+                      "shader_mhz"), (round(float(x), 3) for x in out[:8])))
+        d["marks_us"] = [round(float(x), 3) for x in out[8:]]  # finer marks from the start (0: unset)
+        return d
 
     def set_gait(self, timing, pgg_dt: float, duty_factor: float, freq_set, freq_local=None):
         """srbd_set_gait: gait-adaptive sampling for the following steps (see include/srbd_mpc.h)."""

@@ -281,6 +281,38 @@ class Sampling_MPC:
     def reset(self):
         print("Resetting the controller")
 
+    # ------------------------------------------------------------------ checkpoint (not in the reference)
+    def get_state(self) -> dict:
+        """Checkpoint of the controller's evolving state, as plain numpy arrays (``np.savez``-able):
+        the warm start ``best_control_parameters``, the RNG key ``master_key`` and, for CEM,
+        ``sigma_cem_mppi`` -- everything the next compute call depends on besides its arguments --
+        plus, once a context exists and has stepped, the device-resident chain state (``device_*``,
+        ``srbd_get_state``).  ``set_state`` of it makes the following calls replay bit for bit."""
+        st = {"best_control_parameters": np.array(self.best_control_parameters, dtype=f32).reshape(-1),
+              "master_key": np.array(self.master_key, dtype=np.uint64).reshape(-1)}
+        if self.sampling_method == "cem_mppi":
+            st["sigma_cem_mppi"] = np.array(np.broadcast_to(np.asarray(self.sigma_cem_mppi, dtype=f32),
+                                                            (self.num_control_parameters,)), dtype=f32)
+        if self._ctx is not None and self._ctx.step_id > 0:
+            best, sigma, seed, ctr = self._ctx.get_state()
+            st["device_best"] = best
+            if sigma is not None:
+                st["device_sigma"] = sigma
+            st["device_key"] = np.array([seed, ctr], dtype=np.uint64)
+        return st
+
+    def set_state(self, st: dict) -> "Sampling_MPC":
+        """Restore a ``get_state`` checkpoint (the device part only when this controller has a stepped
+        context; a fresh controller restores it on its first compute call's context otherwise)."""
+        self.best_control_parameters = np.array(st["best_control_parameters"], dtype=f32).reshape(-1)
+        self.master_key = np.array(st["master_key"], dtype=np.uint64).reshape(-1)
+        if "sigma_cem_mppi" in st:
+            self.sigma_cem_mppi = np.array(st["sigma_cem_mppi"], dtype=f32)
+        if "device_best" in st and self._ctx is not None and self._ctx.step_id > 0:
+            key = np.asarray(st["device_key"], dtype=np.uint64)
+            self._ctx.set_state(st["device_best"], st.get("device_sigma"), int(key[0]), int(key[1]))
+        return self
+
     def close(self):
         if self._ctx is not None:
             self._ctx.close()

@@ -60,7 +60,7 @@ def main():
         w0 = CONFIGS[key]
         for n in sizes:
             w = Workload(w0.name, w0.robot, w0.gait, w0.method, w0.parametrization, n, w0.horizon, w0.num_splines)
-            for mode in ("thread", "quad"):
+            for mode in os.environ.get("SWEEP_MODES", "thread,quad").split(","):
                 print(json.dumps(run(w, mode)), flush=True)
 
 

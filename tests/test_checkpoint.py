@@ -1,0 +1,107 @@
+"""Checkpoint / restore: the controller's evolving state as plain arrays (CPU, no device),
+and exact replays of device-resident chains through srbd_get_state / srbd_set_state (GPU)."""
+import io
+
+import numpy as np
+import pytest
+
+from quadruped_pympc_amd import config as mirror
+from tests.helpers import make_case, product_cfg
+
+f32 = np.float32
+
+
+def _controller(method):
+    from quadruped_pympc_amd.controllers.sampling.centroidal_nmpc_hip import Sampling_MPC
+
+    mirror.mpc_params["sampling_method"] = method
+    try:
+        return Sampling_MPC(mirror)
+    finally:
+        mirror.mpc_params["sampling_method"] = "mppi"
+
+
+@pytest.mark.parametrize("method", ["random_sampling", "mppi", "cem_mppi"])
+def test_controller_state_round_trip_without_device(method):
+    """get_state -> np.savez -> np.load (no pickle) -> set_state restores every evolving attribute."""
+    mpc = _controller(method)
+    rng = np.random.default_rng(3)
+    mpc.best_control_parameters = rng.standard_normal(mpc.num_control_parameters).astype(f32)
+    mpc.with_newkey().with_newkey()
+    if method == "cem_mppi":
+        mpc.sigma_cem_mppi = rng.uniform(0.2, 5.0, mpc.num_control_parameters).astype(f32)
+    st = mpc.get_state()
+    assert "device_best" not in st  # no context yet: nothing on a device
+    buf = io.BytesIO()
+    np.savez(buf, **st)
+    buf.seek(0)
+    loaded = dict(np.load(buf, allow_pickle=False))
+
+    other = _controller(method)
+    other.set_state(loaded)
+    np.testing.assert_array_equal(other.best_control_parameters, mpc.best_control_parameters)
+    np.testing.assert_array_equal(other.master_key, mpc.master_key)
+    assert other.master_key[1] == 2
+    if method == "cem_mppi":
+        np.testing.assert_array_equal(other.sigma_cem_mppi, mpc.sigma_cem_mppi)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["mppi", "cem_mppi", "random_sampling"])
+def test_device_chain_replays_from_checkpoint(method):
+    """A device-resident chain restarted from a checkpoint ends in the same state bit for bit."""
+    from quadruped_pympc_amd import _lib
+
+    case = make_case("c2", N=3000, method=method, seed=5)
+    ctx = _lib.Context(product_cfg(case))
+    try:
+        ctx.step(case["state"], case["ref"], case["contact"], case["best"], sigma=case["sigma"], seed=11, counter=4)
+        s0 = ctx.get_state()
+        np.testing.assert_array_equal(s0[0], case["best"])  # a host step leaves its inputs as the state
+        assert s0[2:] == (11, 4)
+        ctx.bench_device_steps(7)
+        s1 = ctx.get_state()
+        assert s1[3] == 4 + 7  # one counter per device step
+        assert not np.array_equal(s1[0], s0[0])
+        ctx.bench_device_steps(3)  # move on, then restore
+        ctx.set_state(*s0)
+        np.testing.assert_array_equal(ctx.get_state()[0], s0[0])
+        ctx.bench_device_steps(7)
+        s1b = ctx.get_state()
+        np.testing.assert_array_equal(s1b[0], s1[0])
+        if method == "cem_mppi":
+            np.testing.assert_array_equal(s1b[1], s1[1])
+        assert s1b[2:] == s1[2:]
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_controller_replays_host_steps_from_checkpoint():
+    """Sampling_MPC: the same compute calls after set_state(get_state()) give identical outputs."""
+    mpc = _controller("mppi")
+    case = make_case("c2", N=mpc.num_parallel_computations, method="mppi", seed=9)
+    P = mpc.num_control_parameters
+    state, ref, contact = case["state"], case["ref"], case["contact"][:, :mpc.horizon]
+    try:
+        mpc.best_control_parameters = np.zeros(P, f32)
+        mpc.compute_control(state, ref, contact, mpc.best_control_parameters, mpc.master_key)
+        st = mpc.get_state()
+
+        def run(k):
+            outs = []
+            for _ in range(k):
+                r = mpc.compute_control(state, ref, contact, mpc.best_control_parameters, mpc.master_key)
+                mpc.best_control_parameters = r[3]
+                mpc.with_newkey()
+                outs.append((np.array(r[0]), np.array(r[2]), np.array(r[3])))
+            return outs
+
+        a = run(3)
+        mpc.set_state(st)
+        b = run(3)
+        for x, y in zip(a, b):
+            for u, v in zip(x, y):
+                np.testing.assert_array_equal(u, v)
+    finally:
+        mpc.close()
