@@ -293,16 +293,27 @@ def bench_single(_lib, w, args):
     k = 0
     best = run_steps(step, ins, best, k, max(1, args.warmup))
     k += max(1, args.warmup)
+    # the timed steps: srbd_step called from C (srbd_bench_host_steps), each call host-to-host at the
+    # C-ABI boundary (returns with GRFs / prediction / parameters on the host)
+    states = np.stack([x[0] for x in ins])
+    refs = np.stack([x[1] for x in ins])
+    contacts = np.stack([x[2] for x in ins])
     lat = []
     if args.steps < args.latency_steps:  # latency sample of >= latency_steps steps besides the timed region
-        best = run_steps(step, ins, best, k, args.latency_steps, lat)
+        l_us, best, state["sigma"] = ctx.bench_host_steps(states, refs, contacts, best, state["sigma"], 42, k,
+                                                          args.latency_steps)
+        lat = list(l_us * 1e-6)
         k += args.latency_steps
-    timed = []
     t0 = time.perf_counter()
-    best = run_steps(step, ins, best, k, args.steps, timed)  # srbd_step returns with outputs on the host
+    t_us, best, state["sigma"] = ctx.bench_host_steps(states, refs, contacts, best, state["sigma"], 42, k,
+                                                      args.steps)
     wall = time.perf_counter() - t0
+    k += args.steps
     if not lat:
-        lat = timed
+        lat = list(t_us * 1e-6)
+    # the same steps through the Python ctypes wrapper (Context.step), for the binding's overhead
+    py = []
+    best = run_steps(step, ins, best, k, min(300, max(20, args.latency_steps // 4)), py)
     dev = None
     if args.device_steps > 0:
         ctx.bench_device_steps(max(1, args.warmup))
@@ -312,7 +323,7 @@ def bench_single(_lib, w, args):
     kern = ctx.time_kernels(200)
     ctx.close()
     return dict(n_total=w.num_samples, n_local=w.num_samples, wall=wall, lat=lat, kern=kern, dev=dev,
-                transport=None)
+                transport=None, py_lat=py)
 
 
 def bench_multi(_lib, w, args, rank, world, local_rank, scaling):
@@ -427,8 +438,13 @@ def main(argv=None):
                    "robot": w.robot, "gait": w.gait,
                    "parallelism": (f"rows sharded over {world} GPUs ({scaling} scaling), record exchange: "
                                    f"{out['transport']}") if world > 1 else "single GPU"},
-        "step": "host-to-host srbd_step (state/ref/contact/params in, GRFs/pred/params out; noise device-resident)",
+        "step": ("host-to-host srbd_step, timed around each call in C (srbd_bench_host_steps; state/ref/contact/"
+                 "params in, GRFs/pred/params out; noise device-resident)") if world == 1 else
+                "host-to-host srbd_step_sharded through the Python binding, max over ranks",
         "device_chain": out["dev"],
+        "python_step": ({"p50_ms": round(float(np.percentile(np.array(out["py_lat"]) * 1e3, 50)), 4),
+                         "steps": len(out["py_lat"]), "path": "Context.step (ctypes) -> srbd_step"}
+                        if out.get("py_lat") else None),
         "kernels_us": {k: round(v, 3) for k, v in out["kern"].items()},
         "roofline": roofline(w, out["n_local"], out["kern"], pmc_traffic(w.name)),
     }
@@ -444,3 +460,5 @@ def main(argv=None):
 
 if __name__ == "__main__":
     main()
+    # teardown marker: a run that printed this and then did not exit hung in process teardown
+    print("bench: body done", file=sys.stderr, flush=True)

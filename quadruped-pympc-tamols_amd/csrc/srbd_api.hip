@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -1299,6 +1300,27 @@ extern "C" int srbd_bench_device_steps(srbd_ctx* c, int32_t steps, float* ms) {
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     c->cur = 0;
+    return SRBD_OK;
+}
+
+// Host-to-host srbd_step latency at the C-ABI boundary: `steps` calls cycling through n_in input sets
+// (state / ref 24 floats, contact 4 x stride each), the warm start fed back, counters consecutive from
+// counter0 (so the fused next-step draws are used, as a controller at 100 Hz does); each call timed with
+// the steady clock.  lat_us: `steps` floats.  sigma: CEM in/out or NULL.
+extern "C" int srbd_bench_host_steps(srbd_ctx* c, const float* state, const float* ref, const float* contact,
+                                     int32_t contact_stride, int32_t n_in, float* best, float* sigma, uint64_t seed,
+                                     uint64_t counter0, int32_t steps, float* lat_us) {
+    if (!c || !state || !ref || !contact || !best || !lat_us || n_in < 1 || steps < 1) return SRBD_E_INVALID;
+    srbd_result res;
+    for (int32_t i = 0; i < steps; ++i) {
+        const int k = i % n_in;
+        const auto t0 = std::chrono::steady_clock::now();
+        const int rc = srbd_step(c, state + 24 * k, ref + 24 * k, contact + (size_t)4 * contact_stride * k,
+                                 contact_stride, best, sigma, nullptr, seed, counter0 + (uint64_t)i, &res, nullptr);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (rc) return rc;
+        lat_us[i] = std::chrono::duration<float, std::micro>(t1 - t0).count();
+    }
     return SRBD_OK;
 }
 

@@ -81,6 +81,7 @@ SIGNATURES = {
     "srbd_finish_host": (_I, [C.POINTER(SrbdConfig), _FP, _I, _FP, _FP, _I, _FP, _FP, C.POINTER(SrbdResult)]),
     "srbd_make_record_host": (_I, [C.POINTER(SrbdConfig), _I, _I, _FP, _FP, _FP]),
     "srbd_bench_device_steps": (_I, [_P, _I, _FP]),
+    "srbd_bench_host_steps": (_I, [_P, _FP, _FP, _FP, _I, _I, _FP, _FP, C.c_uint64, C.c_uint64, _I, _FP]),
     "srbd_time_kernels": (_I, [_P, _I, _FP, _FP, _FP, _FP, _FP]),
     "srbd_device_step_local": (_I, [_P, _P]),
     "srbd_device_step_finish": (_I, [_P, _P, _I]),
@@ -407,6 +408,24 @@ class Context:
         ms = _F(0)
         self.check(lib.srbd_bench_device_steps(self.h, int(steps), C.byref(ms)), "srbd_bench_device_steps")
         return float(ms.value)
+
+    def bench_host_steps(self, states, refs, contacts, best, sigma=None, seed=42, counter0=0, steps=1000):
+        """srbd_bench_host_steps: per-call wall times (us) of `steps` srbd_step calls made from C."""
+        st = np.ascontiguousarray(np.asarray(states, np.float32).reshape(-1, 24))
+        rf = np.ascontiguousarray(np.asarray(refs, np.float32).reshape(-1, 24))
+        ct = np.ascontiguousarray(np.asarray(contacts, np.float32))
+        n_in = st.shape[0]
+        if ct.ndim != 3 or ct.shape[0] != n_in or ct.shape[1] != 4 or rf.shape[0] != n_in:
+            raise ValueError("states / refs (n, 24), contacts (n, 4, >=H)")
+        b = np.ascontiguousarray(np.asarray(best, np.float32).reshape(self.P)).copy()
+        sg = None if sigma is None else np.ascontiguousarray(np.broadcast_to(np.asarray(sigma, np.float32),
+                                                                             (self.P,))).copy()
+        lat = np.zeros(int(steps), np.float32)
+        self.check(lib.srbd_bench_host_steps(self.h, fptr(st), fptr(rf), fptr(ct), int(ct.shape[2]), n_in, fptr(b),
+                                             fptr(sg), int(seed), int(counter0), int(steps), fptr(lat)),
+                   "srbd_bench_host_steps")
+        self.step_id += 1
+        return lat, b, sg
 
     def time_kernels(self, iters: int):
         r, g, m, f, fl = _F(0), _F(0), _F(0), _F(0), _F(0)
