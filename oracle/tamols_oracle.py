@@ -50,21 +50,36 @@ DEFAULT_PARAMS = {
 
 
 class FastHeightMap:
-    """VFA:21-35.  data: (rows, cols, 1, 3) float64."""
+    """VFA:21-35.  data: (rows, cols, 1, 3) float64.
 
-    def __init__(self, data):
+    ``nn="kdtree"`` is the reference's lookup (cKDTree.query).  ``nn="first"`` is the same nearest
+    neighbour by brute force with the first index winning exact distance ties (the kernel's rule,
+    tamols_kernel.hip).  The two differ only when a query is exactly equidistant from two patch points:
+    cKDTree then returns the first tied point its traversal visits, which depends on the leaf order its
+    median-split build leaves behind (an introselect permutation inside scipy), so that tie rule is not
+    reproducible outside scipy (tests/test_tamols_ties.py measures how often it differs).
+    """
+
+    def __init__(self, data, nn="kdtree"):
         self.data = np.asarray(data, dtype=np.float64)
         self.points = self.data[:, :, 0, :2].reshape(-1, 2)
         self.heights = self.data[:, :, 0, 2].reshape(-1)
-        self.tree = cKDTree(self.points)
+        self.nn = nn
+        self.tree = cKDTree(self.points) if nn == "kdtree" else None
+
+    def nearest(self, target):
+        if self.tree is not None:
+            return int(self.tree.query(target[:2])[1])
+        d = (self.points[:, 0] - target[0]) ** 2 + (self.points[:, 1] - target[1]) ** 2
+        return int(np.argmin(d))  # first index among exact ties
 
     def get_height(self, target):
-        dist, idx = self.tree.query(target[:2])
-        return self.heights[idx] + 0.02
+        return self.heights[self.nearest(target)] + 0.02
 
 
 class TamolsOracle:
-    def __init__(self, params=None, robot_name="go2"):
+    def __init__(self, params=None, robot_name="go2", nn="kdtree"):
+        self.nn = nn  # FastHeightMap lookup: the reference's cKDTree, or "first" (first index on exact ties)
         self.p = dict(DEFAULT_PARAMS)
         if params:
             self.p.update(params)
@@ -197,7 +212,7 @@ class TamolsOracle:
         for leg in range(4):
             seed = np.array(seeds[leg], dtype=np.float64).copy()
             hip = np.asarray(hips[leg], dtype=np.float64)
-            hm = FastHeightMap(heightmaps[leg].reshape(R, C, 1, 3))
+            hm = FastHeightMap(heightmaps[leg].reshape(R, C, 1, 3), self.nn)
             cands = hm.data[:, :, 0, :2].reshape(-1, 2).tolist()
             best, best_score = None, float("inf")
             for i, cxy in enumerate(cands):
