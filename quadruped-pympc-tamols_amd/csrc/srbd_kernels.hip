@@ -666,27 +666,35 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
     // ZO: H values per leg; linear: S + 1; cubic: 4 per chunk (start 10 * chunk, NMPC:225).
     constexpr int NPRE = !CT ? 1 : (KIND == SRBD_ZERO_ORDER ? HT : (KIND == SRBD_LINEAR_SPLINE ? ST + 1 : 4 * ST));
     float pre[4][NPRE];
+    // noise through a buffer descriptor: per-lane part (component block + sample) in voffset, the
+    // uniform row in soffset -> no per-load address arithmetic (launch_rollout checks P*ldn*4 < 2^31)
+    const int cblk = KIND == SRBD_ZERO_ORDER ? c * HT : (KIND == SRBD_LINEAR_SPLINE ? c * (ST + 1) : 4 * c);
+    const auto nrs = __builtin_amdgcn_make_buffer_rsrc((void*)noise, (short)0, mc.P * mc.ldn * 4, 0x00020000);
+    const int voff = (cblk * mc.ldn + k) * 4;
+    const float* __restrict__ bl = best + cblk;
+    const float* __restrict__ sl = in->sigma + cblk;
+    auto load_slot = [&](const int i) __attribute__((always_inline)) {
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            const int jr = l * PL + (KIND == SRBD_CUBIC_SPLINE ? 10 * (i >> 2) + (i & 3) : i);  // row - cblk
+            const float nzv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(nrs, voff, jr * mc.ldn * 4, 0));
+            pre[l][i] = bl[jr] + (zs ? nzv * sl[jr] : nzv);
+        }
+    };
+    // Zero-order with the opt-in cost terms: a rolling window of PW slots (slot n + PW loads at step n)
+    // instead of the whole horizon up front -- the terms' extra live values otherwise push the unrolled
+    // horizon past 256 VGPRs into scratch.
+    constexpr int PW = (EXT && KIND == SRBD_ZERO_ORDER) ? (NPRE < 4 ? NPRE : 4) : NPRE;
     if constexpr (CT) {
-        // noise through a buffer descriptor: per-lane part (component block + sample) in voffset, the
-        // uniform row in soffset -> no per-load address arithmetic (launch_rollout checks P*ldn*4 < 2^31)
-        const int cblk = KIND == SRBD_ZERO_ORDER ? c * HT : (KIND == SRBD_LINEAR_SPLINE ? c * (ST + 1) : 4 * c);
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)noise, (short)0, mc.P * mc.ldn * 4, 0x00020000);
-        const int voff = (cblk * mc.ldn + k) * 4;
-        const float* __restrict__ bl = best + cblk;
-        const float* __restrict__ sl = in->sigma + cblk;
         // slot-major issue order: step n's operands are the first to return (loads complete in order),
         // so the horizon starts while the later steps' parameters are still in flight
 #pragma unroll
-        for (int i = 0; i < NPRE; ++i)
-#pragma unroll
-            for (int l = 0; l < 4; ++l) {
-                const int jr = l * PL + (KIND == SRBD_CUBIC_SPLINE ? 10 * (i >> 2) + (i & 3) : i);  // row - cblk
-                const float nzv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, jr * mc.ldn * 4, 0));
-                pre[l][i] = bl[jr] + (zs ? nzv * sl[jr] : nzv);
-            }
+        for (int i = 0; i < PW; ++i) load_slot(i);
     }
 
     auto step = [&](const int n, auto EX) __attribute__((always_inline)) {  // EX: as rollout_kernel
+        if constexpr (CT && PW < NPRE)
+            if (n + PW < NPRE) load_slot(n + PW);  // n is a compile-time constant here (unrolled horizon)
         const float cl[4] = {in->contact[0][n], in->contact[1][n], in->contact[2][n], in->contact[3][n]};
         const float fref = in->fzref[n];
         const int idx = CT && KIND != SRBD_ZERO_ORDER ? chunk_index(n, HT, ST) : mc.sidx[n];
@@ -735,10 +743,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
                     const float d = f - fprev[l];
                     term = term + (d * mc.cost_smooth) * d;
                 }
-                if (c < 2) {
+                {  // x / y lanes only, as a select (a divergent branch in the unrolled horizon spilled)
                     float vv = fabsf(xy) - mc.mu * fz;
                     vv = vv > 0.0f ? vv : 0.0f;
-                    term = term + (vv * mc.cost_cone) * vv;
+                    const float cone = (vv * mc.cost_cone) * vv;
+                    term = c < 2 ? term + cone : term;
                 }
                 ex = ex + term;
                 fprev[l] = f;
@@ -750,7 +759,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
         const float ep = p - rp, ev = v - rv, er_ = r - rr, ew = w - rw;
         const float tp = (ep * Qp) * ep, tv = (ev * Qv) * ev, tr = (er_ * Qr) * er_, tw = (ew * Qw) * ew;
         cost = cost + (((tp + tv) + tr) + tw);
-        if constexpr (decltype(EX)::value) cost = cost + ex;
+        if constexpr (decltype(EX)::value) {
+            cost = cost + ex;
+            // The terms do not feed the dynamics, so the scheduler sank them to the end of the unrolled
+            // horizon and kept every step's forces live (256 VGPRs + up to 800 B of scratch; 334
+            // registers at H12 given 512).  An empty asm on the accumulator pins each step's terms to
+            // that step: 122 VGPRs, no spill.  (The plain kernels' cost terms gain nothing from it.)
+            asm volatile("" : "+v"(cost));
+        }
     };
     auto horizon = [&](auto EX) __attribute__((always_inline)) {
         if constexpr (CT) {
@@ -1652,14 +1668,13 @@ void launch_rollout(const ModelConst& mc, const StepInput* in, const float* nois
                     int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next) {
     if (mc.ga) return launch_rollout_ga(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next);
     const int H = mc.H, S = mc.S;
-    // the opt-in cost terms (mc.cost_on): the EXT instantiations (compile-time shapes for the four-lane
-    // zero-order / linear kernels: C2 32.6 vs 38.7 us/step on the runtime shape; the cubic H16 one
-    // measured slower than its runtime-shape form, 78.9 vs 69.4 us at C3 N=10 000)
-#define SRBD_LR(K, HH, SS)                                                                                      \
-    return mc.cost_on ? launch_rollout_t<K, (K == SRBD_CUBIC_SPLINE ? 0 : HH), (K == SRBD_CUBIC_SPLINE ? 0 : SS), \
-                                         true>(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next)  \
-                      : launch_rollout_t<K, HH, SS, false>(mc, in, noise, costs, recs, rec_stride, mode, threads, s, \
-                                                           next)
+    // the opt-in cost terms (mc.cost_on): the EXT instantiations, on the same compile-time shapes (with
+    // each step's terms pinned to their step they no longer spill: C2 24.6 vs 23.3 us/step without the
+    // terms, C3 cubic H16 N=10 000 48.8 vs 47.3; the runtime-shape form took 68.7)
+#define SRBD_LR(K, HH, SS)                                                                                        \
+    return mc.cost_on                                                                                             \
+               ? launch_rollout_t<K, HH, SS, true>(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next) \
+               : launch_rollout_t<K, HH, SS, false>(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next)
     switch (mc.kind) {
         case SRBD_ZERO_ORDER:
             if (H == 10) SRBD_LR(SRBD_ZERO_ORDER, 10, 0);
