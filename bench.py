@@ -357,11 +357,18 @@ def bench_multi(_lib, w, args, rank, world, local_rank, scaling):
         dist.barrier()
         best = run_steps(step, ins, best, k, args.latency_steps, lat)
         k += args.latency_steps
+    # library-owned exchange (xGMI mailboxes / RCCL): the steps are timed from C like the one-GPU path
+    c_timed = mpc.transport in ("xgmi", "rccl")
+    arrs = (np.stack([x[0] for x in ins]), np.stack([x[1] for x in ins]), np.stack([x[2] for x in ins]))
     dist.barrier()
     torch.cuda.synchronize()
     timed = []
     t0 = time.perf_counter()
-    best = run_steps(step, ins, best, k, args.steps, timed)  # rollout -> xGMI record exchange -> merge
+    if c_timed:  # rollout -> xGMI record exchange -> merge, srbd_step_sharded from C
+        t_us, best, state["sigma"] = mpc.ctx.bench_host_steps(*arrs, best, state["sigma"], 42, k, args.steps)
+        timed = list(t_us * 1e-6)
+    else:
+        best = run_steps(step, ins, best, k, args.steps, timed)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     dist.barrier()
@@ -440,7 +447,9 @@ def main(argv=None):
                                    f"{out['transport']}") if world > 1 else "single GPU"},
         "step": ("host-to-host srbd_step, timed around each call in C (srbd_bench_host_steps; state/ref/contact/"
                  "params in, GRFs/pred/params out; noise device-resident)") if world == 1 else
-                "host-to-host srbd_step_sharded through the Python binding, max over ranks",
+                (f"host-to-host srbd_step_sharded ({out['transport']} record exchange), "
+                 + ("timed in C (srbd_bench_host_steps)" if out["transport"] in ("xgmi", "rccl")
+                    else "through the Python binding") + ", max over ranks"),
         "device_chain": out["dev"],
         "python_step": ({"p50_ms": round(float(np.percentile(np.array(out["py_lat"]) * 1e3, 50)), 4),
                          "steps": len(out["py_lat"]), "path": "Context.step (ctypes) -> srbd_step"}

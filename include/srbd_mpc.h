@@ -184,9 +184,10 @@ int srbd_set_state(srbd_ctx* ctx, const float* best_params, const float* sigma, 
 /* Measurement: replay `steps` device-resident steps (RNG -> rollout -> reduction -> warm start
  * written back on device) back to back; returns elapsed ms (hipEvents on the context stream). */
 int srbd_bench_device_steps(srbd_ctx* ctx, int32_t steps, float* elapsed_ms);
-/* Measurement: `steps` srbd_step calls from C, cycling through n_in input sets (state / ref: n_in x 24
- * floats, contact: n_in x 4 x contact_stride), best (and sigma, CEM) fed back, counters counter0,
- * counter0 + 1, ...; lat_us[i] = wall time of call i (host-to-host at the C-ABI boundary, us). */
+/* Measurement: `steps` srbd_step calls from C (srbd_step_sharded on a sharded context with a connected
+ * xGMI / RCCL exchange), cycling through n_in input sets (state / ref: n_in x 24 floats, contact:
+ * n_in x 4 x contact_stride), best (and sigma, CEM) fed back, counters counter0, counter0 + 1, ...;
+ * lat_us[i] = wall time of call i (host-to-host at the C-ABI boundary, us). */
 int srbd_bench_host_steps(srbd_ctx* ctx, const float* state, const float* ref, const float* contact,
                           int32_t contact_stride, int32_t n_in, float* best_params, float* sigma, uint64_t seed,
                           uint64_t counter0, int32_t steps, float* lat_us);

@@ -1315,8 +1315,14 @@ extern "C" int srbd_bench_host_steps(srbd_ctx* c, const float* state, const floa
     for (int32_t i = 0; i < steps; ++i) {
         const int k = i % n_in;
         const auto t0 = std::chrono::steady_clock::now();
-        const int rc = srbd_step(c, state + 24 * k, ref + 24 * k, contact + (size_t)4 * contact_stride * k,
-                                 contact_stride, best, sigma, nullptr, seed, counter0 + (uint64_t)i, &res, nullptr);
+        const float* st = state + 24 * k;
+        const float* rf = ref + 24 * k;
+        const float* ct = contact + (size_t)4 * contact_stride * k;
+        const uint64_t ctr = counter0 + (uint64_t)i;
+        const int rc = c->cfg.world_size > 1  // the library-owned exchange (xGMI mailboxes or RCCL)
+                           ? srbd_step_sharded(c, st, rf, ct, contact_stride, best, sigma, nullptr, seed, ctr, &res,
+                                               nullptr)
+                           : srbd_step(c, st, rf, ct, contact_stride, best, sigma, nullptr, seed, ctr, &res, nullptr);
         const auto t1 = std::chrono::steady_clock::now();
         if (rc) return rc;
         lat_us[i] = std::chrono::duration<float, std::micro>(t1 - t0).count();

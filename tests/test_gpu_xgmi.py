@@ -28,6 +28,7 @@ def worker_results():
     return json.loads(p.stdout.strip().splitlines()[-1])
 
 
-@pytest.mark.parametrize("case", ["mppi", "cem_mppi", "random_sampling", "mppi_w3", "mppi_ga_w3", "c5_w8", "timeout"])
+@pytest.mark.parametrize("case", ["mppi", "cem_mppi", "random_sampling", "mppi_w3", "mppi_ga_w3", "c5_w8", "bench_w2",
+                                  "timeout"])
 def test_xgmi_exchange_in_process(worker_results, case):
     assert worker_results[case] == "ok", worker_results[case]

@@ -123,6 +123,29 @@ def exchange_case(method, W=2, N=4000, ga=False, wkey="c2"):
         cx.close()
 
 
+def bench_case(W=2, N=4000, steps=3):
+    """srbd_bench_host_steps on sharded contexts (the bench's timed loop at N > 1 GPUs): every rank ends
+    on the same warm start bit for bit, equal to the unsharded loop's to reduction-order tolerance."""
+    case = make_case("c2", N=N, method="mppi", seed=29)
+    states = np.stack([case["state"]] * 2)
+    refs = np.stack([case["ref"]] * 2)
+    contacts = np.stack([case["contact"]] * 2)
+    full = _lib.Context(product_cfg(case))
+    full.step(case["state"], case["ref"], case["contact"], case["best"], seed=42, counter=0)  # warm up
+    lat0, b0, _ = full.bench_host_steps(states, refs, contacts, case["best"], None, 42, 100, steps)
+    full.close()
+    ctxs = connected(case, W)
+    outs = run_threads([lambda cx=cx: cx.bench_host_steps(states, refs, contacts, case["best"], None, 42, 100, steps)
+                        for cx in ctxs])
+    for lat, b, _ in outs:
+        assert lat.shape == (steps,) and (lat > 0).all()
+        np.testing.assert_allclose(b, b0, rtol=1e-4, atol=1e-4)
+    for o in outs[1:]:
+        np.testing.assert_array_equal(outs[0][1], o[1])
+    for cx in ctxs:
+        cx.close()
+
+
 def timeout_case():
     """A rank whose peer never arrives fails after the bounded wait (2 s) instead of hanging."""
     case = make_case("c2", N=2000, seed=5)
@@ -146,7 +169,8 @@ def main():
              ("mppi_w3", lambda: exchange_case("mppi", W=3, N=3001)),
              ("mppi_ga_w3", lambda: exchange_case("mppi", W=3, N=3001, ga=True)),
              # C5 (HyQReal bound MPPI, N=524 288) over 8 ranks of 65 536 rows: needs 8 hardware queues
-             ("c5_w8", lambda: exchange_case("mppi", W=8, N=524288, wkey="c5")), ("timeout", timeout_case)]
+             ("c5_w8", lambda: exchange_case("mppi", W=8, N=524288, wkey="c5")), ("bench_w2", bench_case),
+             ("timeout", timeout_case)]
     for name, fn in cases:
         try:
             fn()
