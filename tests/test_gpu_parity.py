@@ -162,13 +162,32 @@ def test_device_rng_matches_oracle_rng(lib):
 
 
 def test_rng_statistics(lib):
-    case = make_case("c2", N=20000, method="mppi")
+    """Device draws at N = 20 000 (MPPI, NMPC:806-812): the step's costs are the oracle's costs on the C
+    oracle's Philox stream for the same (seed, counter) -- so the device used that stream -- and that
+    stream is sigma_mppi * N(0, 1): row 0 zero (warm start), per-column means within 5 standard errors
+    of 0, the variance within 2 % of sigma^2, lag-1 correlations (across rows and across columns) below
+    5 standard errors, and a normal's tail mass beyond 2 sigma."""
+    from oracle import c_oracle as co
+
+    N = 20000
+    case = make_case("c2", N=N, method="mppi")
     case["best"][:] = 0
-    ctx = lib.Context(product_cfg(case))
-    best, _, res, costs = ctx.step(case["state"], case["ref"], case["contact"], case["best"], seed=3, counter=11,
-                                   want_costs=True)
-    ctx.close()
-    assert np.isfinite(costs).all() and res.best_index >= 0
+    o = case["orc"]
+    cfg = co.make_cfg(N=N, H=o.horizon, method=o.method, param_kind=o.param_kind, mass=case["w"].mass,
+                      inertia=case["w"].inertia)
+    noise = co.gen_noise(cfg, 3, 11)
+    g = run_gpu(lib, case, noise=False, seed=3, counter=11)
+    ref = oracle_step(case, noise)
+    np.testing.assert_allclose(g["costs"], ref["costs"], rtol=1e-4, atol=1e-2)  # libm-ulp normals
+    assert not noise[0].any()
+    z = noise[1:].astype(np.float64) / float(o.sigma_mppi)
+    n = z.shape[0]
+    assert np.abs(z.mean(axis=0)).max() < 5.0 / np.sqrt(n)
+    assert abs(z.var() - 1.0) < 0.02
+    assert abs(np.mean(z[1:] * z[:-1])) < 5.0 / np.sqrt(z.size)
+    assert abs(np.mean(z[:, 1:] * z[:, :-1])) < 5.0 / np.sqrt(z.size)
+    tail = np.mean(np.abs(z) > 2.0)
+    assert abs(tail - 0.0455) < 0.003
 
 
 def test_determinism_and_graph_equivalence(lib):
