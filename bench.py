@@ -10,7 +10,11 @@ O(N*P) input is generated and kept in HBM), fused rollout + cost + block softmax
 (argmin, MPPI/CEM update, GRFs, predicted state), outputs back on the host.  The timed region is
 exactly K such steps (`srbd_step` / `srbd_step_sharded`), bracketed by a barrier and a device
 synchronisation; `value` = rollouts of all ranks x K / max-over-ranks wall time.  `p50_step_ms` /
-`p99_step_ms` are per-step host-to-host latencies (>= 1000 steps).  `device_chain` is the same
+`p99_step_ms` are per-step host-to-host latencies (>= 1000 steps).  One GPU: the steps run armed
+(srbd_set_armed: each srbd_step queues its successor's copy / rollout / merge behind itself, the copy
+kernel waiting on a host-mapped word, so the next call stores its inputs instead of launching; outputs
+bit-identical); `unarmed_step` is the same loop with every call launching its kernels (--unarmed makes
+that the timed mode).  `device_chain` is the same
 step replayed device-resident (warm start kept on the device, hipGraph chain): the bound the host
 round trip sits on.
 
@@ -50,6 +54,7 @@ def parse_args(argv=None):
     ap.add_argument("--device-steps", type=int, default=2000, help="steps of the device-resident chain figure")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--unarmed", action="store_true", help="one GPU: time unarmed srbd_step calls")
     ap.add_argument("--extras", type=int, default=200,
                     help="steps of the supplementary interface / TAMOLS latency probes (0: skip)")
     return ap.parse_args(argv)
@@ -290,6 +295,8 @@ def bench_single(_lib, w, args):
             state["sigma"] = sg
         return b
 
+    armed = not args.unarmed
+    ctx.set_armed(armed, 0)
     k = 0
     best = run_steps(step, ins, best, k, max(1, args.warmup))
     k += max(1, args.warmup)
@@ -311,6 +318,18 @@ def bench_single(_lib, w, args):
     k += args.steps
     if not lat:
         lat = list(t_us * 1e-6)
+    # the other mode over a sample of the same loop
+    ctx.set_armed(not armed, 0)
+    n_other = max(200, min(args.steps, 2000))
+    o_us, best, state["sigma"] = ctx.bench_host_steps(states, refs, contacts, best, state["sigma"], 42, k, n_other)
+    k += n_other
+    served, cancelled = ctx.armed_stats()
+    ctx.set_armed(False, 0)
+    o_us = o_us[min(20, n_other // 10):]
+    other = {"value": round(w.num_samples / (float(o_us.mean()) * 1e-6), 1),
+             "ms_per_step": round(float(o_us.mean()) * 1e-3, 5),
+             "p50_step_ms": round(float(np.percentile(o_us, 50)) * 1e-3, 4),
+             "p99_step_ms": round(float(np.percentile(o_us, 99)) * 1e-3, 4), "steps": int(o_us.size)}
     # the same steps through the Python ctypes wrapper (Context.step), for the binding's overhead
     py = []
     best = run_steps(step, ins, best, k, min(300, max(20, args.latency_steps // 4)), py)
@@ -323,7 +342,7 @@ def bench_single(_lib, w, args):
     kern = ctx.time_kernels(200)
     ctx.close()
     return dict(n_total=w.num_samples, n_local=w.num_samples, wall=wall, lat=lat, kern=kern, dev=dev,
-                transport=None, py_lat=py)
+                transport=None, py_lat=py, armed=armed, other=other, arm_stats=(served, cancelled))
 
 
 def bench_multi(_lib, w, args, rank, world, local_rank, scaling):
@@ -445,12 +464,15 @@ def main(argv=None):
                    "robot": w.robot, "gait": w.gait,
                    "parallelism": (f"rows sharded over {world} GPUs ({scaling} scaling), record exchange: "
                                    f"{out['transport']}") if world > 1 else "single GPU"},
-        "step": ("host-to-host srbd_step, timed around each call in C (srbd_bench_host_steps; state/ref/contact/"
+        "step": (("armed " if out.get("armed") else "")
+                 + "host-to-host srbd_step, timed around each call in C (srbd_bench_host_steps; state/ref/contact/"
                  "params in, GRFs/pred/params out; noise device-resident)") if world == 1 else
                 (f"host-to-host srbd_step_sharded ({out['transport']} record exchange), "
                  + ("timed in C (srbd_bench_host_steps)" if out["transport"] in ("xgmi", "rccl")
                     else "through the Python binding") + ", max over ranks"),
         "device_chain": out["dev"],
+        **({("unarmed_step" if out["armed"] else "armed_step"): out["other"],
+            "armed_served_cancelled": list(out["arm_stats"])} if world == 1 else {}),
         "python_step": ({"p50_ms": round(float(np.percentile(np.array(out["py_lat"]) * 1e3, 50)), 4),
                          "steps": len(out["py_lat"]), "path": "Context.step (ctypes) -> srbd_step"}
                         if out.get("py_lat") else None),

@@ -112,6 +112,21 @@ int srbd_step(srbd_ctx* ctx, const float* state, const float* ref, const float* 
               float* best_params, float* sigma, const float* noise, uint64_t seed, uint64_t counter,
               srbd_result* out, float* out_costs);
 
+/* Armed host steps: the same srbd_step calls with the launch latency taken off the call.  Each
+ * srbd_step with device draws (noise == NULL) queues its successor -- copy, rollout and merge for
+ * (seed, counter + 1) -- behind itself; that chain's copy kernel waits (bounded by deadline_us, 0: 50 ms)
+ * on a host-mapped word, and the next srbd_step stores its inputs and that word instead of launching.  A
+ * call the chain cannot serve (injected noise, another counter or seed, past half the deadline) and every
+ * other entry point cancel it: the cancelled chain recomputes the previous input into scratch buffers and
+ * nothing a caller reads changes.  Outputs are bit-identical to unarmed steps.  One context per process
+ * is armed at a time.  While armed, the copy kernel occupies its hardware queue (other streams of the
+ * process that share that queue wait behind it, up to the deadline), hence opt-in: for a process whose
+ * controller owns the GPU queue (the reference's 100 Hz MPC loop).  No reference counterpart (launch
+ * latency has none in JAX's dispatch model); replaces nothing in SCI:140-159's call.  enable = 0 cancels. */
+int srbd_set_armed(srbd_ctx* ctx, int32_t enable, uint64_t deadline_us);
+/* Armed steps served (fired) and cancelled since the context was created. */
+int srbd_armed_stats(const srbd_ctx* ctx, int64_t* served, int64_t* cancelled);
+
 /*
  * Gait-adaptive sampling (centroidal_nmpc_jax_gait_adaptive.py; replaces
  * compute_rollout :326-501 and the step-frequency draws :687-692 (random sampling), :834-838

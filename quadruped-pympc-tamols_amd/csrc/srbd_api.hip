@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -101,8 +102,47 @@ struct srbd_ctx {
     hipGraphExec_t g_dev2 = nullptr, g_dev1 = nullptr;
     float* d_ga_freq = nullptr;  // injected per-row step frequencies (gait-adaptive parity mode), ldn floats
     bool input_ready = false;
+    // Armed host steps (srbd_set_armed): during a step the next one's copy, rollout and merge are queued
+    // behind it, the copy kernel spinning on the host-mapped word h_go; the next srbd_step writes its
+    // input and stores the go word instead of launching.  The armed run writes its costs into
+    // d_costs_arm (swapped in when it fires), so a cancelled run (which recomputes the previous input)
+    // leaves every buffer a later call reads unchanged.
+    int arm_mode = 0;
+    uint64_t arm_deadline_us = 50000;
+    uint32_t* h_go = nullptr;
+    uint32_t* d_go = nullptr;
+    float* d_costs_arm = nullptr;
+    bool armed = false;
+    uint32_t arm_seq = 0;
+    int arm_buf = 0, arm_nflags = 1;
+    uint64_t arm_seed = 0, arm_ctr = 0;
+    std::chrono::steady_clock::time_point arm_t0;
+    int64_t arm_served = 0, arm_cancelled = 0;
     std::string err;
 };
+
+// At most one armed context per process: an armed copy kernel holds its hardware queue until it fires,
+// is cancelled or reaches its deadline, and other streams may share that queue.  So every entry point
+// cancels the armed context's pending step (g_arm_mu guards g_armed and the contexts' armed flags).
+static std::mutex g_arm_mu;
+static srbd_ctx* g_armed = nullptr;
+static void arm_cancel_locked(srbd_ctx* c) {
+    if (!c || !c->armed) return;
+    __atomic_store_n(c->h_go, c->arm_seq | ARM_CANCEL, __ATOMIC_RELEASE);
+    c->armed = false;
+    ++c->arm_cancelled;
+    if (g_armed == c) g_armed = nullptr;
+}
+// Cancel the process's armed step unless it belongs to `keep`.
+static void arm_cancel_others(const srbd_ctx* keep = nullptr) {
+    std::lock_guard<std::mutex> lk(g_arm_mu);
+    if (g_armed && g_armed != keep) arm_cancel_locked(g_armed);
+}
+static void arm_cancel(srbd_ctx* c) {
+    std::lock_guard<std::mutex> lk(g_arm_mu);
+    arm_cancel_locked(c);
+    if (g_armed) arm_cancel_locked(g_armed);
+}
 
 #define HIP_TRY(ctx, expr)                                                                          \
     do {                                                                                            \
@@ -365,6 +405,7 @@ static void xg_drop_graphs(srbd_ctx* c);
 
 extern "C" void srbd_destroy(srbd_ctx* c) {
     if (!c) return;
+    arm_cancel(c);
     (void)hipSetDevice(c->cfg.device_id);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     comm_release(c);
@@ -375,6 +416,8 @@ extern "C" void srbd_destroy(srbd_ctx* c) {
     (void)hipFree(c->d_out);
     (void)hipFree(c->d_noise_rm);
     (void)hipFree(c->d_costs);
+    (void)hipFree(c->d_costs_arm);
+    if (c->h_go) (void)hipHostFree(c->h_go);
     (void)hipFree(c->d_wrec);
     (void)hipFree(c->d_part);
     (void)hipFree(c->d_ga_freq);
@@ -389,6 +432,7 @@ extern "C" const char* srbd_last_error(const srbd_ctx* c) { return c ? c->err.c_
 
 extern "C" int srbd_set_stream(srbd_ctx* c, void* s) {
     if (!c) return SRBD_E_INVALID;
+    arm_cancel(c);
     (void)hipSetDevice(c->cfg.device_id);
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->own_stream) HIP_TRY(c, hipStreamDestroy(c->stream));
@@ -474,10 +518,12 @@ static int upload_input(srbd_ctx* c) {
 
 // Returns the number of merge blocks that publish (wait_published).
 static int enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput* out, int chain = 0,
-                               int ctr_inc = 1, bool fuse_next = false, Publish pub = {nullptr, 0}) {
+                               int ctr_inc = 1, bool fuse_next = false, Publish pub = {nullptr, 0},
+                               float* costs = nullptr) {
     const ModelConst& mc = c->mc;
     const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1};
-    launch_rollout(mc, c->d_in, c->d_noise[buf], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
+    launch_rollout(mc, c->d_in, c->d_noise[buf], costs ? costs : c->d_costs, c->d_wrec, c->wrec_stride, c->mode,
+                   c->threads,
                    c->stream, fuse_next ? &next : nullptr);
     return launch_merge_tree(mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, c->d_noise[buf], c->d_part,
                              rank_out, out, chain, c->stream, ctr_inc, pub);
@@ -522,36 +568,127 @@ static int copy_out(srbd_ctx* c, float* best, float* sigma, srbd_result* out) {
     return SRBD_OK;
 }
 
+// Queue the next host step (draws for (seed, ctr) already in noise buffer `buf`) behind the work on
+// the stream, its copy kernel spinning on h_go (srbd_set_armed).
+static void arm_next(srbd_ctx* c, uint64_t seed, uint64_t ctr, int buf) {
+    std::lock_guard<std::mutex> lk(g_arm_mu);
+    if (g_armed && g_armed != c) arm_cancel_locked(g_armed);
+    uint32_t s = (c->seq + 1) & ~ARM_CANCEL;  // the cancel token is seq | ARM_CANCEL
+    if (s == 0) s = 1;
+    c->seq = s;
+    const size_t P4 = sizeof(float) * (size_t)c->mc.P;
+    launch_arm_copy(c->d_go, s, c->arm_deadline_us * 100ull, c->d_in_host, c->d_in, offsetof(StepInput, best) + P4,
+                    offsetof(StepInput, sigma), c->mc.method == SRBD_CEM_MPPI ? P4 : 0, c->stream);
+    c->arm_nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, true, Publish{c->d_flag, s},
+                                        c->d_costs_arm);
+    c->armed = true;
+    c->arm_seq = s;
+    c->arm_buf = buf;
+    c->arm_seed = seed;
+    c->arm_ctr = ctr;
+    c->arm_t0 = std::chrono::steady_clock::now();
+    g_armed = c;
+}
+
+// The armed chain can serve this call: device draws, the predicted (seed, counter), and well inside the
+// copy kernel's deadline (the host never fires a chain that may have timed out).
+static bool arm_claim(srbd_ctx* c, const float* noise, uint64_t seed, uint64_t counter) {
+    std::lock_guard<std::mutex> lk(g_arm_mu);
+    if (g_armed && g_armed != c) arm_cancel_locked(g_armed);
+    if (!c->armed) return false;
+    const double age_us =
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c->arm_t0).count();
+    if (!noise && seed == c->arm_seed && counter == c->arm_ctr && age_us < 0.5 * (double)c->arm_deadline_us) {
+        c->armed = false;  // claimed: nobody cancels it now
+        ++c->arm_served;
+        if (g_armed == c) g_armed = nullptr;
+        return true;
+    }
+    arm_cancel_locked(c);
+    return false;
+}
+
 extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, const float* contact,
                          int32_t contact_stride, float* best, float* sigma, const float* noise, uint64_t seed,
                          uint64_t counter, srbd_result* out, float* out_costs) {
     if (!c) return SRBD_E_INVALID;
     if (c->cfg.world_size > 1) return fail(c, SRBD_E_STATE, "sharded context: use srbd_step_local/finish");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    // the armed chain's copy kernel reads h_in only after the go word, so it can be rewritten now
+    const bool fire = c->arm_mode && arm_claim(c, noise, seed, counter);
     int rc = fill_input(&c->cfg, c->mc, c->h_in, state, ref, contact, contact_stride, best, sigma, seed, counter);
-    if (rc) return fail(c, rc, "invalid step arguments");
+    if (rc) {
+        if (fire) __atomic_store_n(c->h_go, c->arm_seq | ARM_CANCEL, __ATOMIC_RELEASE);
+        return fail(c, rc, "invalid step arguments");
+    }
     c->h_in->noise_scaled = noise ? 1 : 0;
-    if ((rc = upload_input(c))) return rc;
-    int buf = 0;
-    if ((rc = acquire_noise(c, noise, seed, counter, &buf))) return rc;
-    const bool fuse = !noise && fusable(c);
-    const Publish pub{c->d_flag, ++c->seq};
-    const int nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fuse, pub);
-    HIP_TRY(c, hipGetLastError());
-    if (fuse) {
+    const bool want_arm = c->arm_mode && !noise && fusable(c);
+    int nflags = 1;
+    uint32_t seq = 0;
+    if (fire) {
+        __atomic_store_n(c->h_go, c->arm_seq, __ATOMIC_RELEASE);
+        seq = c->arm_seq;
+        nflags = c->arm_nflags;
+        std::swap(c->d_costs, c->d_costs_arm);  // the fired run's costs
+        c->cur = c->arm_buf;
         c->pref_valid = true;
-        c->pref_buf = 1 - buf;
+        c->pref_buf = 1 - c->arm_buf;
         c->pref_seed = seed;
         c->pref_ctr = counter + 1;
+    } else {
+        if ((rc = upload_input(c))) return rc;
+        int buf = 0;
+        if ((rc = acquire_noise(c, noise, seed, counter, &buf))) return rc;
+        const bool fuse = !noise && fusable(c);
+        const Publish pub{c->d_flag, ++c->seq};
+        seq = pub.seq;
+        nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fuse, pub);
+        HIP_TRY(c, hipGetLastError());
+        if (fuse) {
+            c->pref_valid = true;
+            c->pref_buf = 1 - buf;
+            c->pref_seed = seed;
+            c->pref_ctr = counter + 1;
+        }
     }
-    if ((rc = wait_published(c, pub.seq, nflags))) return rc;
+    // arm the next step behind this one (its launches overlap this step's GPU time); with costs wanted
+    // the copy-back goes first (it would queue behind the armed copy kernel)
+    if (want_arm && !out_costs && c->pref_valid) arm_next(c, seed, counter + 1, c->pref_buf);
+    if ((rc = wait_published(c, seq, nflags))) return rc;
     if (out_costs) {
         HIP_TRY(c, hipMemcpyAsync(out_costs, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,
                                   c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
+        if (want_arm && c->pref_valid) arm_next(c, seed, counter + 1, c->pref_buf);
     }
     c->input_ready = true;
     return copy_out(c, best, sigma, out);
+}
+
+// Armed host steps (see srbd_ctx): enable != 0 queues each following srbd_step's successor ahead of its
+// input; deadline_us bounds the copy kernel's wait (0: 50 ms).  Disabling cancels a pending step.
+extern "C" int srbd_set_armed(srbd_ctx* c, int32_t enable, uint64_t deadline_us) {
+    if (!c) return SRBD_E_INVALID;
+    arm_cancel(c);
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    if (enable && c->cfg.world_size > 1) return fail(c, SRBD_E_STATE, "armed steps are for srbd_step (unsharded)");
+    if (enable && !c->h_go) {
+        HIP_TRY(c, hipHostMalloc((void**)&c->h_go, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_TRY(c, hipHostGetDevicePointer((void**)&c->d_go, c->h_go, 0));
+        __atomic_store_n(c->h_go, 0u, __ATOMIC_RELEASE);
+    }
+    if (enable && !c->d_costs_arm) HIP_TRY(c, hipMalloc((void**)&c->d_costs_arm, sizeof(float) * c->mc.ldn));
+    c->arm_mode = enable ? 1 : 0;
+    c->arm_deadline_us = deadline_us ? deadline_us : 50000;
+    return SRBD_OK;
+}
+
+extern "C" int srbd_armed_stats(const srbd_ctx* c, int64_t* served, int64_t* cancelled) {
+    if (!c) return SRBD_E_INVALID;
+    std::lock_guard<std::mutex> lk(g_arm_mu);
+    if (served) *served = c->arm_served;
+    if (cancelled) *cancelled = c->arm_cancelled;
+    return SRBD_OK;
 }
 
 // ------------------------------------------------------------------ sharded step
@@ -561,6 +698,7 @@ extern "C" int srbd_step_local(srbd_ctx* c, const float* state, const float* ref
                                int32_t contact_stride, const float* best, const float* sigma, const float* noise_local,
                                uint64_t seed, uint64_t counter, void* d_record) {
     if (!c || !d_record) return SRBD_E_INVALID;
+    arm_cancel(c);
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     // the pinned staging buffer may still feed an in-flight H2D of the previous call
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -587,6 +725,7 @@ extern "C" int srbd_step_local(srbd_ctx* c, const float* state, const float* ref
 extern "C" int srbd_step_finish(srbd_ctx* c, const void* d_records, int32_t nrec, float* best, float* sigma,
                                 srbd_result* out, float* out_costs_local) {
     if (!c || !d_records || nrec < 1 || !best) return SRBD_E_INVALID;
+    arm_cancel(c);
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "srbd_step_finish before srbd_step_local");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     const Publish pub{c->d_flag, ++c->seq};
@@ -607,6 +746,7 @@ extern "C" int srbd_step_finish(srbd_ctx* c, const void* d_records, int32_t nrec
 // advances after the merge.
 extern "C" int srbd_device_step_local(srbd_ctx* c, void* d_record) {
     if (!c || !d_record) return SRBD_E_INVALID;
+    arm_cancel(c);
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step_local once first");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     const bool fuse = fusable(c);
@@ -628,6 +768,7 @@ extern "C" int srbd_device_step_local(srbd_ctx* c, void* d_record) {
 
 extern "C" int srbd_device_step_finish(srbd_ctx* c, const void* d_records, int32_t nrec) {
     if (!c || !d_records || nrec < 1) return SRBD_E_INVALID;
+    arm_cancel(c);
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step_local once first");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     launch_merge(c->mc, c->d_in, (const float*)d_records, nrec, c->rrec_stride, 1, nullptr, nullptr, c->d_out, 1,
@@ -638,6 +779,7 @@ extern "C" int srbd_device_step_finish(srbd_ctx* c, const void* d_records, int32
 
 extern "C" int srbd_sync_result(srbd_ctx* c, float* best, float* sigma, srbd_result* out) {
     if (!c || !best) return SRBD_E_INVALID;
+    arm_cancel(c);
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(StepOutput), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -646,6 +788,7 @@ extern "C" int srbd_sync_result(srbd_ctx* c, float* best, float* sigma, srbd_res
 
 extern "C" int srbd_copy_costs(srbd_ctx* c, float* out_costs) {
     if (!c || !out_costs) return SRBD_E_INVALID;
+    arm_cancel(c);
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     HIP_TRY(c, hipMemcpyAsync(out_costs, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,
                               c->stream));
@@ -664,6 +807,7 @@ static void drop_graphs(srbd_ctx* c) {
 extern "C" int srbd_set_gait(srbd_ctx* c, const float* timing, float pgg_dt, float duty_factor, const float* freq_set,
                              int32_t n_freq, const float* freq_local) {
     if (!c || !timing || !freq_set || n_freq < 1 || n_freq > SRBD_MAX_FREQS) return SRBD_E_INVALID;
+    arm_cancel(c);
     if (c->mc.method == SRBD_CEM_MPPI)
         return fail(c, SRBD_E_INVALID,
                     "gait-adaptive CEM is not provided (the reference's branch is broken as wired, SURVEY App. B #2)");
@@ -701,6 +845,7 @@ extern "C" int srbd_set_gait(srbd_ctx* c, const float* timing, float pgg_dt, flo
 
 extern "C" int srbd_clear_gait(srbd_ctx* c) {
     if (!c) return SRBD_E_INVALID;
+    arm_cancel(c);
     if (c->mc.ga) {
         HIP_TRY(c, hipSetDevice(c->cfg.device_id));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -712,6 +857,7 @@ extern "C" int srbd_clear_gait(srbd_ctx* c) {
 
 extern "C" int srbd_set_cost_terms(srbd_ctx* c, const float* r_force, float w_smooth, float w_cone) {
     if (!c || !r_force) return SRBD_E_INVALID;
+    arm_cancel(c);
     const float w[5] = {r_force[0], r_force[1], r_force[2], w_smooth, w_cone};
     for (float x : w)
         if (!(x >= 0.0f && x < INFINITY)) return fail(c, SRBD_E_INVALID, "cost weights must be finite and >= 0");
@@ -940,6 +1086,7 @@ extern "C" int srbd_comm_get_unique_id(const char* rccl_path, uint8_t* id_out) {
 
 extern "C" int srbd_comm_init(srbd_ctx* c, const char* rccl_path, const uint8_t* id_in) {
     if (!c || !id_in) return SRBD_E_INVALID;
+    arm_cancel(c);
     if (!rccl_load(rccl_path)) return fail(c, SRBD_E_STATE, g_rccl_err);
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     comm_release(c);
@@ -967,6 +1114,7 @@ static size_t xg_bytes(const srbd_ctx* c, int world) {
 
 extern "C" int srbd_xgmi_export(srbd_ctx* c, uint8_t* handle_out) {
     if (!c || !handle_out) return SRBD_E_INVALID;
+    arm_cancel(c);
     const int world = c->cfg.world_size > 0 ? c->cfg.world_size : 1;
     if (world > XCHG_MAX_WORLD) return fail(c, SRBD_E_INVALID, "xGMI exchange: world_size > 16");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
@@ -1014,6 +1162,7 @@ static int xg_table(srbd_ctx* c, int world, float* const* bases) {
 // handles: world x 64 bytes in rank order (each rank's srbd_xgmi_export).
 extern "C" int srbd_xgmi_connect(srbd_ctx* c, const uint8_t* handles) {
     if (!c || !handles) return SRBD_E_INVALID;
+    arm_cancel(c);
     if (!c->xg_base) return fail(c, SRBD_E_STATE, "srbd_xgmi_export first");
     const int world = c->cfg.world_size > 0 ? c->cfg.world_size : 1;
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
@@ -1036,6 +1185,7 @@ extern "C" int srbd_xgmi_connect(srbd_ctx* c, const uint8_t* handles) {
 // All ranks' contexts live in this process (tests, or one process driving several GPUs).
 extern "C" int srbd_xgmi_connect_local(srbd_ctx* const* ctxs, int32_t world) {
     if (!ctxs || world < 1 || world > XCHG_MAX_WORLD) return SRBD_E_INVALID;
+    arm_cancel_others();
     float* bases[XCHG_MAX_WORLD] = {};
     for (int r = 0; r < world; ++r) {
         if (!ctxs[r] || !ctxs[r]->xg_base || ctxs[r]->cfg.rank != r || ctxs[r]->cfg.world_size != world)
@@ -1051,6 +1201,7 @@ extern "C" int srbd_xgmi_connect_local(srbd_ctx* const* ctxs, int32_t world) {
 // word arrived.  The caller agrees across ranks and falls back to RCCL if any rank failed.
 extern "C" int srbd_xgmi_probe(srbd_ctx* c, int32_t* ok) {
     if (!c || !ok) return SRBD_E_INVALID;
+    arm_cancel(c);
     if (!c->xg_world) return fail(c, SRBD_E_STATE, "srbd_xgmi_connect first");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     int* d_ok = nullptr;
@@ -1067,6 +1218,7 @@ extern "C" int srbd_xgmi_probe(srbd_ctx* c, int32_t* ok) {
 
 extern "C" int srbd_xgmi_disconnect(srbd_ctx* c) {
     if (!c) return SRBD_E_INVALID;
+    arm_cancel(c);
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     for (void* p : c->xg_opened) (void)hipIpcCloseMemHandle(p);
@@ -1168,6 +1320,7 @@ extern "C" int srbd_step_sharded(srbd_ctx* c, const float* state, const float* r
                                  int32_t contact_stride, float* best, float* sigma, const float* noise_local,
                                  uint64_t seed, uint64_t counter, srbd_result* out, float* out_costs_local) {
     if (!c || !best) return SRBD_E_INVALID;
+    arm_cancel(c);
     if (c->xg_world)
         return xg_step(c, state, ref, contact, contact_stride, best, sigma, noise_local, seed, counter, out,
                        out_costs_local);
@@ -1182,6 +1335,7 @@ extern "C" int srbd_step_sharded(srbd_ctx* c, const float* state, const float* r
 // `steps` device-resident sharded steps (warm start kept on the device), elapsed ms by hipEvents.
 extern "C" int srbd_sharded_device_steps(srbd_ctx* c, int32_t steps, float* elapsed_ms) {
     if (!c || steps < 1) return SRBD_E_INVALID;
+    arm_cancel(c);
     if (!c->xg_world && !c->comm) return fail(c, SRBD_E_STATE, "srbd_comm_init or srbd_xgmi_connect first");
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run a host step first");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
@@ -1219,6 +1373,7 @@ extern "C" int srbd_sharded_device_steps(srbd_ctx* c, int32_t steps, float* elap
 // srbd_device_step_local), whose warm start never leaves the device.
 extern "C" int srbd_get_state(srbd_ctx* c, float* best, float* sigma, uint64_t* seed, uint64_t* counter) {
     if (!c || !best) return SRBD_E_INVALID;
+    arm_cancel(c);
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "no state yet: run srbd_step (or srbd_set_state) first");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1233,6 +1388,7 @@ extern "C" int srbd_get_state(srbd_ctx* c, float* best, float* sigma, uint64_t* 
 
 extern "C" int srbd_set_state(srbd_ctx* c, const float* best, const float* sigma, uint64_t seed, uint64_t counter) {
     if (!c || !best) return SRBD_E_INVALID;
+    arm_cancel(c);
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step once first (it sets the state/reference inputs)");
     if (c->mc.method == SRBD_CEM_MPPI && !sigma) return fail(c, SRBD_E_INVALID, "CEM: sigma is part of the state");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
@@ -1280,6 +1436,7 @@ static int capture_dev_graphs(srbd_ctx* c) {
 
 extern "C" int srbd_bench_device_steps(srbd_ctx* c, int32_t steps, float* ms) {
     if (!c || steps < 1 || !ms) return SRBD_E_INVALID;
+    arm_cancel(c);
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step once before benchmarking");
     if (c->cfg.world_size > 1 || !c->own_stream) return fail(c, SRBD_E_STATE, "needs an unsharded, own-stream context");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
@@ -1332,6 +1489,7 @@ extern "C" int srbd_bench_host_steps(srbd_ctx* c, const float* state, const floa
 
 extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, float* rng_us, float* reduce_us,
                                  float* fused_us, float* floor_us) {
+    arm_cancel(c);
     // Average duration of each kernel of the step from ONE event pair around `iters` back-to-back
     // launches of it on the context stream: the per-launch figure then carries no event/dispatch
     // overhead of its own (an event pair around a single launch adds ~6 us at this size) and agrees
@@ -1390,6 +1548,7 @@ extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, 
 // [min key, weighted sums, elite, outputs, tail].
 extern "C" int srbd_debug_merge_phases(srbd_ctx* c, int32_t iters, float* out_us) {
     if (!c || iters < 1 || !out_us) return SRBD_E_INVALID;
+    arm_cancel(c);
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step once first");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     uint64_t* d = nullptr;
@@ -1485,6 +1644,7 @@ extern "C" int srbd_tamols_create(int32_t device_id, srbd_tamols_ctx** out) {
 
 extern "C" void srbd_tamols_destroy(srbd_tamols_ctx* t) {
     if (!t) return;
+    arm_cancel_others();
     (void)hipSetDevice(t->device);
     if (t->stream) (void)hipStreamSynchronize(t->stream);
     (void)hipFree(t->d_part);
@@ -1592,6 +1752,7 @@ extern "C" int srbd_tamols_run(srbd_tamols_ctx* t, const double* hm, int32_t row
                                const double* feet, const srbd_tamols_params* p, double* out_fh, double* out_box,
                                int32_t* out_valid, double* out_scores, double* out_seedh) {
     if (!t || !hm || !seeds || !hips || !p || !out_fh || !out_box || !out_valid) return SRBD_E_INVALID;
+    arm_cancel_others();
     const int nc = rows * cols;
     if (rows < 1 || cols < 1 || nc > TAMOLS_MAXCAND) {
         t->err = "patch must have 1..320 points";
@@ -1616,6 +1777,7 @@ extern "C" int srbd_tamols_run_terrain(srbd_tamols_ctx* t, srbd_terrain* ter, do
                                        double* out_fh, double* out_box, int32_t* out_valid, double* out_scores,
                                        double* out_seedh, double* out_hm) {
     if (!t || !ter || !seeds || !hips || !p || !out_fh || !out_box || !out_valid) return SRBD_E_INVALID;
+    arm_cancel_others();
     const int nc = rows * cols;
     if (rows < 1 || cols < 1 || nc > TAMOLS_MAXCAND) {
         t->err = "patch must have 1..320 points";
@@ -1648,6 +1810,7 @@ extern "C" int srbd_tamols_run_terrain(srbd_tamols_ctx* t, srbd_terrain* ter, do
 // first block's start to the last leg's end (us, 100 MHz s_memrealtime).
 extern "C" int srbd_tamols_phases(srbd_tamols_ctx* t, int32_t enable, float* out_us) {
     if (!t) return SRBD_E_INVALID;
+    arm_cancel_others();
     TAM_TRY(t, hipSetDevice(t->device));
     const size_t n = 4 * TAMOLS_BPL * 8;
     if (enable && !t->d_dbg) {
@@ -1681,6 +1844,7 @@ extern "C" int srbd_tamols_phases(srbd_tamols_ctx* t, int32_t enable, float* out
 // Diagnostic: the raw stamps of the last call (4 x TAMOLS_BPL x 8 uint64, 100 MHz ticks).
 extern "C" int srbd_tamols_phases_raw(srbd_tamols_ctx* t, uint64_t* out) {
     if (!t || !out || !t->d_dbg) return SRBD_E_INVALID;
+    arm_cancel_others();
     TAM_TRY(t, hipSetDevice(t->device));
     TAM_TRY(t, hipMemcpy(out, t->d_dbg, sizeof(uint64_t) * 4 * TAMOLS_BPL * 8, hipMemcpyDeviceToHost));
     return SRBD_OK;

@@ -1872,6 +1872,34 @@ void launch_copy16(const void* src, void* dst, size_t bytes0, size_t off1, size_
                        (int)(off1 / 16), (int)(bytes1 / 16));
 }
 
+// Armed step (launch_arm_copy): the step's input copy, queued before the host has the input.
+__global__ void __launch_bounds__(256) arm_copy_kernel(const uint32_t* __restrict__ go, uint32_t seq,
+                                                       uint64_t deadline_ticks, const uint32_t* __restrict__ src,
+                                                       uint32_t* __restrict__ dst, int n0, int off1, int n1) {
+    __shared__ int fire;
+    if (threadIdx.x == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t g = __hip_atomic_load(go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        while (g != seq && g != (seq | ARM_CANCEL) && __builtin_amdgcn_s_memrealtime() - t0 < deadline_ticks) {
+            __builtin_amdgcn_s_sleep(1);
+            g = __hip_atomic_load(go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        fire = g == seq;
+    }
+    __syncthreads();
+    if (!fire) return;
+    // 32-bit words; system scope, so nothing is served from a cache line older than the host's stores
+    for (int i = threadIdx.x; i < n0 + n1; i += blockDim.x) {
+        const int k = i < n0 ? i : off1 + (i - n0);
+        dst[k] = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+void launch_arm_copy(const uint32_t* go, uint32_t seq, uint64_t deadline_ticks, const void* src, void* dst,
+                     size_t bytes0, size_t off1, size_t bytes1, hipStream_t s) {
+    hipLaunchKernelGGL(arm_copy_kernel, dim3(1), dim3(256), 0, s, go, seq, deadline_ticks, (const uint32_t*)src,
+                       (uint32_t*)dst, (int)(bytes0 / 4), (int)(off1 / 4), (int)(bytes1 / 4));
+}
+
 __global__ void empty_kernel() {}
 void launch_empty(hipStream_t s) { hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s); }
 

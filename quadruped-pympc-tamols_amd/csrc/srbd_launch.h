@@ -90,6 +90,13 @@ void launch_advance(const ModelConst& mc, StepInput* in, const StepOutput* out, 
 void launch_empty(hipStream_t s);  // measurement: the event floor
 // src -> dst bytes [0, bytes0) and [off1, off1 + bytes1); all multiples of 16
 void launch_copy16(const void* src, void* dst, size_t bytes0, size_t off1, size_t bytes1, hipStream_t s);
+// Armed step: the copy kernel launched ahead of its input.  Lane 0 spins (s_sleep, bounded by
+// `deadline_ticks` of the 100 MHz clock) on the host-mapped word `go` until it reads `seq` (fire: copy as
+// launch_copy16 does, source read with system-scope loads) or `seq | ARM_CANCEL` / the deadline (no
+// copy: the chain behind it recomputes the previous input and the host discards that run).
+constexpr uint32_t ARM_CANCEL = 0x80000000u;
+void launch_arm_copy(const uint32_t* go, uint32_t seq, uint64_t deadline_ticks, const void* src, void* dst,
+                     size_t bytes0, size_t off1, size_t bytes1, hipStream_t s);
 void launch_div_selftest(const float* a, const float* b, int n, float* o, hipStream_t s);
 
 // TAMOLS (tamols_kernel.hip)

@@ -75,6 +75,8 @@ SIGNATURES = {
     "srbd_set_gait": (_I, [_P, _FP, _F, _F, _FP, _I, _FP]),
     "srbd_clear_gait": (_I, [_P]),
     "srbd_set_cost_terms": (_I, [_P, _FP, _F, _F]),
+    "srbd_set_armed": (_I, [_P, C.c_int32, C.c_uint64]),
+    "srbd_armed_stats": (_I, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "srbd_record_floats": (_I, [_P]),
     "srbd_step_local": (_I, [_P, _FP, _FP, _FP, _I, _FP, _FP, _FP, C.c_uint64, C.c_uint64, _P]),
     "srbd_step_finish": (_I, [_P, _P, _I, _FP, _FP, C.POINTER(SrbdResult), _FP]),
@@ -462,6 +464,17 @@ class Context:
         reference's cost)."""
         r = np.ascontiguousarray(np.asarray(r_force, np.float32).reshape(3))
         self.check(lib.srbd_set_cost_terms(self.h, fptr(r), float(w_smooth), float(w_cone)), "srbd_set_cost_terms")
+
+    def set_armed(self, enable: bool = True, deadline_us: int = 0):
+        """srbd_set_armed: queue each host step's successor ahead of its input (launch latency off the call;
+        outputs unchanged).  deadline_us bounds the armed copy kernel's wait (0: 50 ms)."""
+        self.check(lib.srbd_set_armed(self.h, 1 if enable else 0, int(deadline_us)), "srbd_set_armed")
+
+    def armed_stats(self):
+        """srbd_armed_stats: (steps served by an armed chain, armed chains cancelled)."""
+        a, b = C.c_int64(0), C.c_int64(0)
+        self.check(lib.srbd_armed_stats(self.h, C.byref(a), C.byref(b)), "srbd_armed_stats")
+        return int(a.value), int(b.value)
 
     def set_stream(self, stream_handle: int | None):
         """Launch on a caller-owned hipStream_t; None (or 0, the legacy null stream) -> the context's own."""

@@ -7,6 +7,9 @@
 //   two_launch_flag    two dependent kernels, the second writes the flag
 //   h2d_launch_sync    4 KB pinned H2D + kernel + sync
 //   graph2_sync        graph of two kernels + sync
+//   three_launch_flag  three dependent kernels launched now, the third writes the flag
+//   armed3_flag        the same three kernels launched beforehand, the first spinning on a host-mapped
+//                      go word (bounded): host stores go, spins on the flag (pre-armed step)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,6 +36,18 @@ __global__ void k_flag_args(volatile unsigned* host_flag, unsigned seq, Big b, f
         __threadfence_system();
         *host_flag = seq;
     }
+}
+
+// Spins (bounded: 2e7 ticks of the 100 MHz clock = 200 ms) until *go == seq.
+__global__ void k_arm(const unsigned* go, unsigned seq) {
+    if (threadIdx.x == 0) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) break;
+        }
+    }
+    __syncthreads();
 }
 
 template <class F>
@@ -89,6 +104,33 @@ int main() {
         k_empty<<<1, 64, 0, s>>>(d);
         hipStreamSynchronize(s);
     });
+    double three = p50([&](int i) {
+        k_empty<<<1, 64, 0, s>>>(d);
+        k_empty<<<1, 64, 0, s>>>(d);
+        k_flag<<<1, 64, 0, s>>>(dflag, (unsigned)i + 1);
+        spin((unsigned)i + 1);
+    });
+    unsigned* hgo;
+    hipHostMalloc((void**)&hgo, 64, hipHostMallocMapped | hipHostMallocCoherent);
+    unsigned* dgo;
+    hipHostGetDevicePointer((void**)&dgo, hgo, 0);
+    *hgo = 0;
+    std::vector<double> ta;
+    for (int i = 0; i < 3100; ++i) {
+        const unsigned q = 100000u + (unsigned)i;
+        k_arm<<<1, 64, 0, s>>>(dgo, q);
+        k_empty<<<1, 64, 0, s>>>(d);
+        k_flag<<<1, 64, 0, s>>>(dflag, q);
+        const auto w0 = std::chrono::steady_clock::now();  // let the arm kernel become resident
+        while (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w0).count() < 30.0) {
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        __atomic_store_n(hgo, q, __ATOMIC_RELEASE);
+        spin(q);
+        if (i >= 100) ta.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    }
+    std::nth_element(ta.begin(), ta.begin() + ta.size() / 2, ta.end());
+    const double armed = ta[ta.size() / 2];
     hipGraph_t g;
     hipGraphExec_t ge;
     hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
@@ -102,7 +144,7 @@ int main() {
     });
     hipStreamSynchronize(s);
     printf("{\"launch_sync\": %.2f, \"launch_flag\": %.2f, \"args3k_flag\": %.2f, \"two_launch_flag\": %.2f, "
-           "\"h2d_launch_sync\": %.2f, \"graph2_sync\": %.2f}\n",
-           a, bflag, cargs, two, h2d, gr);
+           "\"h2d_launch_sync\": %.2f, \"graph2_sync\": %.2f, \"three_launch_flag\": %.2f, \"armed3_flag\": %.2f}\n",
+           a, bflag, cargs, two, h2d, gr, three, armed);
     return 0;
 }

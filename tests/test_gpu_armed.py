@@ -1,0 +1,157 @@
+"""Armed host steps (srbd_set_armed): the next srbd_step's copy, rollout and merge are queued during the
+current one, the copy kernel waiting on a host-mapped word.  The outputs must be those of unarmed steps
+bit for bit, on the serve path and on every cancel path (injected noise, a counter jump, another entry
+point, the deadline, another context, destroy)."""
+import time
+
+import numpy as np
+import pytest
+
+from helpers import make_case, product_cfg
+
+pytestmark = pytest.mark.gpu
+f32 = np.float32
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from quadruped_pympc_amd import _lib
+
+    if _lib.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X")
+    return _lib
+
+
+def _inputs(case, k):
+    """Step k's state / reference: the case's, nudged so consecutive steps differ."""
+    st = case["state"].copy()
+    rf = case["ref"].copy()
+    st[0:3] += f32(0.001 * k)
+    rf[3] += f32(0.01 * (k % 5))
+    return st, rf
+
+
+def _run(lib, case, script, armed, deadline_us=0, stats=None):
+    """Run `script` (a list of actions) on a fresh context; returns every step's outputs (and, armed,
+    appends (served, cancelled) to `stats`)."""
+    ctx = lib.Context(product_cfg(case))
+    if armed:
+        ctx.set_armed(True, deadline_us)
+    best = case["best"].copy()
+    sigma = case["sigma"]
+    outs = []
+    try:
+        for k, act in enumerate(script):
+            kind = act[0]
+            if kind == "step":
+                _, ctr, want = act
+                st, rf = _inputs(case, k)
+                best, sg, res, costs = ctx.step(st, rf, case["contact"], best, sigma=sigma, seed=5, counter=ctr,
+                                                want_costs=want)
+                if sg is not None:
+                    sigma = sg
+                outs.append((best.copy(), np.array(res.grf, f32), np.array(res.predicted_state, f32),
+                             res.best_cost, res.best_index, costs))
+            elif kind == "noise":  # injected perturbations (parity mode)
+                st, rf = _inputs(case, k)
+                best, sg, res, costs = ctx.step(st, rf, case["contact"], best, sigma=sigma, noise=case["noise"],
+                                                seed=5, counter=act[1], want_costs=True)
+                outs.append((best.copy(), np.array(res.grf, f32), np.array(res.predicted_state, f32),
+                             res.best_cost, res.best_index, costs))
+            elif kind == "costs":
+                outs.append(("costs", ctx.copy_costs()))
+            elif kind == "terms":
+                ctx.set_cost_terms(*act[1])
+            elif kind == "sleep":
+                time.sleep(act[1])
+            elif kind == "state":
+                b, s, seed, ctr = ctx.get_state()
+                outs.append(("state", b, seed, ctr))
+        if stats is not None:
+            stats.append(ctx.armed_stats())
+    finally:
+        ctx.close()
+    return outs
+
+
+def _same(a, b):
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        assert len(x) == len(y)
+        for u, v in zip(x, y):
+            if u is None or isinstance(u, str):
+                assert u == v
+            else:
+                np.testing.assert_array_equal(np.asarray(u), np.asarray(v))
+
+
+@pytest.mark.parametrize("wkey,method,par,N", [
+    ("c2", "mppi", "zero_order", 10000),
+    ("c2", "random_sampling", "zero_order", 3001),
+    ("c3", "cem_mppi", "cubic_spline", 4096),
+    ("c2", "mppi", "linear_spline", 65536),
+])
+def test_armed_chain_bitwise(lib, wkey, method, par, N):
+    """Consecutive counters: every step after the first is served by the armed chain."""
+    case = make_case(wkey, N=N, method=method, par=par)
+    script = [("step", 100 + k, k % 7 == 3) for k in range(24)]
+    st = []
+    _same(_run(lib, case, script, armed=True, stats=st), _run(lib, case, script, armed=False))
+    assert st[0] == (23, 0)  # every step but the first was served
+
+
+def test_armed_cancel_paths(lib):
+    case = make_case("c2", N=10000, method="mppi")
+    script = ([("step", 10 + k, False) for k in range(4)]
+              + [("noise", 50)]                            # injected noise: cancel, parity path
+              + [("step", 51, False), ("step", 52, False)]
+              + [("step", 90, False)]                      # counter jump
+              + [("step", 91, False), ("costs",)]          # another entry point reads the served step's costs
+              + [("step", 92, False), ("terms", ((0.1, 0.1, 0.001), 0.01, 5.0)), ("step", 93, False)]
+              + [("terms", ((0.0, 0.0, 0.0), 0.0, 0.0)), ("step", 94, False)]
+              + [("sleep", 0.03), ("step", 95, False)]     # past half the 20 ms deadline: not served
+              + [("step", 96, True), ("state",), ("step", 97, False), ("step", 98, False)])
+    st = []
+    _same(_run(lib, case, script, armed=True, deadline_us=20000, stats=st), _run(lib, case, script, armed=False))
+    # served: 11-13, 52, 91, 96, 98; cancelled by: the noise call, the counter jump, copy_costs, both
+    # set_cost_terms, the expired chain before step 95, get_state
+    assert st[0] == (7, 7), st
+
+
+def test_armed_other_context_not_stalled(lib):
+    """A second context's call cancels the first's armed step instead of queueing behind its copy kernel
+    until the deadline (2 s here); the first context's next step then runs unarmed, same outputs."""
+    case = make_case("c2", N=4096, method="mppi")
+    a = lib.Context(product_cfg(case))
+    b = lib.Context(product_cfg(case))
+    ref = lib.Context(product_cfg(case))
+    try:
+        a.set_armed(True, 2_000_000)
+        ba = br = case["best"].copy()
+        for k in range(3):
+            ba, _, ra, _ = a.step(case["state"], case["ref"], case["contact"], ba, seed=1, counter=k)
+            br, _, rr, _ = ref.step(case["state"], case["ref"], case["contact"], br, seed=1, counter=k)
+        t0 = time.perf_counter()
+        b.step(case["state"], case["ref"], case["contact"], case["best"], seed=9, counter=0)
+        assert time.perf_counter() - t0 < 0.5
+        ba, _, ra, _ = a.step(case["state"], case["ref"], case["contact"], ba, seed=1, counter=3)
+        br, _, rr, _ = ref.step(case["state"], case["ref"], case["contact"], br, seed=1, counter=3)
+        np.testing.assert_array_equal(ba, br)
+        np.testing.assert_array_equal(np.array(ra.grf), np.array(rr.grf))
+        t0 = time.perf_counter()
+        a.close()  # armed again after that step: destroy cancels it
+        assert time.perf_counter() - t0 < 0.5
+    finally:
+        a.close()
+        b.close()
+        ref.close()
+
+
+def test_armed_deadline_expiry_on_device(lib):
+    """The copy kernel gives up at its deadline (5 ms) on its own; the stream drains and the next step
+    (not served: past half the deadline) matches the unarmed run."""
+    case = make_case("c2", N=2048, method="mppi")
+    script = [("step", 0, False), ("step", 1, False), ("sleep", 0.05), ("step", 2, False), ("step", 3, False)]
+    st = []
+    _same(_run(lib, case, script, armed=True, deadline_us=5000, stats=st), _run(lib, case, script, armed=False))
+    assert st[0][0] == 2, st  # steps 1 and 3; step 2 found the chain past its deadline
