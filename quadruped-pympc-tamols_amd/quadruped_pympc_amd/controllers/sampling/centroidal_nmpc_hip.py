@@ -164,6 +164,11 @@ class Sampling_MPC:
             if terms:
                 self._ctx.set_cost_terms(terms.get("r_force", (0.0, 0.0, 0.0)), terms.get("w_smooth", 0.0),
                                          terms.get("w_cone", 0.0))
+            # optional (not in the reference): mpc_params['armed_steps'] = True queues each step's successor
+            # ahead of its input (srbd_set_armed; outputs unchanged, launch latency off the call) -- for a
+            # controller process that owns its GPU queue; 'armed_deadline_us' bounds the wait (default 50 ms)
+            if self._cfg.mpc_params.get("armed_steps", False):
+                self._ctx.set_armed(True, int(self._cfg.mpc_params.get("armed_deadline_us", 0)))
         return self._ctx
 
     def _run(self, state, reference, contact_sequence, best_control_parameters, key, sigma, noise):
