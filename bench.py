@@ -10,11 +10,11 @@ O(N*P) input is generated and kept in HBM), fused rollout + cost + block softmax
 (argmin, MPPI/CEM update, GRFs, predicted state), outputs back on the host.  The timed region is
 exactly K such steps (`srbd_step` / `srbd_step_sharded`), bracketed by a barrier and a device
 synchronisation; `value` = rollouts of all ranks x K / max-over-ranks wall time.  `p50_step_ms` /
-`p99_step_ms` are per-step host-to-host latencies (>= 1000 steps).  One GPU: the steps run armed
-(srbd_set_armed: each srbd_step queues its successor's copy / rollout / merge behind itself, the copy
-kernel waiting on a host-mapped word, so the next call stores its inputs instead of launching; outputs
-bit-identical); `unarmed_step` is the same loop with every call launching its kernels (--unarmed makes
-that the timed mode).  `device_chain` is the same
+`p99_step_ms` are per-step host-to-host latencies (>= 1000 steps).  The timed steps launch their
+kernels in the call (as the sharded steps of N > 1 do, so per-N values compare).  One GPU also reports
+`armed_step`: the same loop with srbd_set_armed (each srbd_step queues its successor's copy / rollout /
+merge behind itself, the copy kernel waiting on a host-mapped word, so the next call stores its inputs
+instead of launching; outputs bit-identical); --armed makes that the timed mode.  `device_chain` is the same
 step replayed device-resident (warm start kept on the device, hipGraph chain): the bound the host
 round trip sits on.
 
@@ -54,7 +54,7 @@ def parse_args(argv=None):
     ap.add_argument("--device-steps", type=int, default=2000, help="steps of the device-resident chain figure")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--unarmed", action="store_true", help="one GPU: time unarmed srbd_step calls")
+    ap.add_argument("--armed", action="store_true", help="one GPU: time armed srbd_step calls (srbd_set_armed)")
     ap.add_argument("--extras", type=int, default=200,
                     help="steps of the supplementary interface / TAMOLS latency probes (0: skip)")
     return ap.parse_args(argv)
@@ -295,7 +295,7 @@ def bench_single(_lib, w, args):
             state["sigma"] = sg
         return b
 
-    armed = not args.unarmed
+    armed = bool(args.armed)
     ctx.set_armed(armed, 0)
     k = 0
     best = run_steps(step, ins, best, k, max(1, args.warmup))
