@@ -184,7 +184,7 @@ def cpu_baseline(w, seconds: float):
             "ms_per_step": round(1e3 * dt / max(n, 1), 3)}
 
 
-def interface_latency(w, steps: int):
+def interface_latency(w, steps: int, armed: bool = False, outputs: list | None = None, stats: list | None = None):
     """p50 / p99 ms of one MPC step through the reference's Python plugin API at the workload's shape:
     PeriodicGaitGenerator.compute_contact_sequence (C++ host producer) + SRBDControllerInterface.
     compute_control (prepare_state_and_reference, with_newkey, jitted_compute_control, LegsAttr masking),
@@ -206,7 +206,7 @@ def interface_latency(w, steps: int):
     cfg.robot, cfg.mass, cfg.inertia = w.robot, ROBOTS[w.robot][0], np.array(ROBOTS[w.robot][1])
     cfg.mpc_params.update(horizon=w.horizon, sampling_method=w.method, control_parametrization=w.parametrization,
                           num_splines=w.num_splines, num_parallel_computations=w.num_samples, sigma_mppi=w.sigma,
-                          grf_max=cfg.mass * 9.81, device_id=0)
+                          grf_max=cfg.mass * 9.81, device_id=0, armed_steps=armed)
     iface = SRBDControllerInterface(cfg)
     gtype, freq, duty = GAITS[w.gait]
     pgg = PeriodicGaitGenerator(duty, freq, gtype, w.horizon)
@@ -226,12 +226,17 @@ def interface_latency(w, steps: int):
         cs = pgg.compute_contact_sequence(dts, lens)
         out = iface.compute_control(state, ref, cs, cfg.inertia, pgg.phase_signal, pgg.step_freq, 0)
         lat.append(time.perf_counter() - t0)
+        if outputs is not None:
+            outputs.append(out)
     assert np.isfinite(np.concatenate([out[0].FL, out[6]])).all()
+    if stats is not None:
+        stats.append(iface.controller.context.armed_stats())
     iface.controller.close()
     lat = np.array(lat[20:]) * 1e3
     return {"p50_ms": round(float(np.percentile(lat, 50)), 4), "p99_ms": round(float(np.percentile(lat, 99)), 4),
             "steps": steps, "path": "PeriodicGaitGenerator.compute_contact_sequence + "
-                                    "SRBDControllerInterface.compute_control (Python plugin API)"}
+                                    "SRBDControllerInterface.compute_control (Python plugin API)"
+                                    + (", mpc_params['armed_steps']" if armed else "")}
 
 
 def tamols_latency(calls: int):
@@ -485,6 +490,7 @@ def main(argv=None):
         line["cpu_baseline"] = None
     if world == 1 and args.extras and args.config in ("c2", "c4"):  # the callers either side of the path
         line["interface_step"] = interface_latency(w, args.extras)
+        line["interface_step_armed"] = interface_latency(w, args.extras, armed=True)
         line["tamols_c4"] = tamols_latency(args.extras)
     print(json.dumps(line), flush=True)
 

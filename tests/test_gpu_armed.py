@@ -155,3 +155,32 @@ def test_armed_deadline_expiry_on_device(lib):
     st = []
     _same(_run(lib, case, script, armed=True, deadline_us=5000, stats=st), _run(lib, case, script, armed=False))
     assert st[0][0] == 2, st  # steps 1 and 3; step 2 found the chain past its deadline
+
+
+def test_armed_plugin_api_bitwise(lib):
+    """The reference's call path (PeriodicGaitGenerator + SRBDControllerInterface.compute_control, a new
+    key per call) with mpc_params['armed_steps']: outputs equal the unarmed loop's bit for bit."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from quadruped_pympc_amd.synthetic import CONFIGS
+
+    runs, st = [], []
+    for armed in (True, False):
+        outs = []
+        bench.interface_latency(CONFIGS["c2"], 12, armed=armed, outputs=outs, stats=st)
+        runs.append(outs)
+    assert st[0][0] >= 30 and st[1] == (0, 0), st  # 32 calls: all but the first served
+    for a, b in zip(*runs):
+        assert len(a) == len(b)
+        for u, v in zip(a, b):
+            if hasattr(u, "FL"):
+                for leg in ("FL", "FR", "RL", "RR"):
+                    np.testing.assert_array_equal(np.asarray(getattr(u, leg)), np.asarray(getattr(v, leg)))
+            elif u is None or isinstance(u, (str, bool)):
+                assert u == v
+            else:
+                np.testing.assert_array_equal(np.asarray(u, dtype=object if isinstance(u, (list, tuple)) else None),
+                                              np.asarray(v, dtype=object if isinstance(v, (list, tuple)) else None))
