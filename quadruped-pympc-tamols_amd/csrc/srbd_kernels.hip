@@ -1495,7 +1495,10 @@ __global__ void __launch_bounds__(NT) merge_kernel(const ModelConst mc, StepInpu
 //  4. pass 2 merges the W rank records in rank order, exactly as srbd_step_finish does.
 // Costs (MI355X, one rank): all-thread agent + system fences and a system acquire here cost 7 us per
 // step; this form measures within noise of no release at all (scripts/sharded_probe.py).
-__global__ void __launch_bounds__(MERGE_THREADS) merge_xchg_kernel(const ModelConst mc, StepInput* __restrict__ in,
+// NT / STAGE1: pass 1 as the single-rank merge runs it -- the LDS-staged 512-thread body when this
+// rank's block records fit (C2: 157), else the 1024-thread direct body; pass 2 (W records) direct.
+template <int NT, bool STAGE1>
+__global__ void __launch_bounds__(NT) merge_xchg_kernel(const ModelConst mc, StepInput* __restrict__ in,
                                                                    const float* __restrict__ recs, int nrec,
                                                                    int rec_stride, const float* __restrict__ noise,
                                                                    XchgArgs x, StepOutput* __restrict__ out,
@@ -1505,7 +1508,7 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_xchg_kernel(const ModelCo
     const int stride = rec_floats_rank(mc.P, mc.K);
     const uint32_t epoch = *x.epoch + 1;
     float* mine = x.stage + (size_t)x.rank * stride;
-    merge_body<MERGE_THREADS, false>(mc, in, recs, nrec, rec_stride, 0, noise, mine, nullptr, 0, 0, nullptr, nullptr, 0);
+    merge_body<NT, STAGE1>(mc, in, recs, nrec, rec_stride, 0, noise, mine, nullptr, 0, 0, nullptr, nullptr, 0);
     __syncthreads();
     // slot parity: epoch & 1.  A peer can run at most one exchange ahead of this rank (it cannot pass
     // its next wait before this rank has published that epoch, i.e. finished copying this one), so
@@ -1556,7 +1559,7 @@ __global__ void __launch_bounds__(MERGE_THREADS) merge_xchg_kernel(const ModelCo
                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     }
     __syncthreads();
-    merge_body<MERGE_THREADS, false>(mc, in, x.stage, x.world, stride, 1, noise, nullptr, out, chain, ctr_inc, nullptr, flag, seq);
+    merge_body<NT, false>(mc, in, x.stage, x.world, stride, 1, noise, nullptr, out, chain, ctr_inc, nullptr, flag, seq);
 }
 
 __global__ void advance_kernel(const ModelConst mc, StepInput* __restrict__ in, const StepOutput* __restrict__ out) {
@@ -1747,6 +1750,9 @@ static bool merge_stage_fits(int nrec_block, int rec_stride, int P, int K, size_
 void merge_prepare() {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&merge_kernel<MERGE_STAGE_THREADS, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)MERGE_LDS_DYN_MAX);
+    // its static LDS holds both passes' arrays (11 KB): 16 KB less dynamic LDS (launch_merge_xchg)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&merge_xchg_kernel<MERGE_STAGE_THREADS, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(MERGE_LDS_DYN_MAX - 16 * 1024));
 }
 static int merge_fence_sys() {
     static const int knob = tune_knob("SRBD_MERGE_FENCE", 2);
@@ -1825,11 +1831,22 @@ void launch_xchg_probe(const XchgArgs& x, int* ok, hipStream_t s) {
 void launch_merge_xchg(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                        const float* noise, const XchgArgs& x, StepOutput* out, int chain, hipStream_t s, int ctr_inc,
                        Publish pub) {
-    size_t smem = merge_smem_bytes(nrec, mc.P, mc.K);
+    // the kernel holds both passes' static LDS (two merge_body instantiations), so the staged records
+    // get 16 KB less dynamic LDS than merge_kernel's
+    size_t smem = 0;
+    bool stage = merge_stage_fits(nrec, rec_stride, mc.P, mc.K, &smem);
+    if (stage && smem > MERGE_LDS_DYN_MAX - 16 * 1024) {
+        stage = false;
+        smem = merge_smem_bytes(nrec, mc.P, mc.K);
+    }
     const size_t smem2 = merge_smem_bytes(x.world, mc.P, mc.K);
     smem = smem > smem2 ? smem : smem2;
-    hipLaunchKernelGGL(merge_xchg_kernel, dim3(1), dim3(MERGE_THREADS), smem, s, mc, in, recs, nrec, rec_stride, noise,
-                       x, out, chain, chain ? ctr_inc : 0, pub.flag, pub.seq);
+    if (stage)
+        hipLaunchKernelGGL((merge_xchg_kernel<MERGE_STAGE_THREADS, true>), dim3(1), dim3(MERGE_STAGE_THREADS), smem, s,
+                           mc, in, recs, nrec, rec_stride, noise, x, out, chain, chain ? ctr_inc : 0, pub.flag, pub.seq);
+    else
+        hipLaunchKernelGGL((merge_xchg_kernel<MERGE_THREADS, false>), dim3(1), dim3(MERGE_THREADS), smem, s, mc, in,
+                           recs, nrec, rec_stride, noise, x, out, chain, chain ? ctr_inc : 0, pub.flag, pub.seq);
 }
 
 int tune_knob(const char* name, int dflt) {

@@ -16,6 +16,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "quadruped-pympc-tamols_amd")]
 import numpy as np  # noqa: E402
 
 from bench import make_cfg  # noqa: E402
+from quadruped_pympc_amd import _lib  # noqa: E402
 from quadruped_pympc_amd.sharded import ShardedSamplingMPC  # noqa: E402
 from quadruped_pympc_amd.synthetic import CONFIGS, inputs  # noqa: E402
 
@@ -29,7 +30,7 @@ def local_pair(steps=2000):
     from quadruped_pympc_amd import _lib
 
     w = CONFIGS["c2"]
-    ctxs = [_lib.Context(make_cfg(w, 2 * w.num_samples, r, 2, 0)) for r in range(2)]
+    ctxs = [_lib.Context(make_cfg(_lib, w, 2 * w.num_samples, r, 2, 0)) for r in range(2)]
     for cx in ctxs:
         cx.check(_lib.lib.srbd_xgmi_export(cx.h, (C.c_uint8 * 64)()), "export")
     arr = (C.c_void_p * 2)(*[cx.h.value for cx in ctxs])
@@ -78,7 +79,7 @@ def main():
                             device_id=torch.device("cuda", 0))
     w = CONFIGS["c2"]
     transport = sys.argv[1] if len(sys.argv) > 1 else "rccl"
-    mpc = ShardedSamplingMPC(make_cfg(w, w.num_samples, 0, 1, 0), 0, 1, 0, transport=transport)
+    mpc = ShardedSamplingMPC(make_cfg(_lib, w, w.num_samples, 0, 1, 0), 0, 1, 0, transport=transport)
     s, r, c = inputs(w, 0)
     best = np.zeros(mpc.P, np.float32)
     for k in range(20):
