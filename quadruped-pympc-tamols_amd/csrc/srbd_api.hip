@@ -115,6 +115,7 @@ struct srbd_ctx {
     bool armed = false;
     uint32_t arm_seq = 0;
     int arm_buf = 0, arm_nflags = 1;
+    bool arm_fused = true;  // the chain's draws were made ahead (fused); else its RNG kernel draws them
     uint64_t arm_seed = 0, arm_ctr = 0;
     std::chrono::steady_clock::time_point arm_t0;
     int64_t arm_served = 0, arm_cancelled = 0;
@@ -568,9 +569,11 @@ static int copy_out(srbd_ctx* c, float* best, float* sigma, srbd_result* out) {
     return SRBD_OK;
 }
 
-// Queue the next host step (draws for (seed, ctr) already in noise buffer `buf`) behind the work on
-// the stream, its copy kernel spinning on h_go (srbd_set_armed).
-static void arm_next(srbd_ctx* c, uint64_t seed, uint64_t ctr, int buf) {
+// Queue the next host step behind the work on the stream, its copy kernel spinning on h_go
+// (srbd_set_armed).  fused: the draws for (seed, ctr) are already in noise buffer `buf` (made by this
+// step's rollout launch), so only that call can be served; else the chain's RNG kernel draws into `buf`
+// keyed by the copied input's (seed, counter), so any device-draw call can be.
+static void arm_next(srbd_ctx* c, uint64_t seed, uint64_t ctr, int buf, bool fused = true) {
     std::lock_guard<std::mutex> lk(g_arm_mu);
     if (g_armed && g_armed != c) arm_cancel_locked(g_armed);
     uint32_t s = (c->seq + 1) & ~ARM_CANCEL;  // the cancel token is seq | ARM_CANCEL
@@ -579,8 +582,10 @@ static void arm_next(srbd_ctx* c, uint64_t seed, uint64_t ctr, int buf) {
     const size_t P4 = sizeof(float) * (size_t)c->mc.P;
     launch_arm_copy(c->d_go, s, c->arm_deadline_us * 100ull, c->d_in_host, c->d_in, offsetof(StepInput, best) + P4,
                     offsetof(StepInput, sigma), c->mc.method == SRBD_CEM_MPPI ? P4 : 0, c->stream);
-    c->arm_nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, true, Publish{c->d_flag, s},
+    if (!fused) launch_rng(c->mc, c->d_in, 0, 0, 1, 0, c->d_noise[buf], c->stream);
+    c->arm_nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fused, Publish{c->d_flag, s},
                                         c->d_costs_arm);
+    c->arm_fused = fused;
     c->armed = true;
     c->arm_seq = s;
     c->arm_buf = buf;
@@ -598,7 +603,8 @@ static bool arm_claim(srbd_ctx* c, const float* noise, uint64_t seed, uint64_t c
     if (!c->armed) return false;
     const double age_us =
         std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c->arm_t0).count();
-    if (!noise && seed == c->arm_seed && counter == c->arm_ctr && age_us < 0.5 * (double)c->arm_deadline_us) {
+    if (!noise && (!c->arm_fused || (seed == c->arm_seed && counter == c->arm_ctr)) &&
+        age_us < 0.5 * (double)c->arm_deadline_us) {
         c->armed = false;  // claimed: nobody cancels it now
         ++c->arm_served;
         if (g_armed == c) g_armed = nullptr;
@@ -622,7 +628,7 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
         return fail(c, rc, "invalid step arguments");
     }
     c->h_in->noise_scaled = noise ? 1 : 0;
-    const bool want_arm = c->arm_mode && !noise && fusable(c);
+    const bool want_arm = c->arm_mode && !noise;
     int nflags = 1;
     uint32_t seq = 0;
     if (fire) {
@@ -631,10 +637,12 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
         nflags = c->arm_nflags;
         std::swap(c->d_costs, c->d_costs_arm);  // the fired run's costs
         c->cur = c->arm_buf;
-        c->pref_valid = true;
-        c->pref_buf = 1 - c->arm_buf;
-        c->pref_seed = seed;
-        c->pref_ctr = counter + 1;
+        c->pref_valid = c->arm_fused;
+        if (c->arm_fused) {
+            c->pref_buf = 1 - c->arm_buf;
+            c->pref_seed = seed;
+            c->pref_ctr = counter + 1;
+        }
     } else {
         if ((rc = upload_input(c))) return rc;
         int buf = 0;
@@ -653,13 +661,18 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
     }
     // arm the next step behind this one (its launches overlap this step's GPU time); with costs wanted
     // the copy-back goes first (it would queue behind the armed copy kernel)
-    if (want_arm && !out_costs && c->pref_valid) arm_next(c, seed, counter + 1, c->pref_buf);
+    // fused: the next step's draws are in pref_buf; unfused: the chain redraws into this step's buffer
+    auto arm = [&]() {
+        if (c->pref_valid) arm_next(c, seed, counter + 1, c->pref_buf, true);
+        else if (!fusable(c)) arm_next(c, seed, counter + 1, c->cur, false);
+    };
+    if (want_arm && !out_costs) arm();
     if ((rc = wait_published(c, seq, nflags))) return rc;
     if (out_costs) {
         HIP_TRY(c, hipMemcpyAsync(out_costs, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,
                                   c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
-        if (want_arm && c->pref_valid) arm_next(c, seed, counter + 1, c->pref_buf);
+        if (want_arm) arm();
     }
     c->input_ready = true;
     return copy_out(c, best, sigma, out);

@@ -90,6 +90,8 @@ def _same(a, b):
     ("c2", "random_sampling", "zero_order", 3001),
     ("c3", "cem_mppi", "cubic_spline", 4096),
     ("c2", "mppi", "linear_spline", 65536),
+    ("c2", "mppi", "zero_order", 131072),   # unfused draws: the armed chain carries the RNG kernel
+    ("c3", "cem_mppi", "cubic_spline", 70000),
 ])
 def test_armed_chain_bitwise(lib, wkey, method, par, N):
     """Consecutive counters: every step after the first is served by the armed chain."""
@@ -184,3 +186,13 @@ def test_armed_plugin_api_bitwise(lib):
             else:
                 np.testing.assert_array_equal(np.asarray(u, dtype=object if isinstance(u, (list, tuple)) else None),
                                               np.asarray(v, dtype=object if isinstance(v, (list, tuple)) else None))
+
+
+def test_armed_unfused_any_counter(lib):
+    """Unfused (N > 65 536): the armed chain draws for whatever (seed, counter) the call brings, so
+    counter jumps are served too; outputs equal the unarmed loop's."""
+    case = make_case("c2", N=131072, method="mppi")
+    script = [("step", c, False) for c in (3, 4, 9, 10, 40, 41, 42, 7)]
+    st = []
+    _same(_run(lib, case, script, armed=True, stats=st), _run(lib, case, script, armed=False))
+    assert st[0] == (7, 0), st
