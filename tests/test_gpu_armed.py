@@ -62,6 +62,8 @@ def _run(lib, case, script, armed, deadline_us=0, stats=None):
                 outs.append(("costs", ctx.copy_costs()))
             elif kind == "terms":
                 ctx.set_cost_terms(*act[1])
+            elif kind == "gait":  # gait-adaptive sampling (device-drawn step frequencies)
+                ctx.set_gait(*act[1:])
             elif kind == "sleep":
                 time.sleep(act[1])
             elif kind == "state":
@@ -196,3 +198,16 @@ def test_armed_unfused_any_counter(lib):
     st = []
     _same(_run(lib, case, script, armed=True, stats=st), _run(lib, case, script, armed=False))
     assert st[0] == (7, 0), st
+
+
+def test_armed_gait_adaptive_bitwise(lib):
+    """Gait-adaptive sampling (srbd_set_gait, device-drawn frequencies): armed = unarmed bit for bit,
+    set_gait cancels the pending chain, the following steps are served again."""
+    case = make_case("c2", N=10000, method="mppi")
+    gait = ("gait", (0.1, 0.6, 0.6, 0.1), 0.02, 0.65, np.array((1.4, 2.0, 2.4), f32), None)
+    script = ([gait] + [("step", 20 + k, False) for k in range(6)]
+              + [("gait", (0.0, 0.5, 0.5, 0.0), 0.02, 0.65, np.array((1.4, 2.0, 2.4), f32), None)]
+              + [("step", 26 + k, k == 2) for k in range(5)])
+    st = []
+    _same(_run(lib, case, script, armed=True, stats=st), _run(lib, case, script, armed=False))
+    assert st[0] == (9, 1), st
