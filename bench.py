@@ -55,6 +55,9 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--armed", action="store_true", help="one GPU: time armed srbd_step calls (srbd_set_armed)")
+    ap.add_argument("--other-steps", type=int, default=2000,
+                    help="one GPU: steps of the other mode's sample (armed_step / unarmed_step; 0: skip, e.g. under "
+                         "rocprofv3 --pmc, whose serialised dispatch makes an armed copy kernel wait out its deadline)")
     ap.add_argument("--extras", type=int, default=200,
                     help="steps of the supplementary interface / TAMOLS latency probes (0: skip)")
     return ap.parse_args(argv)
@@ -324,17 +327,20 @@ def bench_single(_lib, w, args):
     if not lat:
         lat = list(t_us * 1e-6)
     # the other mode over a sample of the same loop
-    ctx.set_armed(not armed, 0)
-    n_other = max(200, min(args.steps, 2000))
-    o_us, best, state["sigma"] = ctx.bench_host_steps(states, refs, contacts, best, state["sigma"], 42, k, n_other)
-    k += n_other
+    other = None
+    if args.other_steps > 0:
+        ctx.set_armed(not armed, 0)
+        n_other = max(200, min(args.steps, args.other_steps))
+        o_us, best, state["sigma"] = ctx.bench_host_steps(states, refs, contacts, best, state["sigma"], 42, k,
+                                                          n_other)
+        k += n_other
+        o_us = o_us[min(20, n_other // 10):]
+        other = {"value": round(w.num_samples / (float(o_us.mean()) * 1e-6), 1),
+                 "ms_per_step": round(float(o_us.mean()) * 1e-3, 5),
+                 "p50_step_ms": round(float(np.percentile(o_us, 50)) * 1e-3, 4),
+                 "p99_step_ms": round(float(np.percentile(o_us, 99)) * 1e-3, 4), "steps": int(o_us.size)}
     served, cancelled = ctx.armed_stats()
     ctx.set_armed(False, 0)
-    o_us = o_us[min(20, n_other // 10):]
-    other = {"value": round(w.num_samples / (float(o_us.mean()) * 1e-6), 1),
-             "ms_per_step": round(float(o_us.mean()) * 1e-3, 5),
-             "p50_step_ms": round(float(np.percentile(o_us, 50)) * 1e-3, 4),
-             "p99_step_ms": round(float(np.percentile(o_us, 99)) * 1e-3, 4), "steps": int(o_us.size)}
     # the same steps through the Python ctypes wrapper (Context.step), for the binding's overhead
     py = []
     best = run_steps(step, ins, best, k, min(300, max(20, args.latency_steps // 4)), py)

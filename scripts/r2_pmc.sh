@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-/root/repo}
 cd "$R" || exit 1
 O=$R/gpurun_out; T=${1:-pmc}; mkdir -p $O
 export TMPDIR=/tmp
-ARGS="--steps 200 --warmup 5 --no-cpu-baseline --latency-steps 20 --device-steps 0"
+ARGS="--steps 200 --warmup 5 --no-cpu-baseline --latency-steps 20 --device-steps 0 --other-steps 0"
 pass() {  # name, counters, extra bench args
     local n=$1 c=$2; shift 2
     local t0=$(date +%s.%N)
