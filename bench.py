@@ -46,7 +46,7 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "ns"])
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="multi-GPU: rows per GPU fixed (weak) or total rows fixed (strong); default strong for c5")
     ap.add_argument("--transport", default="auto", choices=["auto", "xgmi", "rccl"])

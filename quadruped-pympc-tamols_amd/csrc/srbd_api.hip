@@ -98,6 +98,11 @@ struct srbd_ctx {
     size_t noise_rm_cap = 0;
     float* d_costs = nullptr;
     float* d_wrec = nullptr;
+    // in-launch group reduction of the block records (GroupArgs): gsize blocks per group, ngroups
+    // group records the merge reads; gsize 1: the merge reads the nblocks block records
+    int gsize = 1, ngroups = 0;
+    float* d_grec = nullptr;
+    uint32_t* d_gcnt = nullptr;
     float* d_part = nullptr;  // first-level merge partials (rank-record format)
     hipGraphExec_t g_dev2 = nullptr, g_dev1 = nullptr;
     float* d_ga_freq = nullptr;  // injected per-row step frequencies (gait-adaptive parity mode), ldn floats
@@ -386,6 +391,16 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
         return cleanup_fail("hipMalloc", e);
     if ((e = hipMalloc((void**)&c->d_wrec, sizeof(float) * (size_t)c->nblocks * c->wrec_stride)) != hipSuccess)
         return cleanup_fail("hipMalloc", e);
+    c->gsize = group_size(c->nblocks, c->wrec_stride, mc.method);
+    c->ngroups = (c->nblocks + c->gsize - 1) / c->gsize;
+    if (c->gsize > 1) {
+        if ((e = hipMalloc((void**)&c->d_grec, sizeof(float) * (size_t)c->ngroups * c->wrec_stride)) != hipSuccess)
+            return cleanup_fail("hipMalloc", e);
+        if ((e = hipMalloc((void**)&c->d_gcnt, sizeof(uint32_t) * (size_t)c->ngroups)) != hipSuccess)
+            return cleanup_fail("hipMalloc", e);
+        if ((e = hipMemsetAsync(c->d_gcnt, 0, sizeof(uint32_t) * (size_t)c->ngroups, c->stream)) != hipSuccess)
+            return cleanup_fail("hipMemset", e);
+    }
     {
         const int m = merge_partials(c->nblocks, false);  // the larger of the two partial counts
         if (m > 0 && (e = hipMalloc((void**)&c->d_part, sizeof(float) * (size_t)m * c->rrec_stride)) != hipSuccess)
@@ -420,6 +435,8 @@ extern "C" void srbd_destroy(srbd_ctx* c) {
     (void)hipFree(c->d_costs_arm);
     if (c->h_go) (void)hipHostFree(c->h_go);
     (void)hipFree(c->d_wrec);
+    (void)hipFree(c->d_grec);
+    (void)hipFree(c->d_gcnt);
     (void)hipFree(c->d_part);
     (void)hipFree(c->d_ga_freq);
     if (c->h_in) (void)hipHostFree(c->h_in);
@@ -517,6 +534,11 @@ static int upload_input(srbd_ctx* c) {
     return SRBD_OK;
 }
 
+// The records the merge reads: the group records when the rollout launch reduces its blocks in groups.
+static GroupArgs grp_of(const srbd_ctx* c) { return GroupArgs{c->d_grec, c->d_gcnt, c->gsize}; }
+static const float* merge_src(const srbd_ctx* c) { return c->gsize > 1 ? c->d_grec : c->d_wrec; }
+static int merge_nrec(const srbd_ctx* c) { return c->gsize > 1 ? c->ngroups : c->nblocks; }
+
 // Returns the number of merge blocks that publish (wait_published).
 static int enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput* out, int chain = 0,
                                int ctr_inc = 1, bool fuse_next = false, Publish pub = {nullptr, 0},
@@ -524,9 +546,8 @@ static int enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput
     const ModelConst& mc = c->mc;
     const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1};
     launch_rollout(mc, c->d_in, c->d_noise[buf], costs ? costs : c->d_costs, c->d_wrec, c->wrec_stride, c->mode,
-                   c->threads,
-                   c->stream, fuse_next ? &next : nullptr);
-    return launch_merge_tree(mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, c->d_noise[buf], c->d_part,
+                   c->threads, c->stream, fuse_next ? &next : nullptr, grp_of(c));
+    return launch_merge_tree(mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, c->d_noise[buf], c->d_part,
                              rank_out, out, chain, c->stream, ctr_inc, pub);
 }
 
@@ -1246,8 +1267,8 @@ static void enqueue_xchg_step(srbd_ctx* c, int buf, StepOutput* out, int chain, 
     const ModelConst& mc = c->mc;
     const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1};
     launch_rollout(mc, c->d_in, c->d_noise[buf], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
-                   c->stream, fuse_next ? &next : nullptr);
-    launch_merge_xchg(mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, c->d_noise[buf], c->xa, out, chain,
+                   c->stream, fuse_next ? &next : nullptr, grp_of(c));
+    launch_merge_xchg(mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, c->d_noise[buf], c->xa, out, chain,
                       c->stream, 1, pub);
 }
 
@@ -1534,12 +1555,12 @@ extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, 
     if (!rc)
         rc = timed([&] {
             launch_rollout(mc, c->d_in, c->d_noise[0], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
-                           c->stream);
+                           c->stream, nullptr, grp_of(c));
         }, rollout_us);
     if (!rc)
         rc = timed([&] {
-            launch_merge_tree(mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, c->d_noise[0], c->d_part, nullptr,
-                              c->d_out, 0, c->stream);
+            launch_merge_tree(mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, c->d_noise[0], c->d_part,
+                              nullptr, c->d_out, 0, c->stream);
         }, reduce_us);
     // the launch the step actually runs when fusion applies: rollout + the next step's draws
     if (fused_us) *fused_us = 0.0f;
@@ -1547,7 +1568,7 @@ extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, 
         const RngJob next{c->d_noise[1], 0, 0, 1, 1};
         rc = timed([&] {
             launch_rollout(mc, c->d_in, c->d_noise[0], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
-                           c->stream, &next);
+                           c->stream, &next, grp_of(c));
         }, fused_us);
     }
     if (!rc) rc = timed([&] { launch_empty(c->stream); }, floor_us);
@@ -1569,7 +1590,7 @@ extern "C" int srbd_debug_merge_phases(srbd_ctx* c, int32_t iters, float* out_us
     HIP_TRY(c, hipMemsetAsync(d, 0, 32 * sizeof(uint64_t), c->stream));
     double acc[24] = {};
     for (int i = 0; i < iters; ++i) {
-        launch_merge(c->mc, c->d_in, c->d_wrec, c->nblocks, c->wrec_stride, 0, c->d_noise[c->cur], nullptr,
+        launch_merge(c->mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, 0, c->d_noise[c->cur], nullptr,
                      c->d_out, 0, c->stream, d);
         uint64_t h[32];
         HIP_TRY(c, hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, c->stream));

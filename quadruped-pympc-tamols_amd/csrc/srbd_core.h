@@ -129,6 +129,24 @@ SRBD_HD float div_by(float x, float d, float r) {
 constexpr float THIRD = 0.3333333432674407958984375f;  // RN(1/3)
 SRBD_HD float div3(float x) { return div_by(x, 3.0f, THIRD); }
 
+// ---- rollout arithmetic (round 3): the reference's float32 operations in its order, except that
+// the three operations with a long correctly rounded sequence take their hardware forms, each within
+// a few ulp of the IEEE result (the parity contract is the tolerance against the C oracle, SURVEY
+// 8(c); every kernel -- thread, four-lane, gait-adaptive, merge tail -- calls these same helpers, so
+// the layouts still agree bit for bit):
+//   x / 3            -> x * RN(1/3)                       (<= 1 ulp)
+//   1 / d            -> v_rcp_f32                         (<= 1 ulp)
+//   sin(x), cos(x)   -> v_sin_f32 / v_cos_f32 of x / 2pi  (revolutions; no range reduction)
+// Measured on the C2 four-lane rollout: 262 -> see DESIGN.md VALU instructions per lane-step.
+SRBD_HD float third(float x) { return x * THIRD; }
+SRBD_HD float rcp_(float d) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_rcpf(d);
+#else
+    return 1.0f / d;
+#endif
+}
+
 // CMJ:67-91, entries divided by DET (IEEE reciprocal once, then Markstein per entry; falls back
 // to plain division when DET is not a comfortably normal number).
 SRBD_HD void inv3(const float A[9], float out[9]) {
@@ -163,9 +181,12 @@ SRBD_HD void skew_dot(const float v[3], const float f[3], float o[3]) {
     o[2] = (-v[1]) * f[0] + v[0] * f[1];
 }
 
+constexpr float INV_2PI = 0.15915493667125701904296875f;  // RN(1/(2 pi))
 SRBD_HD void sincos_(float x, float* s, float* c) {
 #ifdef __HIP_DEVICE_COMPILE__
-    sincosf(x, s, c);
+    const float t = x * INV_2PI;  // revolutions (v_sin/v_cos domain |t| <= 256: |x| <= 1608 rad)
+    *s = __builtin_amdgcn_sinf(t);
+    *c = __builtin_amdgcn_cosf(t);
 #else
     *s = sinf(x);
     *c = cosf(x);
@@ -182,9 +203,9 @@ SRBD_HD void euler_rate_coefs(int c, float sr, float cr, float sp, float cp, flo
     const float DET = a33 * a22 - a32 * a23;
     const float n1 = c == 0 ? a32 * a13 : (c == 1 ? a33 : -a32);
     const float n2 = c == 0 ? -(a22 * a13) : (c == 1 ? -a23 : a22);
-    const float r = 1.0f / DET;  // |DET| >= |cos(pitch)| / 2 >= 8e-10: see euler_rates
-    k1 = div_by(n1, DET, r);
-    k2 = div_by(n2, DET, r);
+    const float r = rcp_(DET);  // |DET| >= |cos(pitch)| / 2 >= 8e-10: see euler_rates
+    k1 = n1 * r;
+    k2 = n2 * r;
 }
 
 SRBD_HD float euler_rate_row(int c, float k1, float k2, float w0, float w1, float w2) {
@@ -195,29 +216,57 @@ SRBD_HD void euler_rates(float sr, float cr, float sp, float cp, float w0, float
     const float a13 = -sp, a22 = cr, a23 = cp * sr, a32 = -sr, a33 = cp * cr;
     const float DET = a33 * a22 - a32 * a23;
     const float n[6] = {a32 * a13, -(a22 * a13), a33, -a23, -a32, a22};
-    // Correctly rounded n / DET via the IEEE reciprocal and one Markstein step.  That needs 1/DET and
-    // the quotients to stay normal: DET = cp (cr^2 + sr^2), so |DET| >= |cos(pitch)| / 2, and over
-    // every finite float32 pitch |cos| >= 1.6e-9 (exhaustive search, attained at 7.73e28); a
-    // non-finite angle makes DET NaN, and NaN propagates to the cost either way.
+    // n / DET as n * rcp(DET) (rcp_: <= 1 ulp; the product <= 2 ulp from the IEEE quotient).  1/DET
+    // stays normal: DET = cp (cr^2 + sr^2), so |DET| >= |cos(pitch)| / 2, and over every finite
+    // float32 pitch |cos| >= 1.6e-9 (exhaustive search, attained at 7.73e28); a non-finite angle
+    // makes DET NaN, and NaN propagates to the cost either way.
     float k[6];
-    const float r = 1.0f / DET;
+    const float r = rcp_(DET);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) k[i] = div_by(n[i], DET, r);
+    for (int i = 0; i < 6; ++i) k[i] = n[i] * r;
     er[0] = euler_rate_row(0, k[0], k[1], w0, w1, w2);
     er[1] = euler_rate_row(1, k[2], k[3], w0, w1, w2);
     er[2] = euler_rate_row(2, k[4], k[5], w0, w1, w2);
 }
 
+// Model constants as the rollout reads them: straight from ModelConst (host, merge tail, four-lane
+// kernel), or from an LDS copy (thread kernel: read per step behind a scheduling barrier, so the ~50
+// uniform values are not all held in SGPRs across the unrolled horizon; see rollout_kernel).
+// LDS layout (KC_*): inv_m | inertia[9] | Iinv[9] | grf_min, grf_max, mu, neg_mu | Q[12] | ref[12] | feet[12]
+enum { KC_INVM = 0, KC_I = 1, KC_IINV = 10, KC_LIM = 20, KC_Q = 24, KC_REF = 36, KC_FEET = 48, KC_N = 60 };
+struct McConst {
+    const ModelConst& m;
+    SRBD_HD float inv_m() const { return m.inv_m; }
+    SRBD_HD const float* inertia() const { return m.inertia; }
+    SRBD_HD const float* Iinv() const { return m.Iinv; }
+    SRBD_HD float grf_min() const { return m.grf_min; }
+    SRBD_HD float grf_max() const { return m.grf_max; }
+    SRBD_HD float mu() const { return m.mu; }
+    SRBD_HD float neg_mu() const { return m.neg_mu; }
+};
+struct LdsConst {
+    const float* k;  // KC_* layout
+    SRBD_HD float inv_m() const { return k[KC_INVM]; }
+    SRBD_HD const float* inertia() const { return k + KC_I; }
+    SRBD_HD const float* Iinv() const { return k + KC_IINV; }
+    SRBD_HD float grf_min() const { return k[KC_LIM]; }
+    SRBD_HD float grf_max() const { return k[KC_LIM + 1]; }
+    SRBD_HD float mu() const { return k[KC_LIM + 2]; }
+    SRBD_HD float neg_mu() const { return k[KC_LIM + 3]; }
+};
+
 // Centroidal_Model_JAX.fd + integrate_jax (CMJ:93-174).  x: 12 evolving states, feet: 12
 // (constant over the rollout), F: 12 clipped foot forces, c: 4 contact flags.
-SRBD_HD void integrate(const ModelConst& mc, float x[12], const float feet[12], const float F[12], const float c[4],
-                       float dt) {
+template <class KC>
+SRBD_HD void integrate_k(const KC& kc, float x[12], const float feet[12], const float F[12], const float c[4],
+                         float dt) {
     float temp[3], lin_acc[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) temp[k] = F[k] * c[0] + F[3 + k] * c[1] + F[6 + k] * c[2] + F[9 + k] * c[3];
-    lin_acc[0] = mc.inv_m * temp[0] + 0.0f;
-    lin_acc[1] = mc.inv_m * temp[1] + 0.0f;
-    lin_acc[2] = mc.inv_m * temp[2] + (-9.81f);
+    const float inv_m = kc.inv_m();
+    lin_acc[0] = inv_m * temp[0] + 0.0f;
+    lin_acc[1] = inv_m * temp[1] + 0.0f;
+    lin_acc[2] = inv_m * temp[2] + (-9.81f);
 
     float sr, cr, sp, cp, sy, cy;
     sincos_(x[6], &sr, &cr);
@@ -246,16 +295,20 @@ SRBD_HD void integrate(const ModelConst& mc, float x[12], const float feet[12], 
                         sr * sp * cy - cr * sy, sr * sp * sy + cr * cy, sr * cp,
                         cr * sp * cy + sr * sy, cr * sp * sy - sr * cy, cr * cp};
     float Iw[3], wxIw[3], a1[3], Rt[3], a2[3];
-    mv3(mc.inertia, x + 9, Iw);
+    mv3(kc.inertia(), x + 9, Iw);
     skew_dot(x + 9, Iw, wxIw);
-    mv3(mc.Iinv, wxIw, a1);
+    mv3(kc.Iinv(), wxIw, a1);
     mv3(R, temp2, Rt);
-    mv3(mc.Iinv, Rt, a2);
+    mv3(kc.Iinv(), Rt, a2);
 
     const float d[12] = {x[3],  x[4],  x[5],  lin_acc[0],    lin_acc[1],    lin_acc[2],
                          er[0], er[1], er[2], -a1[0] + a2[0], -a1[1] + a2[1], -a1[2] + a2[2]};
 #pragma unroll
     for (int k = 0; k < 12; ++k) x[k] = x[k] + d[k] * dt;
+}
+SRBD_HD void integrate(const ModelConst& mc, float x[12], const float feet[12], const float F[12], const float c[4],
+                       float dt) {
+    integrate_k(McConst{mc}, x, feet, F, c, dt);
 }
 
 // NMPC:270-314: where(x > lo, x, lo) then where(x < hi, x, hi), so a NaN becomes the lower bound.
@@ -272,20 +325,26 @@ SRBD_HD float clamp_cs(float x, float lo, float hi) {
 #endif
 }
 
-SRBD_HD void clip_leg(const ModelConst& mc, float& fx, float& fy, float& fz) {
-    fz = clamp_cs(fz, mc.grf_min, mc.grf_max);
-    const float lo = mc.neg_mu * fz, hi = mc.mu * fz;
+template <class KC>
+SRBD_HD void clip_leg_k(const KC& kc, float& fx, float& fy, float& fz) {
+    fz = clamp_cs(fz, kc.grf_min(), kc.grf_max());
+    const float lo = kc.neg_mu() * fz, hi = kc.mu() * fz;
     fx = clamp_cs(fx, lo, hi);
     fy = clamp_cs(fy, lo, hi);
 }
+SRBD_HD void clip_leg(const ModelConst& mc, float& fx, float& fy, float& fz) { clip_leg_k(McConst{mc}, fx, fy, fz); }
 
 // Gravity compensation + contact mask (NMPC:377-402), then clip.
-SRBD_HD void shape_leg(const ModelConst& mc, float fref, float c, float& fx, float& fy, float& fz) {
+template <class KC>
+SRBD_HD void shape_leg_k(const KC& kc, float fref, float c, float& fx, float& fy, float& fz) {
     fz = fref + fz;
-    fx = div3(fx * c);
-    fy = div3(fy * c);
+    fx = third(fx * c);
+    fy = third(fy * c);
     fz = fz * c;
-    clip_leg(mc, fx, fy, fz);
+    clip_leg_k(kc, fx, fy, fz);
+}
+SRBD_HD void shape_leg(const ModelConst& mc, float fref, float c, float& fx, float& fy, float& fz) {
+    shape_leg_k(McConst{mc}, fref, c, fx, fy, fz);
 }
 
 // Opt-in cost terms of one step n (srbd_set_cost_terms), thread-per-sample layout: per component q
@@ -308,7 +367,7 @@ SRBD_HD void extra_cost_step(const ModelConst& mc, int n, const float F[12], con
                 term = term + (d * mc.cost_smooth) * d;
             }
             if (q < 2) {
-                const float pre = div3((q == 0 ? RX[leg] : RY[leg]) * c[leg]);
+                const float pre = third((q == 0 ? RX[leg] : RY[leg]) * c[leg]);
                 float v = fabsf(pre) - mc.mu * F[3 * leg + 2];
                 v = v > 0.0f ? v : 0.0f;
                 term = term + (v * mc.cost_cone) * v;

@@ -1,0 +1,537 @@
+// srbd_device.h -- device helpers shared by the rollout translation units (srbd_kernels.hip: RNG,
+// four-lane rollouts, merge; srbd_rollout_thread.hip: thread-per-sample rollouts).
+#pragma once
+
+#include <utility>
+
+#include "srbd_launch.h"
+
+namespace srbd {
+
+// Timeline probe (measurement build only, `make probe`): thread 0 of every rollout-launch block
+// stores s_memrealtime (100 MHz) at fixed points after draining its outstanding memory operations.
+#ifdef SRBD_ROLLOUT_STAMPS
+constexpr int RSTAMP_N = 6, RSTAMP_BLOCKS = 8192;
+__device__ uint64_t g_rstamp[RSTAMP_BLOCKS * RSTAMP_N];
+#define SRBD_RSTAMP(i)                                                                  \
+    do {                                                                                \
+        if (threadIdx.x == 0 && blockIdx.x < RSTAMP_BLOCKS) {                           \
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                 \
+            g_rstamp[blockIdx.x * RSTAMP_N + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                               \
+    } while (0)
+#else
+#define SRBD_RSTAMP(i) \
+    do {               \
+    } while (0)
+#endif
+
+// Per-step pointer of an unrolled horizon: the same address, passed through an empty asm that also
+// reads `dep` (a value the previous step computes part-way through), so the loads through it issue
+// during the previous step -- not hoisted to the top of the horizon, not merged with another step's
+// loads.  (An asm "memory" clobber does not do this: the step input and the noise are readonly
+// __restrict__ arguments, whose loads LLVM moves freely, and an asm without an input floats to the
+// top.  Hoisted, the step scalars and noise took 210 VGPRs + SGPR spills in the C5 thread rollout and
+// ~150 v_readlane per step in the cubic CEM kernel.)  Uniform loads stay scalar: nothing is clobbered.
+// The returned pointer is in the constant address space, so uniform loads through it stay scalar
+// (s_load); a generic pointer out of the asm would turn them into flat vector loads.  step_gptr: the
+// same in the global address space (per-lane loads).
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T* step_ptr(const T* p, float dep) {
+    auto q = (const __attribute__((address_space(4))) T*)p;
+    asm volatile("" : "+s"(q) : "v"(dep));
+    return q;
+}
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* step_gptr(const T* p, float dep) {
+    auto q = (const __attribute__((address_space(1))) T*)p;
+    asm volatile("" : "+s"(q) : "v"(dep));
+    return q;
+}
+// The same for a uniform integer (a load offset formed from it).
+__device__ __forceinline__ int step_int(int v, float dep) {
+    asm volatile("" : "+s"(v) : "v"(dep));
+    return v;
+}
+
+// ------------------------------------------------------------------ helpers
+// 64-bit wave minimum with DPP (row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15/31, gfx9
+// family), result read from lane 63.  All 64 lanes must be active.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)(uint32_t)v, CTRL, ROWMASK, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)(uint32_t)(v >> 32), CTRL, ROWMASK, 0xF, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return b < a ? b : a; }
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+    v = umin64(v, dpp_u64<0x111, 0xF>(v));
+    v = umin64(v, dpp_u64<0x112, 0xF>(v));
+    v = umin64(v, dpp_u64<0x114, 0xF>(v));
+    v = umin64(v, dpp_u64<0x118, 0xF>(v));
+    v = umin64(v, dpp_u64<0x142, 0xA>(v));
+    v = umin64(v, dpp_u64<0x143, 0xC>(v));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Block-wide min; every thread gets the result.  `red` holds blockDim/64 words.
+__device__ __forceinline__ uint64_t block_min_u64(uint64_t v, uint64_t* red) {
+    v = wave_min_u64(v);
+    const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    uint64_t r = red[0];
+    for (int i = 1; i < nw; ++i) r = red[i] < r ? red[i] : r;
+    return r;
+}
+
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        // one 32x32->64 multiply each (v_mad_u64_u32) instead of separate lo / hi multiplies
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        c[0] = n0;
+        c[1] = (uint32_t)p1;
+        c[2] = n2;
+        c[3] = (uint32_t)p0;
+    }
+}
+
+__device__ __forceinline__ float u01(uint32_t x) { return ((float)(x >> 8) + 0.5f) * 5.9604644775390625e-08f; }
+
+// Noise buffers hold unscaled CEM draws Z when they come from the device RNG (StepInput::noise_scaled
+// == 0): readers form the noise value Z * sigma_j.  Injected noise is stored as given.
+__device__ __forceinline__ bool zs_scaled(const ModelConst& mc, const StepInput* in) {
+    return mc.method == SRBD_CEM_MPPI && in->noise_scaled == 0;
+}
+
+constexpr uint64_t KEY_NONE = ~0ull;
+
+// Sorted (ascending) per-lane candidate list of at most KM keys; fully unrolled (registers only).
+template <int KM>
+__device__ __forceinline__ void lk_insert(uint64_t (&lk)[KM], uint64_t x) {
+#pragma unroll
+    for (int i = KM - 1; i >= 1; --i) lk[i] = (x < lk[i - 1]) ? lk[i - 1] : (x < lk[i] ? x : lk[i]);
+    lk[0] = x < lk[0] ? x : lk[0];
+}
+// K rounds of a wave-wide minimum over the lanes' list heads; the (unique) winning lane pops.
+template <int KM>
+__device__ __forceinline__ void wave_topk(uint64_t (&lk)[KM], int K, uint64_t* out) {
+    for (int e = 0; e < K; ++e) {
+        const uint64_t m = wave_min_u64(lk[0]);
+        const bool pop = lk[0] == m && m != KEY_NONE;
+#pragma unroll
+        for (int i = 0; i < KM - 1; ++i) lk[i] = pop ? lk[i + 1] : lk[i];
+        lk[KM - 1] = pop ? KEY_NONE : lk[KM - 1];
+        if ((threadIdx.x & 63) == 0) out[e] = m;
+    }
+}
+
+// ------------------------------------------------------------------ RNG
+// Noise row r (global), column j.  MPPI: sigma*Z(r-1, j); CEM: Z(r-1, j)*sigma_j; random sampling
+// (NMPC:647-677): rows 1..t sigma0*Z(r-1), rows t+1..2t sigma1*Z(r-1-t) (same draws: the reference
+// reuses one key, App. B #3), rows 2t+1..N-1 U(-s2, s2) from draw r-1-2t.  Row 0 is zero.
+// One item = (local row k, column quad q): one Philox4x32-10 call, two Box-Muller pairs.
+// Box-Muller on the hardware transcendentals: v_log_f32 (log2), v_sqrt_f32, and v_sin/v_cos_f32,
+// which take revolutions, i.e. sin/cos(2 pi ub) directly with no range reduction (ub in (0, 1)).
+// They differ from libm by a few ulp (the host oracle's draws agree to ~1e-6 relative).
+__device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
+    const float ua = u01(a), ub = u01(b);
+    const float rr = __builtin_amdgcn_sqrtf(-1.38629436112f * __builtin_amdgcn_logf(ua));  // -2 ln ua
+    z0 = rr * __builtin_amdgcn_cosf(ub);
+    z1 = rr * __builtin_amdgcn_sinf(ub);
+}
+
+__device__ __forceinline__ void rng_item(const ModelConst& mc, const float* __restrict__ sigma, uint32_t key0,
+                                         uint32_t key1, uint32_t c2, uint32_t c3, int k, int q,
+                                         float* __restrict__ noise) {
+    const int r = mc.row0 + k;
+    uint32_t d = (uint32_t)(r - 1);
+    float scale = mc.sigma_mppi;  // MPPI
+    bool uniform = false;
+    if (mc.method == SRBD_RANDOM_SAMPLING) {
+        const int t = mc.N / 3;
+        if (r <= t) {
+            scale = mc.sigma_rs[0];
+        } else if (r <= 2 * t) {
+            scale = mc.sigma_rs[1];
+            d = (uint32_t)(r - 1 - t);
+        } else {
+            uniform = true;
+            d = (uint32_t)(r - 1 - 2 * t);
+        }
+    }
+    uint32_t c[4] = {d, (uint32_t)q, c2, c3};
+    philox4x32_10(c, key0, key1);
+    float v[4];
+    if (uniform) {
+        const float s2 = mc.sigma_rs[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = u01(c[i]) * (2.0f * s2) - s2;
+    } else {
+        box_muller(c[0], c[1], v[0], v[1]);
+        box_muller(c[2], c[3], v[2], v[3]);
+        // CEM: the standard normals themselves (they do not depend on the step's sigma, so the next
+        // step's draws can be made early); every reader multiplies by sigma_j (zs_scale), the same
+        // float product Z * sigma the reference forms (NMPC:951-958)
+        if (mc.method != SRBD_CEM_MPPI) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = scale * v[i];
+        }
+    }
+    const size_t ldn = (size_t)mc.ldn;
+    float* __restrict__ o = noise + (size_t)(4 * q) * ldn + k;
+#pragma unroll
+    // Write-through (sc1) stores: the draws leave no dirty lines in the XCD L2s, so the end of the
+    // launch that makes them has nothing to write back (the next step reads them from memory on other
+    // XCDs anyway).  C2: 25.6 -> 24.1 us per step; the fused rollout launch 14.7 -> 14.2 us.
+    for (int i = 0; i < 4; ++i)  // row 0: the warm start itself
+        __hip_atomic_store(&o[i * ldn], r > 0 ? v[i] : 0.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Items (k, q) enumerated k-fastest so consecutive lanes store consecutive floats; the item index is
+// advanced incrementally (no per-item division).  P is a multiple of 12, so quads are whole.
+__device__ __forceinline__ void rng_items(const ModelConst& mc, const StepInput* __restrict__ in, const RngJob& job,
+                                          int first, int stride) {
+    uint64_t seed = job.seed, ctr = job.ctr;
+    if (job.dev_ctr) {
+        seed = ((uint64_t)in->seed_hi << 32) | in->seed_lo;
+        ctr = (((uint64_t)in->ctr_hi << 32) | in->ctr_lo) + (uint64_t)job.ctr_offset;
+    }
+    const int n = mc.n_local, nq = mc.P / 4;
+    int q = first / n, k = first - q * n;
+    const int sq = stride / n, sk = stride - sq * n;
+    while (q < nq) {
+        rng_item(mc, in->sigma, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ctr, (uint32_t)(ctr >> 32), k, q,
+                 job.noise);
+        k += sk;
+        q += sq;
+        if (k >= n) {
+            k -= n;
+            ++q;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ rollout
+// Compile-time chunk index of the linear/cubic spline (== max(where(n >= linspace(0,H,S+1))) for
+// integer n, NMPC:187-189).
+__host__ __device__ constexpr int chunk_index(int n, int H, int S) { return (n * S) / H; }
+
+template <int N>
+struct IntC {
+    static constexpr int value = N;
+};
+template <class F, int... Ns>
+__device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, Ns...>) {
+    (f(IntC<Ns>{}), ...);
+}
+
+// Record words are stored write-through (sc1: relaxed agent-scope atomic stores) and read back with sc1
+// loads by a group's last arriver (group_reduce): the hand-off form of MI355X_MICROARCH.md's table row 1
+// (every storing wave waits vmcnt(0), one lane per block adds to the group's counter after a barrier,
+// the workgroup whose add returns last loads).  A record the merge kernel reads after the launch needs
+// no more than the kernel boundary; the same stores serve both.
+__device__ __forceinline__ void st_rec(float* p, float v) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_rec(const float* p) {
+    return __uint_as_float(
+        __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// The group's last arriver merges the group's nb block records (blocks b0 .. b0 + nb - 1, in that order)
+// into grp.grecs[g], the same arithmetic as merge_body's rescaled sums: beta_g = min key (first row on
+// ties), scale_i = exp(-(m_i - beta_g)), sum_i scale_i s_i, sum_i scale_i v_i[j] in record order, and
+// the K smallest keys of the group (one wave's K-round DPP minimum over the records' sorted lists).  The
+// records are first copied into LDS with sc1 loads (all in flight together: one memory round trip; the
+// round-2 measurement of column-by-column sc1 loads cost up to 8 us per group at 64 records), then every
+// phase reads LDS.  group_size keeps nb * rec_stride <= GROUP_LDS_FLOATS.
+// All threads of the block call it after block_epilogue's stores.
+template <int KM>
+__device__ __forceinline__ void group_topk(const float* st, int rec_stride, int nb, int P, int K, uint64_t* out) {
+    const int lane = threadIdx.x & 63;
+    uint64_t lk[KM];
+    const float* R = st + (size_t)lane * rec_stride + REC_HDR + P;
+#pragma unroll
+    for (int q = 0; q < KM; ++q)
+        lk[q] = (lane < nb && q < K) ? ((uint64_t)__float_as_uint(R[2 * q + 1]) << 32) | __float_as_uint(R[2 * q])
+                                     : KEY_NONE;
+    wave_topk(lk, K, out);
+}
+
+__device__ __forceinline__ void group_reduce(const ModelConst& mc, const float* __restrict__ recs, int rec_stride,
+                                             const GroupArgs& grp, int nroll) {
+    __shared__ int last_sh;
+    __shared__ float st[GROUP_LDS_FLOATS];
+    __shared__ float sc_sh[GROUP_MAX];
+    __shared__ float gh_sh[2];  // beta_g, tag
+    __shared__ uint64_t gk_sh[MAXK + 1];
+    const int tid = threadIdx.x, T = blockDim.x;
+    const int g = (int)blockIdx.x / grp.gsize, b0 = g * grp.gsize;
+    const int nb = min(grp.gsize, nroll - b0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's record stores have completed
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(grp.cnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_sh = old == (uint32_t)(nb - 1);
+    }
+    __syncthreads();
+    if (!last_sh) return;
+    if (tid == 0) __hip_atomic_store(grp.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    {  // stage the nb consecutive records (sc1 loads, U per thread in flight)
+        constexpr int U = 16;
+        const int n = nb * rec_stride;
+        const float* src = recs + (size_t)b0 * rec_stride;
+        for (int i0 = 0; i0 < n; i0 += U * T) {
+            float v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * T + tid;
+                v[u] = i < n ? ld_rec(src + i) : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * T + tid;
+                if (i < n) st[i] = v[u];
+            }
+        }
+    }
+    __syncthreads();
+    const int P = mc.P, K = mc.K;
+    const bool rs = mc.method == SRBD_RANDOM_SAMPLING;
+    float* G = grp.grecs + (size_t)g * rec_stride;
+    if (tid < 64) {  // wave 0: headers, beta_g, scales, top-K
+        const float* R = st + (size_t)tid * rec_stride;
+        const bool have = tid < nb;
+        const float m = have ? R[0] : 0.0f;
+        const uint32_t row = have ? __float_as_uint(R[2]) : 0u;
+        const uint64_t key = have ? ((uint64_t)__float_as_uint(m) << 32) | row : KEY_NONE;
+        const uint64_t gk = wave_min_u64(key);
+        const float beta = __uint_as_float((uint32_t)(gk >> 32));
+        if (key == gk) gh_sh[1] = R[3];  // keys are unique: one writer
+        if (tid == 0) {
+            gh_sh[0] = beta;
+            gk_sh[MAXK] = gk;
+        }
+        if (have) sc_sh[tid] = rs ? 1.0f : expf(-1.0f * (m - beta));
+        if (K == 1) {
+            if (tid == 0) gk_sh[0] = gk;
+        } else if (K <= 10) {
+            group_topk<10>(st, rec_stride, nb, P, K, gk_sh);
+        } else {
+            group_topk<MAXK>(st, rec_stride, nb, P, K, gk_sh);
+        }
+    }
+    __syncthreads();
+    if (!rs) {  // column j < P: sum_i scale_i v_i[j]; column P: sum_i scale_i s_i (record order)
+        for (int j = tid; j <= P; j += T) {
+            const int off = j < P ? REC_HDR + j : 1;
+            float a = 0.0f;
+            for (int i = 0; i < nb; ++i) a = a + sc_sh[i] * st[(size_t)i * rec_stride + off];
+            G[off] = a;
+        }
+    }
+    if (tid == 0) {
+        G[0] = gh_sh[0];
+        if (rs) G[1] = 1.0f;
+        G[2] = __uint_as_float((uint32_t)gk_sh[MAXK]);
+        G[3] = gh_sh[1];
+    }
+    if (tid < K) {
+        const uint64_t kk = gk_sh[tid];
+        G[REC_HDR + P + 2 * tid] = __uint_as_float((uint32_t)kk);
+        G[REC_HDR + P + 2 * tid + 1] = __uint_as_float((uint32_t)(kk >> 32));
+    }
+}
+
+// Wave sum in a fixed DPP tree (row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15/31); the total
+// lands in lane 63.  All 64 lanes must be active.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_f32(float v) {
+    v = v + dpp_f32<0x111, 0xF>(v);
+    v = v + dpp_f32<0x112, 0xF>(v);
+    v = v + dpp_f32<0x114, 0xF>(v);
+    v = v + dpp_f32<0x118, 0xF>(v);
+    v = v + dpp_f32<0x142, 0xA>(v);
+    v = v + dpp_f32<0x143, 0xC>(v);
+    return v;
+}
+
+// The block record's weighted sums: v[j] = sum_k e_k noise_k[j] for the P columns and s = sum_k e_k (column
+// P), over the block's SPB samples (noise `base` = row 0 of the block, SoA [P][ldn]); e in e_sh[0..SPB).
+//  SPB = 64 (four-lane kernel, small thread blocks): thread j sums its column's 64 products in sample order,
+//   its 16 float4 loads in flight at once (one memory round trip, a 128-op dependent chain).
+//  SPB = 128 / 256 (thread kernel): that chain is 2-4x longer with 2-4 round trips (113 of the C5 rollout's
+//   176 us); instead wave w takes columns w, w + NW, ..., lane l reads samples SPL l .. SPL l + SPL - 1 of a
+//   column in one load, forms its SPL products in sample order and the wave adds the 64 partials in a fixed
+//   DPP tree; CB columns' loads are issued together.
+template <int SPL>
+__device__ __forceinline__ void block_wsum_tree(const ModelConst& mc, const StepInput* __restrict__ in,
+                                                const float* __restrict__ base, bool zs, const float* e_sh,
+                                                float* rec) {
+    constexpr int CB = SPL == 4 ? 8 : 12;  // columns per batch of loads
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, NW = blockDim.x >> 6;
+    const int P = mc.P;
+    const size_t ldn = (size_t)mc.ldn;
+    float e[SPL];
+#pragma unroll
+    for (int u = 0; u < SPL; ++u) e[u] = e_sh[SPL * lane + u];
+    for (int j0 = w; j0 <= P; j0 += CB * NW) {
+        float z[CB][SPL];
+#pragma unroll
+        for (int b = 0; b < CB; ++b) {
+            const int j = j0 + b * NW;
+            const float* col = base + (size_t)(j < P ? j : 0) * ldn + SPL * lane;
+            if constexpr (SPL == 4) {
+                const float4 v = *reinterpret_cast<const float4*>(col);
+                z[b][0] = v.x, z[b][1] = v.y, z[b][2] = v.z, z[b][3] = v.w;
+            } else {
+                const float2 v = *reinterpret_cast<const float2*>(col);
+                z[b][0] = v.x, z[b][1] = v.y;
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < CB; ++b) {
+            const int j = j0 + b * NW;
+            if (j > P) break;
+            float a;
+            if (j < P) {
+                const float sj = zs ? in->sigma[j] : 1.0f;  // x * 1 == x
+                a = e[0] * (z[b][0] * sj);
+#pragma unroll
+                for (int u = 1; u < SPL; ++u) a = a + e[u] * (z[b][u] * sj);
+            } else {
+                a = e[0];
+#pragma unroll
+                for (int u = 1; u < SPL; ++u) a = a + e[u];
+            }
+            a = wave_sum_f32(a);
+            if (lane == 63) st_rec(&rec[j < P ? REC_HDR + j : 1], a);
+        }
+    }
+}
+__device__ __forceinline__ void block_wsum(const ModelConst& mc, const StepInput* __restrict__ in, int SPB,
+                                           const float* __restrict__ base, bool zs, const float* e_sh, float* rec) {
+    if (SPB == 128) return block_wsum_tree<2>(mc, in, base, zs, e_sh, rec);
+    if (SPB == 256) return block_wsum_tree<4>(mc, in, base, zs, e_sh, rec);
+    const int tid = threadIdx.x, T = blockDim.x, P = mc.P;
+    const size_t ldn = (size_t)mc.ldn;
+    for (int j = tid; j <= P; j += T) {
+        float a = 0.0f;
+        if (j < P) {
+            const float4* row = reinterpret_cast<const float4*>(base + (size_t)j * ldn);
+            const float sj = zs ? in->sigma[j] : 1.0f;  // x * 1 == x
+#pragma unroll 16
+            for (int i = 0; i < SPB / 4; ++i) {
+                const float4 v = row[i];
+                a = a + e_sh[4 * i] * (v.x * sj);
+                a = a + e_sh[4 * i + 1] * (v.y * sj);
+                a = a + e_sh[4 * i + 2] * (v.z * sj);
+                a = a + e_sh[4 * i + 3] * (v.w * sj);
+            }
+            st_rec(&rec[REC_HDR + j], a);
+        } else {
+            for (int i = 0; i < SPB; ++i) a = a + e_sh[i];
+            st_rec(&rec[1], a);
+        }
+    }
+}
+
+// Per-block record (see srbd_core.h REC_*): min key, sum_k e_k, sum_k e_k * noise_k[j], top-K keys,
+// e_k = exp(-(c_k - m_b)).  SPB samples per block (multiple of 4); the thread owning sample `sib`
+// passes it (others pass sib = -1) with its `tag` (the gait-adaptive step frequency, else 0), which
+// the owner of the block's best row stores in the record header.  All threads of the block must call
+// this.
+__device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepInput* __restrict__ in, const int SPB,
+                                               int sib, bool valid, float cost, const float* __restrict__ noise,
+                                               float* __restrict__ recs, int rec_stride, float* e_sh, uint64_t* red,
+                                               uint64_t* elite_sh, bool cemt, float tag, const GroupArgs& grp,
+                                               int nroll) {
+    const int tid = threadIdx.x;
+    const int k0 = blockIdx.x * SPB;
+    const uint64_t key = (sib >= 0 && valid) ? cost_key(cost, (uint32_t)(mc.row0 + k0 + sib)) : ~0ull;
+    const uint64_t bkey = block_min_u64(key, red);
+    const float m = u2f((uint32_t)(bkey >> 32));
+    float* rec = recs + (size_t)blockIdx.x * rec_stride;
+    const int P = mc.P, K = mc.K;
+    if (tid == 0) elite_sh[0] = bkey;
+    uint64_t last = bkey;
+    for (int r = 1; r < K; ++r) {
+        const uint64_t cand = key > last ? key : ~0ull;
+        last = block_min_u64(cand, red);
+        if (tid == 0) elite_sh[r] = last;
+    }
+    SRBD_RSTAMP(3);
+    if (mc.method != SRBD_RANDOM_SAMPLING) {
+        if (sib >= 0) e_sh[sib] = valid ? expf(-1.0f * (cost - m)) : 0.0f;
+        __syncthreads();
+        const bool zs = cemt && zs_scaled(mc, in);
+        block_wsum(mc, in, SPB, noise + k0, zs, e_sh, rec);
+    }
+    __syncthreads();
+    SRBD_RSTAMP(4);
+    if (tid == 0) {
+        st_rec(&rec[0], m);
+        st_rec(&rec[2], u2f((uint32_t)bkey));
+        if (mc.method == SRBD_RANDOM_SAMPLING) st_rec(&rec[1], 1.0f);
+    }
+    if (sib >= 0 && key == bkey) st_rec(&rec[3], tag);  // keys are unique: exactly one writer
+    if (tid < K) {
+        const uint64_t kk = elite_sh[tid];
+        st_rec(&rec[REC_HDR + P + 2 * tid], u2f((uint32_t)kk));
+        st_rec(&rec[REC_HDR + P + 2 * tid + 1], u2f((uint32_t)(kk >> 32)));
+    }
+    if (grp.gsize > 1) group_reduce(mc, recs, rec_stride, grp, nroll);
+}
+
+// ---- gait-adaptive rollout (centroidal_nmpc_jax_gait_adaptive.py:326-501).
+// One thread per sample.  The sample's step frequency f is injected (ga_explicit) or drawn from the
+// per-call set with one Philox call on the sample's own counter lane (jax.random.choice, GA:692/836;
+// the threefry stream is not reproduced); its contact sequence is the JAX gait
+// generator's (periodic_gait_generator_jax.py:68-151) run from the caller's leg phases, kept as one
+// bit mask per leg; each leg's decode index counts its stance steps so far (n_, GA:339/353-356,
+// -1 before the first touchdown: jnp's negative index wraps to the leg's last parameter) with
+// horizon_leg = stance steps + 1 (GA:345-348); the cost gains (f - 1.3) * 100 * (f - 1.3) (GA:500).
+constexpr uint32_t GA_FREQ_LANE = 0x10000u;  // Philox counter word 1 of the frequency draw (noise uses < P/4)
+
+__device__ __forceinline__ float ga_sample_freq(const ModelConst& mc, const StepInput* __restrict__ in, int k) {
+    if (in->ga_explicit) return mc.ga_freq[k];
+    const uint64_t seed = ((uint64_t)in->seed_hi << 32) | in->seed_lo;
+    uint32_t c[4] = {(uint32_t)(mc.row0 + k), GA_FREQ_LANE, in->ctr_lo, in->ctr_hi};
+    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint32_t i = (uint32_t)(((uint64_t)c[0] * (uint32_t)in->ga_nfreq) >> 32);  // uniform in [0, n)
+    return in->ga_freqs[i];
+}
+
+// Per-leg contact masks of one sample (bit n = stance at step n), PGGJ:136-151 with run :68-89:
+// restart (t >= 1 -> 0), advance by pgg_dt * f (the product first), stance while t < duty.
+__device__ __forceinline__ void ga_contact_masks(const StepInput* __restrict__ in, int H, float f, uint32_t mask[4]) {
+    const float inc = in->ga_dt * f;
+    float t[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        t[l] = in->ga_timing[l];
+        mask[l] = 0u;
+    }
+    for (int n = 0; n < H; ++n)
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            t[l] = t[l] >= 1.0f ? 0.0f : t[l];
+            t[l] = t[l] + inc;
+            mask[l] |= (t[l] < in->ga_duty ? 1u : 0u) << n;
+        }
+}
+
+}  // namespace srbd

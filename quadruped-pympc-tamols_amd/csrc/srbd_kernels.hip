@@ -10,176 +10,11 @@
 //   merge_kernel      merges block (or rank) records: global argmin, MPPI/CEM softmax-weighted
 //                     update, CEM sigma, final GRF decode + predicted state
 //   advance_kernel    device-resident warm start for back-to-back steps (benchmark chain)
-#include <utility>
-
-#include "srbd_launch.h"
+#include "srbd_device.h"
 
 #include <cstdlib>
 
 namespace srbd {
-
-// Timeline probe (measurement build only, `make probe`): thread 0 of every rollout-launch block
-// stores s_memrealtime (100 MHz) at fixed points after draining its outstanding memory operations.
-#ifdef SRBD_ROLLOUT_STAMPS
-constexpr int RSTAMP_N = 6, RSTAMP_BLOCKS = 8192;
-__device__ uint64_t g_rstamp[RSTAMP_BLOCKS * RSTAMP_N];
-#define SRBD_RSTAMP(i)                                                                  \
-    do {                                                                                \
-        if (threadIdx.x == 0 && blockIdx.x < RSTAMP_BLOCKS) {                           \
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                 \
-            g_rstamp[blockIdx.x * RSTAMP_N + (i)] = __builtin_amdgcn_s_memrealtime(); \
-        }                                                                               \
-    } while (0)
-#else
-#define SRBD_RSTAMP(i) \
-    do {               \
-    } while (0)
-#endif
-
-// ------------------------------------------------------------------ helpers
-// 64-bit wave minimum with DPP (row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15/31, gfx9
-// family), result read from lane 63.  All 64 lanes must be active.
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)(uint32_t)v, CTRL, ROWMASK, 0xF, false);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)(uint32_t)(v >> 32), CTRL, ROWMASK, 0xF, false);
-    return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return b < a ? b : a; }
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-    v = umin64(v, dpp_u64<0x111, 0xF>(v));
-    v = umin64(v, dpp_u64<0x112, 0xF>(v));
-    v = umin64(v, dpp_u64<0x114, 0xF>(v));
-    v = umin64(v, dpp_u64<0x118, 0xF>(v));
-    v = umin64(v, dpp_u64<0x142, 0xA>(v));
-    v = umin64(v, dpp_u64<0x143, 0xC>(v));
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
-    return ((uint64_t)hi << 32) | lo;
-}
-
-// Block-wide min; every thread gets the result.  `red` holds blockDim/64 words.
-__device__ __forceinline__ uint64_t block_min_u64(uint64_t v, uint64_t* red) {
-    v = wave_min_u64(v);
-    const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[w] = v;
-    __syncthreads();
-    uint64_t r = red[0];
-    for (int i = 1; i < nw; ++i) r = red[i] < r ? red[i] : r;
-    return r;
-}
-
-__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        if (r) {
-            k0 += 0x9E3779B9u;
-            k1 += 0xBB67AE85u;
-        }
-        // one 32x32->64 multiply each (v_mad_u64_u32) instead of separate lo / hi multiplies
-        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
-        c[0] = n0;
-        c[1] = (uint32_t)p1;
-        c[2] = n2;
-        c[3] = (uint32_t)p0;
-    }
-}
-
-__device__ __forceinline__ float u01(uint32_t x) { return ((float)(x >> 8) + 0.5f) * 5.9604644775390625e-08f; }
-
-// Noise buffers hold unscaled CEM draws Z when they come from the device RNG (StepInput::noise_scaled
-// == 0): readers form the noise value Z * sigma_j.  Injected noise is stored as given.
-__device__ __forceinline__ bool zs_scaled(const ModelConst& mc, const StepInput* in) {
-    return mc.method == SRBD_CEM_MPPI && in->noise_scaled == 0;
-}
-
-// ------------------------------------------------------------------ RNG
-// Noise row r (global), column j.  MPPI: sigma*Z(r-1, j); CEM: Z(r-1, j)*sigma_j; random sampling
-// (NMPC:647-677): rows 1..t sigma0*Z(r-1), rows t+1..2t sigma1*Z(r-1-t) (same draws: the reference
-// reuses one key, App. B #3), rows 2t+1..N-1 U(-s2, s2) from draw r-1-2t.  Row 0 is zero.
-// One item = (local row k, column quad q): one Philox4x32-10 call, two Box-Muller pairs.
-// Box-Muller on the hardware transcendentals: v_log_f32 (log2), v_sqrt_f32, and v_sin/v_cos_f32,
-// which take revolutions, i.e. sin/cos(2 pi ub) directly with no range reduction (ub in (0, 1)).
-// They differ from libm by a few ulp (the host oracle's draws agree to ~1e-6 relative).
-__device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
-    const float ua = u01(a), ub = u01(b);
-    const float rr = __builtin_amdgcn_sqrtf(-1.38629436112f * __builtin_amdgcn_logf(ua));  // -2 ln ua
-    z0 = rr * __builtin_amdgcn_cosf(ub);
-    z1 = rr * __builtin_amdgcn_sinf(ub);
-}
-
-__device__ __forceinline__ void rng_item(const ModelConst& mc, const float* __restrict__ sigma, uint32_t key0,
-                                         uint32_t key1, uint32_t c2, uint32_t c3, int k, int q,
-                                         float* __restrict__ noise) {
-    const int r = mc.row0 + k;
-    uint32_t d = (uint32_t)(r - 1);
-    float scale = mc.sigma_mppi;  // MPPI
-    bool uniform = false;
-    if (mc.method == SRBD_RANDOM_SAMPLING) {
-        const int t = mc.N / 3;
-        if (r <= t) {
-            scale = mc.sigma_rs[0];
-        } else if (r <= 2 * t) {
-            scale = mc.sigma_rs[1];
-            d = (uint32_t)(r - 1 - t);
-        } else {
-            uniform = true;
-            d = (uint32_t)(r - 1 - 2 * t);
-        }
-    }
-    uint32_t c[4] = {d, (uint32_t)q, c2, c3};
-    philox4x32_10(c, key0, key1);
-    float v[4];
-    if (uniform) {
-        const float s2 = mc.sigma_rs[2];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = u01(c[i]) * (2.0f * s2) - s2;
-    } else {
-        box_muller(c[0], c[1], v[0], v[1]);
-        box_muller(c[2], c[3], v[2], v[3]);
-        // CEM: the standard normals themselves (they do not depend on the step's sigma, so the next
-        // step's draws can be made early); every reader multiplies by sigma_j (zs_scale), the same
-        // float product Z * sigma the reference forms (NMPC:951-958)
-        if (mc.method != SRBD_CEM_MPPI) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = scale * v[i];
-        }
-    }
-    const size_t ldn = (size_t)mc.ldn;
-    float* __restrict__ o = noise + (size_t)(4 * q) * ldn + k;
-#pragma unroll
-    // Write-through (sc1) stores: the draws leave no dirty lines in the XCD L2s, so the end of the
-    // launch that makes them has nothing to write back (the next step reads them from memory on other
-    // XCDs anyway).  C2: 25.6 -> 24.1 us per step; the fused rollout launch 14.7 -> 14.2 us.
-    for (int i = 0; i < 4; ++i)  // row 0: the warm start itself
-        __hip_atomic_store(&o[i * ldn], r > 0 ? v[i] : 0.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Items (k, q) enumerated k-fastest so consecutive lanes store consecutive floats; the item index is
-// advanced incrementally (no per-item division).  P is a multiple of 12, so quads are whole.
-__device__ __forceinline__ void rng_items(const ModelConst& mc, const StepInput* __restrict__ in, const RngJob& job,
-                                          int first, int stride) {
-    uint64_t seed = job.seed, ctr = job.ctr;
-    if (job.dev_ctr) {
-        seed = ((uint64_t)in->seed_hi << 32) | in->seed_lo;
-        ctr = (((uint64_t)in->ctr_hi << 32) | in->ctr_lo) + (uint64_t)job.ctr_offset;
-    }
-    const int n = mc.n_local, nq = mc.P / 4;
-    int q = first / n, k = first - q * n;
-    const int sq = stride / n, sk = stride - sq * n;
-    while (q < nq) {
-        rng_item(mc, in->sigma, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)ctr, (uint32_t)(ctr >> 32), k, q,
-                 job.noise);
-        k += sk;
-        q += sq;
-        if (k >= n) {
-            k -= n;
-            ++q;
-        }
-    }
-}
 
 __global__ void __launch_bounds__(256) rng_kernel(const ModelConst mc, const StepInput* __restrict__ in,
                                                   const RngJob job) {
@@ -201,312 +36,6 @@ __global__ void __launch_bounds__(256) transpose_kernel(const float* __restrict_
         const int col = by + i, row = bx + tx;
         if (col < P && row < n) dst[(size_t)col * ldn + row] = tile[tx][i];
     }
-}
-
-// ------------------------------------------------------------------ rollout
-// Compile-time chunk index of the linear/cubic spline (== max(where(n >= linspace(0,H,S+1))) for
-// integer n, NMPC:187-189).
-__host__ __device__ constexpr int chunk_index(int n, int H, int S) { return (n * S) / H; }
-
-template <int N>
-struct IntC {
-    static constexpr int value = N;
-};
-template <class F, int... Ns>
-__device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, Ns...>) {
-    (f(IntC<Ns>{}), ...);
-}
-
-// Per-block record (see srbd_core.h REC_*): min key, sum_k e_k, sum_k e_k * noise_k[j], top-K keys,
-// e_k = exp(-(c_k - m_b)).  SPB samples per block (multiple of 4); the thread owning sample `sib`
-// passes it (others pass sib = -1) with its `tag` (the gait-adaptive step frequency, else 0), which
-// the owner of the block's best row stores in the record header.  All threads of the block must call
-// this.
-__device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepInput* __restrict__ in, const int SPB,
-                                               int sib, bool valid, float cost, const float* __restrict__ noise,
-                                               float* __restrict__ recs, int rec_stride, float* e_sh, uint64_t* red,
-                                               uint64_t* elite_sh, bool cemt, float tag = 0.0f) {
-    const int tid = threadIdx.x, T = blockDim.x;
-    const int k0 = blockIdx.x * SPB;
-    const uint64_t key = (sib >= 0 && valid) ? cost_key(cost, (uint32_t)(mc.row0 + k0 + sib)) : ~0ull;
-    const uint64_t bkey = block_min_u64(key, red);
-    const float m = u2f((uint32_t)(bkey >> 32));
-    float* rec = recs + (size_t)blockIdx.x * rec_stride;
-    const int P = mc.P, K = mc.K;
-    if (tid == 0) elite_sh[0] = bkey;
-    uint64_t last = bkey;
-    for (int r = 1; r < K; ++r) {
-        const uint64_t cand = key > last ? key : ~0ull;
-        last = block_min_u64(cand, red);
-        if (tid == 0) elite_sh[r] = last;
-    }
-    SRBD_RSTAMP(3);
-    if (mc.method != SRBD_RANDOM_SAMPLING) {
-        if (sib >= 0) e_sh[sib] = valid ? expf(-1.0f * (cost - m)) : 0.0f;
-        __syncthreads();
-        const size_t ldn = (size_t)mc.ldn;
-        const float* base = noise + k0;
-        const bool zs = cemt && zs_scaled(mc, in);
-        for (int j = tid; j <= P; j += T) {
-            float a = 0.0f;
-            if (j < P) {
-                const float4* row = reinterpret_cast<const float4*>(base + (size_t)j * ldn);
-                const float sj = zs ? in->sigma[j] : 1.0f;  // x * 1 == x
-#pragma unroll 16
-                for (int i = 0; i < SPB / 4; ++i) {
-                    const float4 v = row[i];
-                    a = a + e_sh[4 * i] * (v.x * sj);
-                    a = a + e_sh[4 * i + 1] * (v.y * sj);
-                    a = a + e_sh[4 * i + 2] * (v.z * sj);
-                    a = a + e_sh[4 * i + 3] * (v.w * sj);
-                }
-                rec[REC_HDR + j] = a;
-            } else {
-                for (int i = 0; i < SPB; ++i) a = a + e_sh[i];
-                rec[1] = a;
-            }
-        }
-    }
-    __syncthreads();
-    SRBD_RSTAMP(4);
-    if (tid == 0) {
-        rec[0] = m;
-        rec[2] = u2f((uint32_t)bkey);
-        if (mc.method == SRBD_RANDOM_SAMPLING) rec[1] = 1.0f;
-    }
-    if (sib >= 0 && key == bkey) rec[3] = tag;  // keys are unique: exactly one writer
-    if (tid < K) {
-        const uint64_t kk = elite_sh[tid];
-        rec[REC_HDR + P + 2 * tid] = u2f((uint32_t)kk);
-        rec[REC_HDR + P + 2 * tid + 1] = u2f((uint32_t)(kk >> 32));
-    }
-}
-
-// One thread per sample.  Best throughput when samples fill the GPU (>= ~1 wave per SIMD).
-template <int KIND, int HT, int ST, bool CEMT, bool EXT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == SRBD_ZERO_ORDER ? 2 : 1))) rollout_kernel(const ModelConst mc, const StepInput* __restrict__ in,
-                                                      const float* __restrict__ noise, float* __restrict__ costs,
-                                                      float* __restrict__ recs, int rec_stride,
-    const RngJob next_rng, int nroll) {
-    // blocks past the rollout grid generate the next step's noise on the CUs the rollout leaves idle
-    if ((int)blockIdx.x >= nroll) {
-        rng_items(mc, in, next_rng, ((int)blockIdx.x - nroll) * (int)blockDim.x + (int)threadIdx.x,
-                  ((int)gridDim.x - nroll) * (int)blockDim.x);
-        return;
-    }
-    __shared__ float e_sh[256];
-    __shared__ uint64_t red[4];
-    __shared__ uint64_t elite_sh[MAXK];
-
-    constexpr bool CT = HT > 0 && (KIND == SRBD_ZERO_ORDER || ST > 0);  // compile-time shape
-    const int H = CT ? HT : mc.H;
-    const int S = CT ? ST : mc.S;
-    const int PL = CT ? (KIND == SRBD_ZERO_ORDER ? 3 * HT : (KIND == SRBD_LINEAR_SPLINE ? 3 * (ST + 1) : 12 * ST))
-                      : mc.PL;
-    const int tid = threadIdx.x, T = blockDim.x;
-    const int k = blockIdx.x * T + tid;  // local row (padded rows < ldn are readable zeros)
-    const bool valid = k < mc.n_local;
-    const size_t ldn = (size_t)mc.ldn;
-    const float* __restrict__ nz = noise + k;
-    const float* __restrict__ best = in->best;
-    const bool zs = CEMT && zs_scaled(mc, in);  // CEMT: CEM kernels only carry the scaling code
-
-    float x[12], feet[12];
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-        x[i] = in->state[i];
-        feet[i] = in->state[12 + i];
-    }
-    float cost3[3] = {0.0f, 0.0f, 0.0f};
-    float Fprev[12];  // EXT: opt-in cost terms (srbd_set_cost_terms), a separate instantiation so the
-                      // default horizon carries none of their code (a runtime test cost C3 17 %)
-    auto step = [&](const int n, auto EX) __attribute__((always_inline)) {
-        const float c[4] = {in->contact[0][n], in->contact[1][n], in->contact[2][n], in->contact[3][n]};
-        const float fref = in->fzref[n];
-        const int idx = CT && KIND != SRBD_ZERO_ORDER ? chunk_index(n, HT, ST) : mc.sidx[n];
-        float F[12], RX[4], RY[4];
-#pragma unroll
-        for (int leg = 0; leg < 4; ++leg) {
-            const int base = leg * PL;
-            auto acc = [&](int j) {
-                const float z = nz[(size_t)(base + j) * ldn];
-                return best[base + j] + (zs ? z * in->sigma[base + j] : z);
-            };
-            float fx, fy, fz;
-            decode_leg(KIND, H, S, idx, mc.sq[n], mc.somq[n], mc.sa[n], mc.sb[n], mc.sc[n], mc.sd[n], n, acc, fx,
-                       fy, fz);
-            RX[leg] = fx;
-            RY[leg] = fy;
-            shape_leg(mc, fref, c[leg], fx, fy, fz);
-            F[3 * leg] = fx;
-            F[3 * leg + 1] = fy;
-            F[3 * leg + 2] = fz;
-        }
-        integrate(mc, x, feet, F, c, mc.dts[n]);
-        // tracking cost (NMPC:451) per component: cost_c += ((t_p + t_v) + t_rpy) + t_omega
-        float t[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-            const float e = x[i] - in->ref[i];
-            t[i] = (e * mc.Q[i]) * e;
-        }
-#pragma unroll
-        for (int q = 0; q < 3; ++q) cost3[q] = cost3[q] + (((t[q] + t[3 + q]) + t[6 + q]) + t[9 + q]);
-        if constexpr (decltype(EX)::value) extra_cost_step(mc, n, F, RX, RY, c, fref, Fprev, cost3);
-    };
-    auto horizon = [&](auto EX) __attribute__((always_inline)) {
-        if constexpr (CT) {
-            unroll_seq([&](auto nc) { step(decltype(nc)::value, EX); },
-                       std::make_integer_sequence<int, (CT ? HT : 1)>{});
-        } else {
-            for (int n = 0; n < H; ++n) step(n, EX);
-        }
-    };
-    horizon(std::bool_constant<EXT>{});
-    float cost = (cost3[0] + cost3[1]) + cost3[2];
-    cost = cost + in->cost_feet;  // 0, or NaN when a foot term is non-finite (Q_feet = 0)
-    // NMPC:686-687
-    if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
-    if (valid && costs) costs[k] = cost;
-    block_epilogue(mc, in, T, tid, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh, CEMT);
-}
-
-// ---- gait-adaptive rollout (centroidal_nmpc_jax_gait_adaptive.py:326-501).
-// One thread per sample.  The sample's step frequency f is injected (ga_explicit) or drawn from the
-// per-call set with one Philox call on the sample's own counter lane (jax.random.choice, GA:692/836;
-// the threefry stream is not reproduced); its contact sequence is the JAX gait
-// generator's (periodic_gait_generator_jax.py:68-151) run from the caller's leg phases, kept as one
-// bit mask per leg; each leg's decode index counts its stance steps so far (n_, GA:339/353-356,
-// -1 before the first touchdown: jnp's negative index wraps to the leg's last parameter) with
-// horizon_leg = stance steps + 1 (GA:345-348); the cost gains (f - 1.3) * 100 * (f - 1.3) (GA:500).
-constexpr uint32_t GA_FREQ_LANE = 0x10000u;  // Philox counter word 1 of the frequency draw (noise uses < P/4)
-
-__device__ __forceinline__ float ga_sample_freq(const ModelConst& mc, const StepInput* __restrict__ in, int k) {
-    if (in->ga_explicit) return mc.ga_freq[k];
-    const uint64_t seed = ((uint64_t)in->seed_hi << 32) | in->seed_lo;
-    uint32_t c[4] = {(uint32_t)(mc.row0 + k), GA_FREQ_LANE, in->ctr_lo, in->ctr_hi};
-    philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-    const uint32_t i = (uint32_t)(((uint64_t)c[0] * (uint32_t)in->ga_nfreq) >> 32);  // uniform in [0, n)
-    return in->ga_freqs[i];
-}
-
-// Per-leg contact masks of one sample (bit n = stance at step n), PGGJ:136-151 with run :68-89:
-// restart (t >= 1 -> 0), advance by pgg_dt * f (the product first), stance while t < duty.
-__device__ __forceinline__ void ga_contact_masks(const StepInput* __restrict__ in, int H, float f, uint32_t mask[4]) {
-    const float inc = in->ga_dt * f;
-    float t[4];
-#pragma unroll
-    for (int l = 0; l < 4; ++l) {
-        t[l] = in->ga_timing[l];
-        mask[l] = 0u;
-    }
-    for (int n = 0; n < H; ++n)
-#pragma unroll
-        for (int l = 0; l < 4; ++l) {
-            t[l] = t[l] >= 1.0f ? 0.0f : t[l];
-            t[l] = t[l] + inc;
-            mask[l] |= (t[l] < in->ga_duty ? 1u : 0u) << n;
-        }
-}
-
-template <int KIND>
-__global__ void __launch_bounds__(256) rollout_ga_kernel(const ModelConst mc, const StepInput* __restrict__ in,
-                                                         const float* __restrict__ noise, float* __restrict__ costs,
-                                                         float* __restrict__ recs, int rec_stride,
-                                                         const RngJob next_rng, int nroll) {
-    if ((int)blockIdx.x >= nroll) {
-        rng_items(mc, in, next_rng, ((int)blockIdx.x - nroll) * (int)blockDim.x + (int)threadIdx.x,
-                  ((int)gridDim.x - nroll) * (int)blockDim.x);
-        return;
-    }
-    __shared__ float e_sh[256];
-    __shared__ uint64_t red[4];
-    __shared__ uint64_t elite_sh[MAXK];
-    const int H = mc.H, S = mc.S, PL = mc.PL;
-    const int tid = threadIdx.x, T = blockDim.x;
-    const int k = blockIdx.x * T + tid;  // rows >= n_local are padding (readable zeros)
-    const bool valid = k < mc.n_local;
-    const size_t ldn = (size_t)mc.ldn;
-    const float* __restrict__ nz = noise + k;
-    const float* __restrict__ best = in->best;
-
-    const float f = ga_sample_freq(mc, in, k);
-    uint32_t mask[4];
-    ga_contact_masks(in, H, f, mask);
-    float seg[4];  // horizon_leg / S (GA:200 / :223), IEEE division
-#pragma unroll
-    for (int l = 0; l < 4; ++l) seg[l] = ((float)__popc(mask[l]) + 1.0f) / (float)S;
-    int cnt[4] = {-1, -1, -1, -1};
-
-    float x[12], feet[12];
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-        x[i] = in->state[i];
-        feet[i] = in->state[12 + i];
-    }
-    float cost3[3] = {0.0f, 0.0f, 0.0f};
-    const bool extra = mc.cost_on != 0;  // opt-in cost terms (srbd_set_cost_terms)
-    float Fprev[12];
-    for (int n = 0; n < H; ++n) {
-        float c[4];
-#pragma unroll
-        for (int l = 0; l < 4; ++l) {
-            const uint32_t b = (mask[l] >> n) & 1u;
-            c[l] = b ? 1.0f : 0.0f;
-            cnt[l] += (int)b;
-        }
-        const float ns = ((c[0] + c[1]) + c[2]) + c[3];
-        const float fref = mc.fz_ns[(int)ns];
-        float F[12], RX[4], RY[4];
-#pragma unroll
-        for (int leg = 0; leg < 4; ++leg) {
-            const int base = leg * PL;
-            auto acc = [&](int j) {
-                j = j < 0 ? j + PL : j;
-                return best[base + j] + nz[(size_t)(base + j) * ldn];
-            };
-            const int st = cnt[leg];
-            int idx = 0;
-            float q = 0.0f, omq = 0.0f, a = 0.0f, bb = 0.0f, cc = 0.0f, d = 0.0f;
-            if (KIND != SRBD_ZERO_ORDER) {  // spline_coef of srbd_api.hip with (step, horizon_leg) per leg
-                for (int i = 0; i <= S; ++i)
-                    if (st >= in->ga_cb[i]) idx = i;
-                float tau = (float)st / seg[leg];
-                tau = tau - (float)idx;
-                q = tau / 1.0f;
-                omq = 1.0f - q;
-                a = 2.0f * q * q * q - 3.0f * q * q + 1.0f;
-                bb = (q * q * q - 2.0f * q * q + q) * 1.0f;
-                cc = -2.0f * q * q * q + 3.0f * q * q;
-                d = (q * q * q - q * q) * 1.0f;
-            }
-            float fx, fy, fz;
-            decode_leg(KIND, H, S, idx, q, omq, a, bb, cc, d, st, acc, fx, fy, fz);
-            RX[leg] = fx;
-            RY[leg] = fy;
-            shape_leg(mc, fref, c[leg], fx, fy, fz);
-            F[3 * leg] = fx;
-            F[3 * leg + 1] = fy;
-            F[3 * leg + 2] = fz;
-        }
-        integrate(mc, x, feet, F, c, mc.dts[n]);
-        float t[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-            const float e = x[i] - in->ref[i];
-            t[i] = (e * mc.Q[i]) * e;
-        }
-#pragma unroll
-        for (int q = 0; q < 3; ++q) cost3[q] = cost3[q] + (((t[q] + t[3 + q]) + t[6 + q]) + t[9 + q]);
-        if (extra) extra_cost_step(mc, n, F, RX, RY, c, fref, Fprev, cost3);
-    }
-    float cost = (cost3[0] + cost3[1]) + cost3[2];
-    cost = cost + in->cost_feet;
-    const float df = f - 1.3f;
-    cost = cost + (df * 100.0f) * df;  // GA:500
-    if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
-    if (valid && costs) costs[k] = cost;
-    block_epilogue(mc, in, T, tid, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh, false, f);
 }
 
 // ---- four lanes per sample: lane c in {0,1,2} owns component c (x, y, z) of every 3-vector of
@@ -557,7 +86,7 @@ struct QuadRB {
 __device__ __forceinline__ QuadRB quad_rb_prep(const QuadLane& L, float r, float w) {
     const int c = L.c;
     float sn, cs;
-    sincosf(r, &sn, &cs);
+    sincos_(r, &sn, &cs);
     const float sr = qp<QP_B0>(sn), cr = qp<QP_B0>(cs);
     const float sp = qp<QP_B1>(sn), cp = qp<QP_B1>(cs);
     const float sy = qp<QP_B2>(sn), cy = qp<QP_B2>(cs);
@@ -609,10 +138,10 @@ __device__ __forceinline__ float quad_cross(float vl, float fl) {
 }
 
 template <int KIND, int HT, int ST, bool CEMT, bool EXT>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) rollout_quad_kernel(const ModelConst mc, const StepInput* __restrict__ in,
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) rollout_quad_kernel(const ModelConst mc, const StepInput* __restrict__ in,
                                                            const float* __restrict__ noise, float* __restrict__ costs,
                                                            float* __restrict__ recs, int rec_stride,
-    const RngJob next_rng, int nroll) {
+    const RngJob next_rng, int nroll, const GroupArgs grp) {
     // blocks past the rollout grid generate the next step's noise on the CUs the rollout leaves idle
     SRBD_RSTAMP(0);
     if ((int)blockIdx.x >= nroll) {
@@ -678,7 +207,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
         for (int l = 0; l < 4; ++l) {
             const int jr = l * PL + (KIND == SRBD_CUBIC_SPLINE ? 10 * (i >> 2) + (i & 3) : i);  // row - cblk
             const float nzv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(nrs, voff, jr * mc.ldn * 4, 0));
-            pre[l][i] = bl[jr] + (zs ? nzv * sl[jr] : nzv);
+            if constexpr (CEMT) {  // unscaled CEM device draws: Z * sigma_j (z * 1 == z; the load unconditional)
+                const float sj = sl[jr];
+                pre[l][i] = bl[jr] + nzv * (zs ? sj : 1.0f);
+            } else {
+                pre[l][i] = bl[jr] + nzv;
+            }
         }
     };
     // Zero-order with the opt-in cost terms: a rolling window of PW slots (slot n + PW loads at step n)
@@ -692,11 +226,17 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
         for (int i = 0; i < PW; ++i) load_slot(i);
     }
 
+    float dep = p;  // step_ptr dependency: set part-way through each step
     auto step = [&](const int n, auto EX) __attribute__((always_inline)) {  // EX: as rollout_kernel
         if constexpr (CT && PW < NPRE)
             if (n + PW < NPRE) load_slot(n + PW);  // n is a compile-time constant here (unrolled horizon)
-        const float cl[4] = {in->contact[0][n], in->contact[1][n], in->contact[2][n], in->contact[3][n]};
-        const float fref = in->fzref[n];
+        // this step's scalars through step_ptr: loaded per step, not hoisted across the unrolled horizon
+        // (hoisted: SGPR spills to VGPR lanes, ~150 v_readlane per step in the cubic CEM kernel)
+        const auto is = step_ptr(in, dep);
+        const float cl[4] = {is->contact[0][n], is->contact[1][n], is->contact[2][n], is->contact[3][n]};
+        const float fref = is->fzref[n];
+        const float dt = mc.dts[n];
+        const float sq = mc.sq[n], somq = mc.somq[n], sa = mc.sa[n], sb = mc.sb[n], scc = mc.sc[n], sd = mc.sd[n];
         const int idx = CT && KIND != SRBD_ZERO_ORDER ? chunk_index(n, HT, ST) : mc.sidx[n];
         // force and torque sums in leg order (integrate(): temp = sum_i f_i c_i, temp2 = sum_i t_i c_i;
         // 0 + x == x).  No per-leg branch on the contact flags: the straight-line horizon schedules
@@ -720,18 +260,18 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
                 raw = P(n, n + c * H);
             } else if (KIND == SRBD_LINEAR_SPLINE) {
                 const int o = idx + c * (S + 1);
-                raw = mc.somq[n] * P(idx, o) + mc.sq[n] * P(idx + 1, o + 1);
+                raw = somq * P(idx, o) + sq * P(idx + 1, o + 1);
             } else {
                 const int o = 10 * idx + 4 * c;
                 const float p0 = P(4 * idx, o), p1 = P(4 * idx + 1, o + 1), p2 = P(4 * idx + 2, o + 2),
                             p3 = P(4 * idx + 3, o + 3);
                 const float phi = 0.5f * ((p2 - p1) + (p1 - p0));
                 const float phin = 0.5f * ((p3 - p2) + (p2 - p1));
-                raw = mc.sa[n] * p1 + mc.sb[n] * phi + mc.sc[n] * p2 + mc.sd[n] * phin;
+                raw = sa * p1 + sb * phi + scc * p2 + sd * phin;
             }
             // shape_leg / clip_leg, component-wise
             float zp = clamp_cs((fref + raw) * cl[l], mc.grf_min, mc.grf_max);
-            const float xy = div3(raw * cl[l]);
+            const float xy = third(raw * cl[l]);
             const float fz = qp<QP_B2>(c == 2 ? zp : xy);
             const float f = c == 2 ? fz : clamp_cs(xy, mc.neg_mu * fz, mc.mu * fz);
             temp = temp + f * cl[l];
@@ -753,7 +293,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
                 fprev[l] = f;
             }
         }
-        quad_rigid_body(mc, L, temp, temp2, mc.dts[n], p, v, r, w);
+        dep = temp2;  // the next step's scalar loads issue from here on (step_ptr)
+        quad_rigid_body(mc, L, temp, temp2, dt, p, v, r, w);
         // tracking cost (NMPC:451), accumulated per component lane: cost_c += ((tp + tv) + tr) + tw,
         // the three lanes summed once after the horizon (see rollout_kernel for the same order)
         const float ep = p - rp, ev = v - rv, er_ = r - rr, ew = w - rw;
@@ -783,7 +324,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) r
     if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
     if (valid && q4 == 0 && costs) costs[k] = cost;
     block_epilogue(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh,
-                   CEMT);
+                   CEMT, 0.0f, grp, nroll);
     SRBD_RSTAMP(5);
 }
 
@@ -796,7 +337,7 @@ template <int KIND, int HT>
 __global__ void __launch_bounds__(512) rollout_ga_quad_kernel(const ModelConst mc, const StepInput* __restrict__ in,
                                                               const float* __restrict__ noise,
                                                               float* __restrict__ costs, float* __restrict__ recs,
-                                                              int rec_stride, const RngJob next_rng, int nroll) {
+                                                              int rec_stride, const RngJob next_rng, int nroll, const GroupArgs grp) {
     if ((int)blockIdx.x >= nroll) {
         rng_items(mc, in, next_rng, ((int)blockIdx.x - nroll) * (int)blockDim.x + (int)threadIdx.x,
                   ((int)gridDim.x - nroll) * (int)blockDim.x);
@@ -888,7 +429,7 @@ __global__ void __launch_bounds__(512) rollout_ga_quad_kernel(const ModelConst m
                 }
             }
             const float zp = clamp_cs((fref + raw) * cl[l], mc.grf_min, mc.grf_max);
-            const float xy = div3(raw * cl[l]);
+            const float xy = third(raw * cl[l]);
             const float fz = qp<QP_B2>(c == 2 ? zp : xy);
             const float fo = c == 2 ? fz : clamp_cs(xy, mc.neg_mu * fz, mc.mu * fz);
             temp = temp + fo * cl[l];
@@ -906,7 +447,7 @@ __global__ void __launch_bounds__(512) rollout_ga_quad_kernel(const ModelConst m
     if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
     if (valid && q4 == 0 && costs) costs[k] = cost;
     block_epilogue(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh,
-                   false, f);
+                   false, f, grp, nroll);
 }
 
 // ------------------------------------------------------------------ merge
@@ -924,28 +465,6 @@ constexpr int MERGE_RPT = 8;    // record headers per thread (nrec <= MERGE_RPT 
 #ifndef MERGE_STAGE_THREADS
 #define MERGE_STAGE_THREADS 512
 #endif
-constexpr uint64_t KEY_NONE = ~0ull;
-
-// Sorted (ascending) per-lane candidate list of at most KM keys; fully unrolled (registers only).
-template <int KM>
-__device__ __forceinline__ void lk_insert(uint64_t (&lk)[KM], uint64_t x) {
-#pragma unroll
-    for (int i = KM - 1; i >= 1; --i) lk[i] = (x < lk[i - 1]) ? lk[i - 1] : (x < lk[i] ? x : lk[i]);
-    lk[0] = x < lk[0] ? x : lk[0];
-}
-// K rounds of a wave-wide minimum over the lanes' list heads; the (unique) winning lane pops.
-template <int KM>
-__device__ __forceinline__ void wave_topk(uint64_t (&lk)[KM], int K, uint64_t* out) {
-    for (int e = 0; e < K; ++e) {
-        const uint64_t m = wave_min_u64(lk[0]);
-        const bool pop = lk[0] == m && m != KEY_NONE;
-#pragma unroll
-        for (int i = 0; i < KM - 1; ++i) lk[i] = pop ? lk[i + 1] : lk[i];
-        lk[KM - 1] = pop ? KEY_NONE : lk[KM - 1];
-        if ((threadIdx.x & 63) == 0) out[e] = m;
-    }
-}
-
 // Block-wide K smallest record keys (ascending) into `elite`, K <= KM: every thread's list starts as
 // its first record's keys (a record's keys ascend already), later records insert; per-wave K-round
 // minima; then one wave over the MERGE_WAVES wave lists.  Caller syncs afterwards.
@@ -1382,7 +901,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
             for (int l = 0; l < 4; ++l) {
                 const float cl = tail_pre[1 + l];
                 const float zp = clamp_cs((tail_pre[0] + raw[l]) * cl, gmin, gmax);
-                const float xy = div3(raw[l] * cl);
+                const float xy = third(raw[l] * cl);
                 const float fz = qp<QP_B2>(c == 2 ? zp : xy);
                 f[l] = c == 2 ? fz : clamp_cs(xy, neg_mu * fz, mu * fz);
             }
@@ -1589,7 +1108,8 @@ __global__ void div_selftest_kernel(const float* a, const float* b, int n, float
 // ------------------------------------------------------------------ launchers
 template <int KIND, int HT, int ST, bool EXT = false>
 static void launch_rollout_t(const ModelConst& mc, const StepInput* in, const float* noise, float* costs,
-                             float* recs, int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next) {
+                             float* recs, int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next,
+                             const GroupArgs& grp) {
     const RngJob job = next ? *next : RngJob{nullptr, 0, 0, 0, 0};
     const int extra = next ? (rng_grid(mc) < 1024 ? rng_grid(mc) : 1024) : 0;
     const bool cem = mc.method == SRBD_CEM_MPPI;
@@ -1599,21 +1119,12 @@ static void launch_rollout_t(const ModelConst& mc, const StepInput* in, const fl
         const dim3 grid(blocks + extra * 256 / threads);
         if (cem)
             hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, true, EXT>), grid, dim3(threads), 0, s, mc, in, noise,
-                               costs, recs, rec_stride, job, blocks);
+                               costs, recs, rec_stride, job, blocks, grp);
         else
             hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, EXT>), grid, dim3(threads), 0, s, mc, in, noise,
-                               costs, recs, rec_stride, job, blocks);
+                               costs, recs, rec_stride, job, blocks, grp);
     } else {
-        const int blocks = (mc.n_local + threads - 1) / threads;
-        const dim3 grid(blocks + extra * (256 / threads));
-        // thread form with the cost terms: runtime shapes only (the four-lane kernel is the default)
-        constexpr int HTT = EXT ? 0 : HT, STT = EXT ? 0 : ST;
-        if (cem)
-            hipLaunchKernelGGL((rollout_kernel<KIND, HTT, STT, true, EXT>), grid, dim3(threads), 0, s, mc, in, noise,
-                               costs, recs, rec_stride, job, blocks);
-        else
-            hipLaunchKernelGGL((rollout_kernel<KIND, HTT, STT, false, EXT>), grid, dim3(threads), 0, s, mc, in, noise,
-                               costs, recs, rec_stride, job, blocks);
+        launch_rollout_thread(mc, in, noise, costs, recs, rec_stride, threads, s, next, grp);
     }
 }
 
@@ -1624,7 +1135,8 @@ bool rollout_specialised(int kind, int H, int S) {
 
 // Same samples per block as the context's rollout mode (the merge reads one record per block).
 static void launch_rollout_ga(const ModelConst& mc, const StepInput* in, const float* noise, float* costs,
-                              float* recs, int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next) {
+                              float* recs, int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next,
+                              const GroupArgs& grp) {
     const RngJob job = next ? *next : RngJob{nullptr, 0, 0, 0, 0};
     const int extra = next ? (rng_grid(mc) < 1024 ? rng_grid(mc) : 1024) : 0;
     const int spb = mode == ROLLOUT_QUAD ? threads / 4 : threads;
@@ -1634,7 +1146,7 @@ static void launch_rollout_ga(const ModelConst& mc, const StepInput* in, const f
 #define SRBD_GQ(K, HH)                                                                                            \
     {                                                                                                              \
         hipLaunchKernelGGL((rollout_ga_quad_kernel<K, HH>), grid, block, 0, s, mc, in, noise, costs, recs, rec_stride, \
-                           job, blocks);                                                                           \
+                           job, blocks, grp);                                                                           \
         return;                                                                                                    \
     }
         const int H = mc.H;
@@ -1655,29 +1167,21 @@ static void launch_rollout_ga(const ModelConst& mc, const StepInput* in, const f
         }
 #undef SRBD_GQ
     }
-    const dim3 grid(blocks + extra * 256 / spb), block(spb);
-    if (mc.kind == SRBD_ZERO_ORDER)
-        hipLaunchKernelGGL((rollout_ga_kernel<SRBD_ZERO_ORDER>), grid, block, 0, s, mc, in, noise, costs, recs,
-                           rec_stride, job, blocks);
-    else if (mc.kind == SRBD_LINEAR_SPLINE)
-        hipLaunchKernelGGL((rollout_ga_kernel<SRBD_LINEAR_SPLINE>), grid, block, 0, s, mc, in, noise, costs, recs,
-                           rec_stride, job, blocks);
-    else
-        hipLaunchKernelGGL((rollout_ga_kernel<SRBD_CUBIC_SPLINE>), grid, block, 0, s, mc, in, noise, costs, recs,
-                           rec_stride, job, blocks);
+    launch_rollout_ga_thread(mc, in, noise, costs, recs, rec_stride, spb, s, next, grp);
 }
 
 void launch_rollout(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
-                    int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next) {
-    if (mc.ga) return launch_rollout_ga(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next);
+                    int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next, const GroupArgs& grp) {
+    if (mc.ga) return launch_rollout_ga(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next, grp);
     const int H = mc.H, S = mc.S;
     // the opt-in cost terms (mc.cost_on): the EXT instantiations, on the same compile-time shapes (with
     // each step's terms pinned to their step they no longer spill: C2 24.6 vs 23.3 us/step without the
     // terms, C3 cubic H16 N=10 000 48.8 vs 47.3; the runtime-shape form took 68.7)
 #define SRBD_LR(K, HH, SS)                                                                                        \
     return mc.cost_on                                                                                             \
-               ? launch_rollout_t<K, HH, SS, true>(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next) \
-               : launch_rollout_t<K, HH, SS, false>(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next)
+               ? launch_rollout_t<K, HH, SS, true>(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next, \
+                                                   grp)                                                           \
+               : launch_rollout_t<K, HH, SS, false>(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next, grp)
     switch (mc.kind) {
         case SRBD_ZERO_ORDER:
             if (H == 10) SRBD_LR(SRBD_ZERO_ORDER, 10, 0);
@@ -1694,6 +1198,18 @@ void launch_rollout(const ModelConst& mc, const StepInput* in, const float* nois
             SRBD_LR(SRBD_CUBIC_SPLINE, 0, 0);
     }
 #undef SRBD_LR
+}
+
+int group_size(int nblocks, int rec_stride, int method) {
+    const int knob = tune_knob("SRBD_GROUP_SIZE", 0);  // read per context (tests vary it)
+    // measured (round 3, r3e): the group hand-off adds ~2-3 us to the rollout launch and saves 1.7 us of merge
+    // at C2 (157 blocks), 4.8 at N = 65 536 (1024 blocks), 6 at C5 (2048); CEM's group top-K adds ~8 us at C3
+    const bool use = method != SRBD_CEM_MPPI && nblocks >= GROUP_MIN_BLOCKS;
+    int g = knob > 0 ? knob : (use ? (nblocks + GROUP_TARGET - 1) / GROUP_TARGET : 1);
+    const int cap = GROUP_LDS_FLOATS / rec_stride;  // the last arriver's LDS copy of its group's records
+    g = g > cap ? cap : g;
+    g = g > GROUP_MAX ? GROUP_MAX : g;
+    return g < 1 ? 1 : g;
 }
 
 int rng_grid(const ModelConst& mc) {

@@ -17,6 +17,24 @@ struct RngJob {
 };
 int rng_grid(const ModelConst& mc);
 
+// In-launch second reduction level of the rollout's block records.  Consecutive rollout blocks form
+// groups of `gsize`; every block publishes its record write-through and counts itself in cnt[group];
+// the group's last arriver merges the group's records (in block order) into grecs[group], a record of
+// the same format, so the merge kernel reads ceil(nblocks / gsize) records instead of nblocks.
+// gsize <= 1: no grouping (the merge reads the block records).
+constexpr int GROUP_MAX = 64;      // records one group merges (one wave's lanes hold their keys)
+constexpr int GROUP_TARGET = 32;   // groups per launch the sizing aims at (group_size)
+constexpr int GROUP_LDS_FLOATS = 6144;  // the last arriver stages its group's records in LDS (24 KB)
+constexpr int GROUP_MIN_BLOCKS = 512;   // grouping pays from here on (MPPI / random sampling)
+struct GroupArgs {
+    float* grecs;   // ngroups x rec_stride
+    uint32_t* cnt;  // ngroups arrival counters, zero between launches (each group's last arriver resets its own)
+    int gsize;      // blocks per group
+};
+// blocks per group for a launch of `nblocks` rollout blocks of `rec_stride`-float records (1: no grouping:
+// CEM, or fewer than GROUP_MIN_BLOCKS blocks); SRBD_GROUP_SIZE overrides (1 disables grouping)
+int group_size(int nblocks, int rec_stride, int method);
+
 // rollout variants: one thread per sample (block = `threads` samples) or four lanes per sample
 // (block = 256 threads = 64 samples)
 enum { ROLLOUT_THREAD = 0, ROLLOUT_QUAD = 1 };
@@ -24,7 +42,14 @@ bool rollout_specialised(int kind, int H, int S);
 // next != NULL: extra blocks of the same launch generate the next step's draws (RngJob) beside the
 // rollout, on the CUs it leaves idle.
 void launch_rollout(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
-                    int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next = nullptr);
+                    int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next = nullptr,
+                    const GroupArgs& grp = GroupArgs{nullptr, nullptr, 1});
+// the thread-per-sample forms (srbd_rollout_thread.hip): plain and gait-adaptive
+void launch_rollout_thread(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
+                           int rec_stride, int threads, hipStream_t s, const RngJob* next, const GroupArgs& grp);
+void launch_rollout_ga_thread(const ModelConst& mc, const StepInput* in, const float* noise, float* costs,
+                              float* recs, int rec_stride, int spb, hipStream_t s, const RngJob* next,
+                              const GroupArgs& grp);
 // Counter: `ctr` (host-known), or in->ctr + ctr_offset when dev_ctr != 0 (device-resident chain).
 void launch_rng(const ModelConst& mc, const StepInput* in, uint64_t seed, uint64_t ctr, int dev_ctr, int ctr_offset,
                 float* noise, hipStream_t s);

@@ -56,6 +56,8 @@ CONFIGS = {
     "c4": Workload("go2_stones_tamols_mppi_n10000_h12_zo", "go2", "trot", "mppi", "zero_order", 10000, 12,
                    terrain="stepping_stones_medium"),
     "c5": Workload("hyqreal1_bound_mppi_n524288_h12_zo", "hyqreal1", "bound", "mppi", "zero_order", 524288, 12),
+    # BASELINE.json north_star's target shape: MPPI, zero-order, N = 65 536, H = 12 on one MI355X
+    "ns": Workload("go2_trot_flat_mppi_n65536_h12_zo", "go2", "trot", "mppi", "zero_order", 65536, 12),
 }
 
 
