@@ -58,6 +58,8 @@ def parse_args(argv=None):
     ap.add_argument("--other-steps", type=int, default=2000,
                     help="one GPU: steps of the other mode's sample (armed_step / unarmed_step; 0: skip, e.g. under "
                          "rocprofv3 --pmc, whose serialised dispatch makes an armed copy kernel wait out its deadline)")
+    ap.add_argument("--targets", type=int, default=1000,
+                    help="one GPU, c2: steps of the supplementary north_star_65536 / c3 lines (0: skip)")
     ap.add_argument("--extras", type=int, default=200,
                     help="steps of the supplementary interface / TAMOLS latency probes (0: skip)")
     return ap.parse_args(argv)
@@ -150,6 +152,38 @@ def pmc_traffic(workload_name: str):
         return d.get(workload_name, {}).get("rollout_hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+
+
+def supplementary(_lib, key: str, steps: int, pmc_key=None):
+    """A target shape beside the headline line (one GPU): BASELINE north_star's MPPI ZO N=65 536 H=12
+    ("ns") or C3 (CEM cubic N=65 536 H=16).  Host-to-host srbd_step latencies timed from C, the device-
+    resident chain, per-kernel averages and the rollout roofline, measured as for the headline."""
+    import numpy as np
+
+    from quadruped_pympc_amd.synthetic import CONFIGS
+
+    w = CONFIGS[key]
+    ctx = _lib.Context(make_cfg(_lib, w, w.num_samples, 0, 1, 0))
+    ins = step_inputs(w, 32)
+    best = np.zeros(ctx.P, np.float32)
+    sigma = np.full(ctx.P, 3.0, np.float32) if w.method == "cem_mppi" else None
+    arrs = (np.stack([x[0] for x in ins]), np.stack([x[1] for x in ins]), np.stack([x[2] for x in ins]))
+    _, best, sigma = ctx.bench_host_steps(*arrs, best, sigma, 42, 0, 20)  # warm-up
+    t_us, best, sigma = ctx.bench_host_steps(*arrs, best, sigma, 42, 20, steps)
+    ctx.bench_device_steps(20)
+    ms = ctx.bench_device_steps(steps)
+    kern = ctx.time_kernels(200)
+    ctx.close()
+    return {"workload": w.name, "num_samples": w.num_samples, "horizon": w.horizon, "method": w.method,
+            "parametrization": w.parametrization,
+            "value": round(w.num_samples / (float(t_us.mean()) * 1e-6), 1), "unit": "rollouts/s",
+            "ms_per_step": round(float(t_us.mean()) * 1e-3, 5),
+            "p50_step_ms": round(float(np.percentile(t_us, 50)) * 1e-3, 4),
+            "p99_step_ms": round(float(np.percentile(t_us, 99)) * 1e-3, 4), "steps": int(t_us.size),
+            "device_chain": {"value": round(w.num_samples * steps / (ms * 1e-3), 1),
+                             "ms_per_step": round(ms / steps, 5), "steps": steps},
+            "kernels_us": {k: round(v, 3) for k, v in kern.items()},
+            "roofline": roofline(w, w.num_samples, kern, pmc_traffic(w.name))}
 
 
 def cpu_baseline(w, seconds: float):
@@ -494,6 +528,9 @@ def main(argv=None):
         line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
     else:
         line["cpu_baseline"] = None
+    if world == 1 and args.targets > 0 and args.config == "c2":  # the north-star shape and C3 beside the headline
+        line["north_star_65536"] = supplementary(_lib, "ns", args.targets)
+        line["c3"] = supplementary(_lib, "c3", args.targets)
     if world == 1 and args.extras and args.config in ("c2", "c4"):  # the callers either side of the path
         line["interface_step"] = interface_latency(w, args.extras)
         line["interface_step_armed"] = interface_latency(w, args.extras, armed=True)

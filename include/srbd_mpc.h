@@ -117,8 +117,10 @@ int srbd_step(srbd_ctx* ctx, const float* state, const float* ref, const float* 
  * (seed, counter + 1) -- behind itself; that chain's copy kernel waits (bounded by deadline_us, 0: 50 ms)
  * on a host-mapped word, and the next srbd_step stores its inputs and that word instead of launching.  A
  * call the chain cannot serve (injected noise, another counter or seed, past half the deadline) and every
- * other entry point cancel it: the cancelled chain recomputes the previous input into scratch buffers and
- * nothing a caller reads changes.  Outputs are bit-identical to unarmed steps.  One context per process
+ * other entry point cancel it: the cancelled chain computes nothing (its copy kernel writes its verdict
+ * to a device word every kernel of the chain checks first) and nothing a caller reads changes.  A claimed
+ * chain whose copy kernel had already given up (deadline passed before the go word) publishes a cancel
+ * token instead of outputs, and the call re-runs unarmed.  Outputs are bit-identical to unarmed steps.  One context per process
  * is armed at a time.  While armed, the copy kernel occupies its hardware queue (other streams of the
  * process that share that queue wait behind it, up to the deadline), hence opt-in: for a process whose
  * controller owns the GPU queue (the reference's 100 Hz MPC loop).  No reference counterpart (launch
@@ -126,6 +128,10 @@ int srbd_step(srbd_ctx* ctx, const float* state, const float* ref, const float* 
 int srbd_set_armed(srbd_ctx* ctx, int32_t enable, uint64_t deadline_us);
 /* Armed steps served (fired) and cancelled since the context was created. */
 int srbd_armed_stats(const srbd_ctx* ctx, int64_t* served, int64_t* cancelled);
+/* Claimed chains that had already given up and were re-run unarmed (counted as cancelled above). */
+int srbd_armed_refired(const srbd_ctx* ctx, int64_t* refired);
+/* Test hook: the host sleeps delay_us between claiming an armed chain and storing its go word. */
+int srbd_debug_arm_delay(srbd_ctx* ctx, uint32_t delay_us);
 
 /*
  * Gait-adaptive sampling (centroidal_nmpc_jax_gait_adaptive.py; replaces

@@ -14,6 +14,7 @@
 #include <chrono>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <rccl/rccl.h>  // types only: RCCL is dlopen'ed (the caller's copy, e.g. torch's)
@@ -116,6 +117,9 @@ struct srbd_ctx {
     uint64_t arm_deadline_us = 50000;
     uint32_t* h_go = nullptr;
     uint32_t* d_go = nullptr;
+    uint32_t* d_fired = nullptr;  // arm_copy_kernel's verdict for the chain behind it (Publish::gate)
+    int64_t arm_refired = 0;      // claimed chains whose copy had already given up: re-run unarmed
+    uint32_t arm_test_delay_us = 0;  // srbd_debug_arm_delay: host sleep between claim and go (tests only)
     float* d_costs_arm = nullptr;
     bool armed = false;
     uint32_t arm_seq = 0;
@@ -433,6 +437,7 @@ extern "C" void srbd_destroy(srbd_ctx* c) {
     (void)hipFree(c->d_noise_rm);
     (void)hipFree(c->d_costs);
     (void)hipFree(c->d_costs_arm);
+    (void)hipFree(c->d_fired);
     if (c->h_go) (void)hipHostFree(c->h_go);
     (void)hipFree(c->d_wrec);
     (void)hipFree(c->d_grec);
@@ -544,9 +549,11 @@ static int enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput
                                int ctr_inc = 1, bool fuse_next = false, Publish pub = {nullptr, 0},
                                float* costs = nullptr) {
     const ModelConst& mc = c->mc;
-    const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1};
+    const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1, pub.gate};
+    GroupArgs grp = grp_of(c);
+    grp.gate = pub.gate;
     launch_rollout(mc, c->d_in, c->d_noise[buf], costs ? costs : c->d_costs, c->d_wrec, c->wrec_stride, c->mode,
-                   c->threads, c->stream, fuse_next ? &next : nullptr, grp_of(c));
+                   c->threads, c->stream, fuse_next ? &next : nullptr, grp);
     return launch_merge_tree(mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, c->d_noise[buf], c->d_part,
                              rank_out, out, chain, c->stream, ctr_inc, pub);
 }
@@ -560,13 +567,27 @@ static bool published(const srbd_ctx* c, uint32_t seq, int nflags) {
     return true;
 }
 
-static int wait_published(srbd_ctx* c, uint32_t seq, int nflags = 1) {
+// cancelled != NULL (an armed chain): also accepts the chain's cancel token seq | ARM_CANCEL (it did not
+// fire, Publish::gate) and reports it there.
+static int wait_published(srbd_ctx* c, uint32_t seq, int nflags = 1, int* cancelled = nullptr) {
+    auto token = [&]() {
+        return cancelled && __atomic_load_n(c->h_flag, __ATOMIC_ACQUIRE) == (seq | ARM_CANCEL);
+    };
+    if (cancelled) *cancelled = 0;
     for (uint64_t it = 1;; ++it) {
         if (published(c, seq, nflags)) return SRBD_OK;
+        if (token()) {
+            *cancelled = 1;
+            return SRBD_OK;
+        }
         if ((it & 4095) == 0) {
             const hipError_t e = hipStreamQuery(c->stream);
             if (e == hipSuccess) {  // drained: the flag stores have completed
                 if (published(c, seq, nflags)) return SRBD_OK;
+                if (token()) {
+                    *cancelled = 1;
+                    return SRBD_OK;
+                }
                 return fail(c, SRBD_E_HIP, "step completed without publishing its outputs");
             }
             if (e != hipErrorNotReady) HIP_TRY(c, e);
@@ -601,10 +622,13 @@ static void arm_next(srbd_ctx* c, uint64_t seed, uint64_t ctr, int buf, bool fus
     if (s == 0) s = 1;
     c->seq = s;
     const size_t P4 = sizeof(float) * (size_t)c->mc.P;
+    // the age a claim checks runs from before the copy kernel can start waiting (its deadline counts from
+    // its own start, which is later), so a claim never sees a younger chain than the kernel does
+    c->arm_t0 = std::chrono::steady_clock::now();
     launch_arm_copy(c->d_go, s, c->arm_deadline_us * 100ull, c->d_in_host, c->d_in, offsetof(StepInput, best) + P4,
-                    offsetof(StepInput, sigma), c->mc.method == SRBD_CEM_MPPI ? P4 : 0, c->stream);
-    if (!fused) launch_rng(c->mc, c->d_in, 0, 0, 1, 0, c->d_noise[buf], c->stream);
-    c->arm_nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fused, Publish{c->d_flag, s},
+                    offsetof(StepInput, sigma), c->mc.method == SRBD_CEM_MPPI ? P4 : 0, c->d_fired, c->stream);
+    if (!fused) launch_rng(c->mc, c->d_in, 0, 0, 1, 0, c->d_noise[buf], c->stream, c->d_fired);
+    c->arm_nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fused, Publish{c->d_flag, s, c->d_fired},
                                         c->d_costs_arm);
     c->arm_fused = fused;
     c->armed = true;
@@ -612,7 +636,6 @@ static void arm_next(srbd_ctx* c, uint64_t seed, uint64_t ctr, int buf, bool fus
     c->arm_buf = buf;
     c->arm_seed = seed;
     c->arm_ctr = ctr;
-    c->arm_t0 = std::chrono::steady_clock::now();
     g_armed = c;
 }
 
@@ -652,7 +675,36 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
     const bool want_arm = c->arm_mode && !noise;
     int nflags = 1;
     uint32_t seq = 0;
+    // the unarmed launch of this call (also the fallback of a claimed chain that had already given up)
+    auto launch_unarmed = [&]() -> int {
+        int r;
+        if ((r = upload_input(c))) return r;
+        int buf = 0;
+        if ((r = acquire_noise(c, noise, seed, counter, &buf))) return r;
+        const bool fuse = !noise && fusable(c);
+        const Publish pub{c->d_flag, ++c->seq, nullptr};
+        seq = pub.seq;
+        nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fuse, pub);
+        HIP_TRY(c, hipGetLastError());
+        if (fuse) {
+            c->pref_valid = true;
+            c->pref_buf = 1 - buf;
+            c->pref_seed = seed;
+            c->pref_ctr = counter + 1;
+        }
+        return SRBD_OK;
+    };
+    // arm the next step behind this one (its launches overlap this step's GPU time); with costs wanted
+    // the copy-back goes first (it would queue behind the armed copy kernel)
+    // fused: the next step's draws are in pref_buf; unfused: the chain redraws into this step's buffer
+    auto arm = [&]() {
+        if (c->pref_valid) arm_next(c, seed, counter + 1, c->pref_buf, true);
+        else if (!fusable(c)) arm_next(c, seed, counter + 1, c->cur, false);
+    };
+    const int claimed_buf = c->arm_buf;
+    const bool claimed_fused = c->arm_fused;
     if (fire) {
+        if (c->arm_test_delay_us) std::this_thread::sleep_for(std::chrono::microseconds(c->arm_test_delay_us));
         __atomic_store_n(c->h_go, c->arm_seq, __ATOMIC_RELEASE);
         seq = c->arm_seq;
         nflags = c->arm_nflags;
@@ -664,31 +716,30 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
             c->pref_seed = seed;
             c->pref_ctr = counter + 1;
         }
-    } else {
-        if ((rc = upload_input(c))) return rc;
-        int buf = 0;
-        if ((rc = acquire_noise(c, noise, seed, counter, &buf))) return rc;
-        const bool fuse = !noise && fusable(c);
-        const Publish pub{c->d_flag, ++c->seq};
-        seq = pub.seq;
-        nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fuse, pub);
-        HIP_TRY(c, hipGetLastError());
-        if (fuse) {
-            c->pref_valid = true;
-            c->pref_buf = 1 - buf;
-            c->pref_seed = seed;
-            c->pref_ctr = counter + 1;
-        }
+    } else if ((rc = launch_unarmed())) {
+        return rc;
     }
-    // arm the next step behind this one (its launches overlap this step's GPU time); with costs wanted
-    // the copy-back goes first (it would queue behind the armed copy kernel)
-    // fused: the next step's draws are in pref_buf; unfused: the chain redraws into this step's buffer
-    auto arm = [&]() {
-        if (c->pref_valid) arm_next(c, seed, counter + 1, c->pref_buf, true);
-        else if (!fusable(c)) arm_next(c, seed, counter + 1, c->cur, false);
-    };
     if (want_arm && !out_costs) arm();
-    if ((rc = wait_published(c, seq, nflags))) return rc;
+    int cancelled = 0;
+    if ((rc = wait_published(c, seq, nflags, fire ? &cancelled : nullptr))) return rc;
+    if (cancelled) {
+        // The claimed chain had already given up (its copy kernel's deadline passed before the go word, e.g.
+        // this thread was preempted between the claim and the go store): it computed nothing and published
+        // its cancel token.  Undo the claim, cancel the chain just armed behind it, run the call unarmed --
+        // never the previous input's outputs (round-2 advisor finding).
+        std::swap(c->d_costs, c->d_costs_arm);
+        arm_cancel(c);
+        ++c->arm_refired;
+        --c->arm_served;  // counted as served at the claim
+        ++c->arm_cancelled;
+        c->pref_valid = claimed_fused;  // this call's draws are in the claimed chain's buffer
+        c->pref_buf = claimed_buf;
+        c->pref_seed = seed;
+        c->pref_ctr = counter;
+        if ((rc = launch_unarmed())) return rc;
+        if (want_arm && !out_costs) arm();
+        if ((rc = wait_published(c, seq, nflags))) return rc;
+    }
     if (out_costs) {
         HIP_TRY(c, hipMemcpyAsync(out_costs, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,
                                   c->stream));
@@ -712,8 +763,25 @@ extern "C" int srbd_set_armed(srbd_ctx* c, int32_t enable, uint64_t deadline_us)
         __atomic_store_n(c->h_go, 0u, __ATOMIC_RELEASE);
     }
     if (enable && !c->d_costs_arm) HIP_TRY(c, hipMalloc((void**)&c->d_costs_arm, sizeof(float) * c->mc.ldn));
+    if (enable && !c->d_fired) {
+        HIP_TRY(c, hipMalloc((void**)&c->d_fired, sizeof(uint32_t)));
+        HIP_TRY(c, hipMemset(c->d_fired, 0, sizeof(uint32_t)));
+    }
     c->arm_mode = enable ? 1 : 0;
     c->arm_deadline_us = deadline_us ? deadline_us : 50000;
+    return SRBD_OK;
+}
+
+extern "C" int srbd_armed_refired(const srbd_ctx* c, int64_t* refired) {
+    if (!c || !refired) return SRBD_E_INVALID;
+    std::lock_guard<std::mutex> lk(g_arm_mu);
+    *refired = c->arm_refired;
+    return SRBD_OK;
+}
+
+extern "C" int srbd_debug_arm_delay(srbd_ctx* c, uint32_t delay_us) {
+    if (!c) return SRBD_E_INVALID;
+    c->arm_test_delay_us = delay_us;
     return SRBD_OK;
 }
 
@@ -1666,7 +1734,8 @@ extern "C" int srbd_tamols_create(int32_t device_id, srbd_tamols_ctx** out) {
               hipHostGetDevicePointer((void**)&t->d_flag, t->h_flag, 0) == hipSuccess &&
               hipMalloc((void**)&t->d_part, sizeof(double) * 4 * TAMOLS_BPL * 4) == hipSuccess &&
               hipMalloc((void**)&t->d_cnt, sizeof(unsigned) * 8) == hipSuccess &&
-              hipMemset(t->d_cnt, 0, sizeof(unsigned) * 8) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+              hipMemset(t->d_cnt, 0, sizeof(unsigned) * 8) == hipSuccess && tamols_prepare() == 0 &&
+              hipDeviceSynchronize() == hipSuccess;
     if (!ok) {
         srbd_tamols_destroy(t);
         return fail(nullptr, SRBD_E_HIP, "TAMOLS context allocation failed");

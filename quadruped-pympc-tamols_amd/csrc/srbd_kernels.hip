@@ -18,6 +18,7 @@ namespace srbd {
 
 __global__ void __launch_bounds__(256) rng_kernel(const ModelConst mc, const StepInput* __restrict__ in,
                                                   const RngJob job) {
+    if (job.gate && (*job.gate & ARM_CANCEL)) return;  // armed chain that did not fire
     rng_items(mc, in, job, blockIdx.x * 256 + threadIdx.x, gridDim.x * 256);
 }
 
@@ -142,6 +143,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
                                                            const float* __restrict__ noise, float* __restrict__ costs,
                                                            float* __restrict__ recs, int rec_stride,
     const RngJob next_rng, int nroll, const GroupArgs grp) {
+    if (grp.gate && (*grp.gate & ARM_CANCEL)) return;  // armed chain that did not fire: nothing to compute
     // blocks past the rollout grid generate the next step's noise on the CUs the rollout leaves idle
     SRBD_RSTAMP(0);
     if ((int)blockIdx.x >= nroll) {
@@ -338,6 +340,7 @@ __global__ void __launch_bounds__(512) rollout_ga_quad_kernel(const ModelConst m
                                                               const float* __restrict__ noise,
                                                               float* __restrict__ costs, float* __restrict__ recs,
                                                               int rec_stride, const RngJob next_rng, int nroll, const GroupArgs grp) {
+    if (grp.gate && (*grp.gate & ARM_CANCEL)) return;  // armed chain that did not fire
     if ((int)blockIdx.x >= nroll) {
         rng_items(mc, in, next_rng, ((int)blockIdx.x - nroll) * (int)blockDim.x + (int)threadIdx.x,
                   ((int)gridDim.x - nroll) * (int)blockDim.x);
@@ -997,7 +1000,14 @@ __global__ void __launch_bounds__(NT) merge_kernel(const ModelConst mc, StepInpu
                                                               StepOutput* __restrict__ out, int chain,
                                                               int ctr_inc, uint64_t* __restrict__ dbg,
                                                               uint32_t* __restrict__ flag, uint32_t seq,
-                                                              int split_cs, int fence_sys) {
+                                                              int split_cs, int fence_sys,
+                                                              const uint32_t* __restrict__ gate) {
+    if (gate && (*gate & ARM_CANCEL)) {  // armed chain that did not fire (Publish::gate)
+        if (threadIdx.x == 0 && flag)
+            __hip_atomic_store(flag + (split_cs > 0 ? blockIdx.x : 0), seq | ARM_CANCEL, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
     merge_body<NT, STAGE>(mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag,
                       seq, split_cs, fence_sys);
 }
@@ -1219,8 +1229,8 @@ int rng_grid(const ModelConst& mc) {
 }
 
 void launch_rng(const ModelConst& mc, const StepInput* in, uint64_t seed, uint64_t ctr, int dev_ctr, int ctr_offset,
-                float* noise, hipStream_t s) {
-    const RngJob job{noise, seed, ctr, dev_ctr, ctr_offset};
+                float* noise, hipStream_t s, const uint32_t* gate) {
+    const RngJob job{noise, seed, ctr, dev_ctr, ctr_offset, gate};
     hipLaunchKernelGGL(rng_kernel, dim3(rng_grid(mc)), dim3(256), 0, s, mc, in, job);
 }
 
@@ -1277,17 +1287,18 @@ static int merge_fence_sys() {
 static void launch_merge_kernel(bool stage, dim3 grid, size_t smem, hipStream_t s, const ModelConst& mc,
                                 StepInput* in, const float* recs, int nrec, int rec_stride, int rows_in_rec,
                                 const float* noise, float* rank_out, StepOutput* out, int chain, int ctr_inc,
-                                uint64_t* dbg, uint32_t* flag, uint32_t seq, int split_cs) {
+                                uint64_t* dbg, uint32_t* flag, uint32_t seq, int split_cs,
+                                const uint32_t* gate = nullptr) {
     if (stage) {
         hipLaunchKernelGGL((merge_kernel<MERGE_STAGE_THREADS, true>), grid, dim3(MERGE_STAGE_THREADS), smem, s, mc, in,
                            recs, nrec, rec_stride,
                            rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag, seq, split_cs,
-                           merge_fence_sys());
+                           merge_fence_sys(), gate);
     } else {
         hipLaunchKernelGGL((merge_kernel<MERGE_THREADS, false>), grid, dim3(MERGE_THREADS), smem, s, mc, in, recs, nrec,
                            rec_stride,
                            rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag, seq, split_cs,
-                           merge_fence_sys());
+                           merge_fence_sys(), gate);
     }
 }
 
@@ -1304,7 +1315,7 @@ int launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nre
     const bool stage = !cs && merge_stage_fits(nrec, rec_stride, mc.P, mc.K, &smem);
     if (cs) smem = merge_smem_bytes(nrec, mc.P, mc.K);
     launch_merge_kernel(stage, dim3(nb), smem, s, mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out,
-                        chain, chain ? ctr_inc : 0, dbg, pub.flag, pub.seq, cs);
+                        chain, chain ? ctr_inc : 0, dbg, pub.flag, pub.seq, cs, pub.gate);
     return nb;
 }
 
@@ -1387,7 +1398,7 @@ int launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, in
     size_t smem = 0;
     const bool stage = merge_stage_fits(per, rec_stride, mc.P, mc.K, &smem);
     launch_merge_kernel(stage, dim3(m), smem, s, mc, in, recs, nrec, rec_stride, 0, noise, partials, nullptr, 0, 0,
-                        nullptr, nullptr, 0u, 0);
+                        nullptr, nullptr, 0u, 0, pub.gate);
     return launch_merge(mc, in, partials, m, rec_floats_rank(mc.P, mc.K), 1, noise, rank_out, out, chain, s, nullptr,
                         ctr_inc, pub);
 }
@@ -1408,7 +1419,8 @@ void launch_copy16(const void* src, void* dst, size_t bytes0, size_t off1, size_
 // Armed step (launch_arm_copy): the step's input copy, queued before the host has the input.
 __global__ void __launch_bounds__(256) arm_copy_kernel(const uint32_t* __restrict__ go, uint32_t seq,
                                                        uint64_t deadline_ticks, const uint32_t* __restrict__ src,
-                                                       uint32_t* __restrict__ dst, int n0, int off1, int n1) {
+                                                       uint32_t* __restrict__ dst, int n0, int off1, int n1,
+                                                       uint32_t* __restrict__ fired) {
     __shared__ int fire;
     if (threadIdx.x == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -1418,6 +1430,10 @@ __global__ void __launch_bounds__(256) arm_copy_kernel(const uint32_t* __restric
             g = __hip_atomic_load(go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         fire = g == seq;
+        // the chain behind reads this word (Publish::gate / GroupArgs::gate / RngJob::gate) after the kernel
+        // boundary: fired -> seq, cancelled or timed out -> seq | ARM_CANCEL (nothing computed, that token
+        // published, the host re-runs the call unarmed)
+        *fired = fire ? seq : (seq | ARM_CANCEL);
     }
     __syncthreads();
     if (!fire) return;
@@ -1428,9 +1444,9 @@ __global__ void __launch_bounds__(256) arm_copy_kernel(const uint32_t* __restric
     }
 }
 void launch_arm_copy(const uint32_t* go, uint32_t seq, uint64_t deadline_ticks, const void* src, void* dst,
-                     size_t bytes0, size_t off1, size_t bytes1, hipStream_t s) {
+                     size_t bytes0, size_t off1, size_t bytes1, uint32_t* fired, hipStream_t s) {
     hipLaunchKernelGGL(arm_copy_kernel, dim3(1), dim3(256), 0, s, go, seq, deadline_ticks, (const uint32_t*)src,
-                       (uint32_t*)dst, (int)(bytes0 / 4), (int)(off1 / 4), (int)(bytes1 / 4));
+                       (uint32_t*)dst, (int)(bytes0 / 4), (int)(off1 / 4), (int)(bytes1 / 4), fired);
 }
 
 __global__ void empty_kernel() {}

@@ -14,6 +14,7 @@ struct RngJob {
     float* noise;
     uint64_t seed, ctr;
     int dev_ctr, ctr_offset;
+    const uint32_t* gate;  // armed chain: skip the draws when *gate holds the cancel bit (ARM_CANCEL)
 };
 int rng_grid(const ModelConst& mc);
 
@@ -30,6 +31,7 @@ struct GroupArgs {
     float* grecs;   // ngroups x rec_stride
     uint32_t* cnt;  // ngroups arrival counters, zero between launches (each group's last arriver resets its own)
     int gsize;      // blocks per group
+    const uint32_t* gate;  // armed chain (Publish::gate): every block exits at once when the chain did not fire
 };
 // blocks per group for a launch of `nblocks` rollout blocks of `rec_stride`-float records (1: no grouping:
 // CEM, or fewer than GROUP_MIN_BLOCKS blocks); SRBD_GROUP_SIZE overrides (1 disables grouping)
@@ -43,7 +45,7 @@ bool rollout_specialised(int kind, int H, int S);
 // rollout, on the CUs it leaves idle.
 void launch_rollout(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
                     int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next = nullptr,
-                    const GroupArgs& grp = GroupArgs{nullptr, nullptr, 1});
+                    const GroupArgs& grp = GroupArgs{nullptr, nullptr, 1, nullptr});
 // the thread-per-sample forms (srbd_rollout_thread.hip): plain and gait-adaptive
 void launch_rollout_thread(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
                            int rec_stride, int threads, hipStream_t s, const RngJob* next, const GroupArgs& grp);
@@ -52,7 +54,7 @@ void launch_rollout_ga_thread(const ModelConst& mc, const StepInput* in, const f
                               const GroupArgs& grp);
 // Counter: `ctr` (host-known), or in->ctr + ctr_offset when dev_ctr != 0 (device-resident chain).
 void launch_rng(const ModelConst& mc, const StepInput* in, uint64_t seed, uint64_t ctr, int dev_ctr, int ctr_offset,
-                float* noise, hipStream_t s);
+                float* noise, hipStream_t s, const uint32_t* gate = nullptr);
 void launch_transpose(const float* src, int n, int P, int ldn, float* dst, hipStream_t s);
 size_t merge_smem_bytes(int nrec, int P, int K);
 // Completion published to the host: after every output write is visible system-wide, the merge
@@ -60,6 +62,10 @@ size_t merge_smem_bytes(int nrec, int P, int K);
 struct Publish {
     uint32_t* flag;
     uint32_t seq;
+    // armed chain: the word arm_copy_kernel writes (seq when it fired, seq | ARM_CANCEL when not); a chain
+    // that did not fire computes nothing and publishes seq | ARM_CANCEL, so the host never takes the
+    // previous input's outputs for the current call (it re-runs the step unarmed)
+    const uint32_t* gate;
 };
 // chain != 0: also write the new parameters / sigma / RNG counter back into `in` (device warm start).
 // With step outputs and no rank record the merge is column-split over merge_blocks(mc) blocks, each
@@ -72,7 +78,7 @@ void merge_prepare();  // once per context: the LDS-staged merge's dynamic LDS l
 int merge_blocks(const ModelConst& mc);
 int launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                   int rows_in_rec, const float* noise, float* rank_out, StepOutput* out, int chain, hipStream_t s,
-                  uint64_t* dbg = nullptr, int ctr_inc = 1, Publish pub = {nullptr, 0});
+                  uint64_t* dbg = nullptr, int ctr_inc = 1, Publish pub = {nullptr, 0, nullptr});
 // Two-level merge when there are many block records: merge_partials(nrec) first-level blocks each
 // reduce a slice of the records (spreading the record reads over CUs) into rank-format partials,
 // then the partials are merged.
@@ -110,7 +116,7 @@ void launch_merge_xchg(const ModelConst& mc, StepInput* in, const float* recs, i
 int tune_knob(const char* name, int dflt);
 int launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                        const float* noise, float* partials, float* rank_out, StepOutput* out, int chain,
-                       hipStream_t s, int ctr_inc = 1, Publish pub = {nullptr, 0});
+                       hipStream_t s, int ctr_inc = 1, Publish pub = {nullptr, 0, nullptr});
 void launch_advance(const ModelConst& mc, StepInput* in, const StepOutput* out, hipStream_t s);
 void launch_empty(hipStream_t s);  // measurement: the event floor
 // src -> dst bytes [0, bytes0) and [off1, off1 + bytes1); all multiples of 16
@@ -121,7 +127,7 @@ void launch_copy16(const void* src, void* dst, size_t bytes0, size_t off1, size_
 // copy: the chain behind it recomputes the previous input and the host discards that run).
 constexpr uint32_t ARM_CANCEL = 0x80000000u;
 void launch_arm_copy(const uint32_t* go, uint32_t seq, uint64_t deadline_ticks, const void* src, void* dst,
-                     size_t bytes0, size_t off1, size_t bytes1, hipStream_t s);
+                     size_t bytes0, size_t off1, size_t bytes1, uint32_t* fired, hipStream_t s);
 void launch_div_selftest(const float* a, const float* b, int n, float* o, hipStream_t s);
 
 // TAMOLS (tamols_kernel.hip)
@@ -204,5 +210,6 @@ struct TamolsJob {
     uint64_t* dbg;       // diagnostic phase stamps (4 x TAMOLS_BPL x 8) or NULL
 };
 void launch_tamols_fused(const TamolsJob& j, hipStream_t s);
+int tamols_prepare();  // once per context: the staged scene's dynamic LDS limit (0 on success)
 
 }  // namespace srbd

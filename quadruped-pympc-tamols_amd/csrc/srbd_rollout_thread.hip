@@ -18,6 +18,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
                                                       const float* __restrict__ noise, float* __restrict__ costs,
                                                       float* __restrict__ recs, int rec_stride,
     const RngJob next_rng, int nroll, const GroupArgs grp) {
+    if (grp.gate && (*grp.gate & ARM_CANCEL)) return;  // armed chain that did not fire: nothing to compute
     // blocks past the rollout grid generate the next step's noise on the CUs the rollout leaves idle
     if ((int)blockIdx.x >= nroll) {
         rng_items(mc, in, next_rng, ((int)blockIdx.x - nroll) * (int)blockDim.x + (int)threadIdx.x,
@@ -242,6 +243,7 @@ __global__ void __launch_bounds__(256) rollout_ga_kernel(const ModelConst mc, co
                                                          const float* __restrict__ noise, float* __restrict__ costs,
                                                          float* __restrict__ recs, int rec_stride,
                                                          const RngJob next_rng, int nroll, const GroupArgs grp) {
+    if (grp.gate && (*grp.gate & ARM_CANCEL)) return;  // armed chain that did not fire
     if ((int)blockIdx.x >= nroll) {
         rng_items(mc, in, next_rng, ((int)blockIdx.x - nroll) * (int)blockDim.x + (int)threadIdx.x,
                   ((int)gridDim.x - nroll) * (int)blockDim.x);

@@ -373,6 +373,16 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
 #undef TAM_STAMP
 }
 
+// Once per TAMOLS context (srbd_tamols_create, on its device): the staged scene needs up to
+// TAMOLS_LDS_PRIMS x 80 B = 80 KB of dynamic LDS on top of ~23 KB static, above the default dynamic-LDS
+// limit a launch gets without the attribute (round-2 advisor finding; gfx950 has 160 KB per CU).
+int tamols_prepare() {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&tamols_fused_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)((sizeof(srbd_terrain_prim) + 2 * sizeof(double)) * TAMOLS_LDS_PRIMS));
+    return e == hipSuccess ? 0 : -1;
+}
+
 void launch_tamols_fused(const TamolsJob& j, hipStream_t s) {
     const int nb = j.a.ncand < TAMOLS_BPL ? j.a.ncand : TAMOLS_BPL;
     const int np = j.use_terrain ? j.t.nprims : 0;

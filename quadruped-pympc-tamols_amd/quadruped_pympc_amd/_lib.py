@@ -77,6 +77,8 @@ SIGNATURES = {
     "srbd_set_cost_terms": (_I, [_P, _FP, _F, _F]),
     "srbd_set_armed": (_I, [_P, C.c_int32, C.c_uint64]),
     "srbd_armed_stats": (_I, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "srbd_armed_refired": (_I, [_P, C.POINTER(C.c_int64)]),
+    "srbd_debug_arm_delay": (_I, [_P, C.c_uint32]),
     "srbd_record_floats": (_I, [_P]),
     "srbd_step_local": (_I, [_P, _FP, _FP, _FP, _I, _FP, _FP, _FP, C.c_uint64, C.c_uint64, _P]),
     "srbd_step_finish": (_I, [_P, _P, _I, _FP, _FP, C.POINTER(SrbdResult), _FP]),
@@ -475,6 +477,16 @@ class Context:
         a, b = C.c_int64(0), C.c_int64(0)
         self.check(lib.srbd_armed_stats(self.h, C.byref(a), C.byref(b)), "srbd_armed_stats")
         return int(a.value), int(b.value)
+
+    def armed_refired(self) -> int:
+        """srbd_armed_refired: claimed chains that had already given up and were re-run unarmed."""
+        a = C.c_int64(0)
+        self.check(lib.srbd_armed_refired(self.h, C.byref(a)), "srbd_armed_refired")
+        return int(a.value)
+
+    def debug_arm_delay(self, delay_us: int):
+        """srbd_debug_arm_delay (tests): host sleep between an armed claim and its go word."""
+        self.check(lib.srbd_debug_arm_delay(self.h, int(delay_us)), "srbd_debug_arm_delay")
 
     def set_stream(self, stream_handle: int | None):
         """Launch on a caller-owned hipStream_t; None (or 0, the legacy null stream) -> the context's own."""

@@ -9,16 +9,23 @@ when it is not.  A reference package that is installed but fails to import (for 
 
 Device: ``mpc_params['device_id']`` may be an ordinal or ``'auto'`` (the default when the key is
 absent, as in the reference's config).  ``'auto'`` maps replica process i to GPU i mod G
-(SURVEY 8(e) replica mode), with i = ``LOCAL_RANK`` under torchrun, else the multiprocessing
-identity of the process (``batched_simulations.py:49-55`` starts one ``Process`` per replica), else
-0.  It is resolved when the HIP context is created (the first compute call), never at construction.
+(SURVEY 8(e) replica mode), with i, in order of precedence: ``SRBD_REPLICA_INDEX`` (an explicit
+replica index a launcher sets), ``LOCAL_RANK`` under torchrun, the multiprocessing identity of the
+process as the last resort (``batched_simulations.py:49-55`` starts one ``Process`` per replica; the
+identity also counts Manager / Pool helpers the parent created, so a launcher that creates those should
+set ``SRBD_REPLICA_INDEX``), else 0.  It is resolved when the HIP context is created (the first compute
+call), never at construction, and the resolution is logged (logger ``quadruped_pympc_amd.runtime``,
+INFO) with its source.
 """
 from __future__ import annotations
 
 import importlib
 import importlib.util
+import logging
 import multiprocessing
 import os
+
+log = logging.getLogger(__name__)
 
 REFERENCE_CONFIG = "quadruped_pympc.config"
 
@@ -39,14 +46,21 @@ def active_config(config_module=None):
     return mirror
 
 
-def replica_index() -> int:
-    """Index of this replica process: LOCAL_RANK, else the multiprocessing identity (Process-k -> k-1),
-    else 0 (the main process)."""
-    lr = os.environ.get("LOCAL_RANK")
-    if lr is not None and lr.strip().lstrip("-").isdigit():
-        return int(lr)
+def replica_source() -> tuple[int, str]:
+    """(index, source) of this replica process: SRBD_REPLICA_INDEX, else LOCAL_RANK, else the
+    multiprocessing identity (Process-k -> k-1), else (0, 'main')."""
+    for var in ("SRBD_REPLICA_INDEX", "LOCAL_RANK"):
+        v = os.environ.get(var)
+        if v is not None and v.strip().isdigit():
+            return int(v), var
     ident = getattr(multiprocessing.current_process(), "_identity", ())
-    return ident[0] - 1 if ident else 0
+    if ident:
+        return ident[0] - 1, "multiprocessing identity"
+    return 0, "main"
+
+
+def replica_index() -> int:
+    return replica_source()[0]
 
 
 def resolve_device_id(spec, device_count=None) -> int:
@@ -58,5 +72,8 @@ def resolve_device_id(spec, device_count=None) -> int:
             device_count = _lib.device_count()
         if device_count < 1:
             return 0  # context creation then fails loudly (no CPU fallback)
-        return replica_index() % device_count
+        idx, src = replica_source()
+        dev = idx % device_count
+        log.info("device_id 'auto' -> GPU %d (replica %d from %s, %d GPU(s) visible)", dev, idx, src, device_count)
+        return dev
     return int(spec)

@@ -71,18 +71,33 @@ def test_broken_reference_config_raises(monkeypatch):
 
 def test_explicit_ordinal_and_auto(monkeypatch):
     monkeypatch.delenv("LOCAL_RANK", raising=False)
+    monkeypatch.delenv("SRBD_REPLICA_INDEX", raising=False)
     assert runtime.resolve_device_id(3, device_count=8) == 3
     assert runtime.resolve_device_id("2", device_count=8) == 2
     assert runtime.resolve_device_id("auto", device_count=8) == 0  # main process
     monkeypatch.setenv("LOCAL_RANK", "5")
     assert runtime.resolve_device_id("auto", device_count=4) == 1
     assert runtime.resolve_device_id(None, device_count=0) == 0
+    # an explicit replica index (a launcher's) wins over LOCAL_RANK and the multiprocessing identity
+    monkeypatch.setenv("SRBD_REPLICA_INDEX", "6")
+    assert runtime.replica_source() == (6, "SRBD_REPLICA_INDEX")
+    assert runtime.resolve_device_id("auto", device_count=4) == 2
+
+
+def test_auto_resolution_is_logged(monkeypatch, caplog):
+    import logging
+
+    monkeypatch.setenv("SRBD_REPLICA_INDEX", "3")
+    with caplog.at_level(logging.INFO, logger="quadruped_pympc_amd.runtime"):
+        assert runtime.resolve_device_id("auto", device_count=2) == 1
+    assert "GPU 1" in caplog.text and "SRBD_REPLICA_INDEX" in caplog.text
 
 
 def _child(q):
     import os
 
     os.environ.pop("LOCAL_RANK", None)
+    os.environ.pop("SRBD_REPLICA_INDEX", None)
     q.put(runtime.resolve_device_id("auto", device_count=8))
 
 

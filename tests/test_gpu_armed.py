@@ -211,3 +211,31 @@ def test_armed_gait_adaptive_bitwise(lib):
     st = []
     _same(_run(lib, case, script, armed=True, stats=st), _run(lib, case, script, armed=False))
     assert st[0] == (9, 1), st
+
+
+@pytest.mark.parametrize("N", [10000, 131072])
+def test_claimed_chain_that_gave_up_reruns_unarmed(lib, N):
+    """Round-2 advisor finding: a claim younger than half the deadline whose copy kernel has nevertheless
+    timed out (the host was delayed between the claim and the go word) must not return the previous
+    input's outputs.  The chain then computes nothing and publishes its cancel token; the call re-runs
+    unarmed.  Forced here with a 400 us deadline and a 3 ms host delay after each claim (steps timed from
+    C: the next call claims well inside half the deadline): every output equals the unarmed loop's bit for
+    bit and every claim is counted as re-run."""
+    case = make_case("c2", N=N, method="mppi")
+    steps = 8
+    ref = []
+    for armed in (False, True):
+        ctx = lib.Context(product_cfg(case))
+        states = np.stack([_inputs(case, k)[0] for k in range(steps)])
+        refs = np.stack([_inputs(case, k)[1] for k in range(steps)])
+        contacts = np.stack([case["contact"]] * steps)
+        if armed:
+            ctx.set_armed(True, 400)
+            ctx.debug_arm_delay(3000)
+        lat, best, _ = ctx.bench_host_steps(states, refs, contacts, case["best"], None, 5, 0, steps)
+        outs = (best.copy(), ctx.armed_stats(), ctx.armed_refired())
+        ctx.close()
+        ref.append(outs)
+    (b0, _, _), (b1, (served, cancelled), refired) = ref
+    np.testing.assert_array_equal(b0, b1)
+    assert refired >= 1 and served + refired <= steps, (served, cancelled, refired)

@@ -54,7 +54,7 @@ def check_reduction(case, g, noise=None):
     np.testing.assert_allclose(g["grf"], r["grf"], rtol=1e-5, atol=1e-3)
     np.testing.assert_allclose(g["pred"], r["pred"], rtol=1e-5, atol=1e-5)
     if "sigma" in r:
-        np.testing.assert_allclose(g["sigma"], r["sigma"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(g["sigma"], r["sigma"], rtol=1e-5, atol=1e-5, equal_nan=True)
     return r
 
 
@@ -64,6 +64,8 @@ def check_end_to_end(case, g, noise=None):
     try:
         np.testing.assert_allclose(g["grf"], ref["grf"], rtol=1e-4, atol=5e-3)
         np.testing.assert_allclose(g["best"], ref["best"], rtol=1e-4, atol=1e-3)
+        if "sigma" in ref:  # CEM (NMPC:1075-1081); NaN where the reference's jnp.cov is NaN (one elite row)
+            np.testing.assert_allclose(g["sigma"], ref["sigma"], rtol=1e-4, atol=1e-5, equal_nan=True)
     except AssertionError:
         # near tie: the selection flipped on costs equal to tolerance; the GPU is then consistent
         # with the oracle's reduction applied to the GPU's own costs
@@ -119,6 +121,23 @@ def test_small_and_ragged_n(lib, N, method):
     if N == 1:  # zero noise: MPPI/CEM keep the previous params, RS returns row 0 (= previous)
         np.testing.assert_array_equal(g["best"], case["best"])
     check_end_to_end(case, g)
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 4, 65, 257])
+def test_cem_sigma_small_n(lib, N):
+    """CEM sigma with fewer samples than num_elite: the reference takes jnp.argsort(costs)[:10] (all N rows)
+    and jnp.cov over them with ddof 1 (NMPC:1075-1081), so N = 1 gives NaN (0 / 0) for every parameter,
+    which the two jnp.where clips keep (NaN compares false).  The GPU merge forms the same statistics over
+    min(K, N) elite rows and returns NaN there too (no guard: a drop-in keeps the reference's output)."""
+    case = make_case("c2", N=N, method="cem_mppi", seed=100 + N)
+    g = run_gpu(lib, case)
+    ref = oracle_step(case)
+    np.testing.assert_allclose(g["sigma"], ref["sigma"], rtol=1e-5, atol=1e-5, equal_nan=True)
+    if N == 1:
+        assert np.isnan(g["sigma"]).all() and np.isnan(ref["sigma"]).all()
+    else:
+        assert np.isfinite(g["sigma"]).all() and (g["sigma"] >= np.float32(0.2)).all()
+        assert (g["sigma"] <= np.float32(5)).all()
 
 
 def test_all_swing_and_full_stance(lib):

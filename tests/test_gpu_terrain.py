@@ -114,3 +114,40 @@ def test_argument_errors(lib):
     hf = np.zeros((1, 5))
     assert lib.lib.srbd_terrain_create(0, bad, 0, 1, 0.0, lib.dptr(hf), 1, 5, 0, 0, 0.1, 0.1, 0.0,
                                        C.byref(h)) == lib.E_INVALID
+
+
+@pytest.mark.parametrize("n_box,n_cyl", [(500, 500), (560, 540)])
+def test_large_scene_fused_tamols(lib, n_box, n_cyl):
+    """Scenes at the LDS staging limit (1000 primitives: 80 KB of dynamic LDS beside the kernel's static
+    ~23 KB, which needs the dynamic-LDS attribute srbd_tamols_create sets) and past it (1100: the fused
+    kernel reads the primitives from global memory): raycast patches bit-exact vs the terrain oracle, and
+    the fused raycast + TAMOLS call equal to TAMOLS on those patches."""
+    from quadruped_pympc_amd import config
+    from quadruped_pympc_amd.helpers.terrain import GpuTerrain
+    from quadruped_pympc_amd.helpers.visual_foothold_adaptation import TamolsSearch, tamols_params_struct
+
+    rng = np.random.default_rng(n_box)
+    prims, hf = random_scene(rng, n_box=n_box, n_cyl=n_cyl)
+    ter = GpuTerrain(prims, has_ground=True, ground_z=-0.05, hfield=hf, miss_z=-9.0)
+    s = TamolsSearch(0)
+    try:
+        feet = np.array([[0.32, 0.13, 0.05], [0.32, -0.13, 0.05], [-0.06, 0.13, 0.05], [-0.06, -0.13, 0.05]])
+        seeds = feet + np.array([0.12, 0.02, 0.0])
+        hips = feet + np.array([0.0, 0.0, 0.3])
+        want = T.patches(prims, seeds, [0.3] * 4, 13, 7, 0.04, 0.04, 10.0, has_ground=True, ground_z=-0.05,
+                         hfield=hf, miss_z=-9.0)
+        hms = ter.patches(seeds, [0.3] * 4, 13, 7, 0.04, 0.04, ray_z=10.0)
+        np.testing.assert_array_equal(hms, want)
+        params = dict(config.simulation_params["tamols_params"])
+        params["h_des"] = 0.25
+        ps = tamols_params_struct(params, "go2")
+        kw = dict(forward_vel=np.array([0.5, 0.0, 0.0]), base_position=np.array([0.13, 0.0, 0.35]),
+                  current_contact=np.array([0, 1, 1, 0], np.int32), current_feet_pos=feet)
+        fused = s.run_terrain(ter, 0.3, seeds, hips, ps, **kw)
+        np.testing.assert_array_equal(fused["heightmaps"], want)
+        two = s.run(hms, seeds, hips, ps, **kw)
+        for k in ("footholds", "boxes", "valid", "scores", "seed_heights"):
+            np.testing.assert_array_equal(fused[k], two[k])
+    finally:
+        s.close()
+        ter.close()
