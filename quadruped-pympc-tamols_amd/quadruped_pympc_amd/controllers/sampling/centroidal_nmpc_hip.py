@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import copy
 import sys
+import warnings
 
 import numpy as np
 
@@ -307,15 +308,21 @@ class Sampling_MPC:
         return st
 
     def set_state(self, st: dict) -> "Sampling_MPC":
-        """Restore a ``get_state`` checkpoint (the device part only when this controller has a stepped
-        context; a fresh controller restores it on its first compute call's context otherwise)."""
+        """Restore a ``get_state`` checkpoint.  The host part (warm start, key, sigma) always; the device part
+        (``device_*``: what the next device-resident step starts from) only into a context that has run a
+        step, since srbd_set_state needs that step's state/reference inputs.  A fresh controller drops the
+        device part with a RuntimeWarning: its compute calls start from the host part anyway."""
         self.best_control_parameters = np.array(st["best_control_parameters"], dtype=f32).reshape(-1)
         self.master_key = np.array(st["master_key"], dtype=np.uint64).reshape(-1)
         if "sigma_cem_mppi" in st:
             self.sigma_cem_mppi = np.array(st["sigma_cem_mppi"], dtype=f32)
-        if "device_best" in st and self._ctx is not None and self._ctx.step_id > 0:
-            key = np.asarray(st["device_key"], dtype=np.uint64)
-            self._ctx.set_state(st["device_best"], st.get("device_sigma"), int(key[0]), int(key[1]))
+        if "device_best" in st:
+            if self._ctx is not None and self._ctx.step_id > 0:
+                key = np.asarray(st["device_key"], dtype=np.uint64)
+                self._ctx.set_state(st["device_best"], st.get("device_sigma"), int(key[0]), int(key[1]))
+            else:
+                warnings.warn("set_state: no stepped context yet, the checkpoint's device-resident part "
+                              "(device_best/device_sigma/device_key) is not restored", RuntimeWarning, stacklevel=2)
         return self
 
     def close(self):

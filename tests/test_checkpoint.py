@@ -21,6 +21,17 @@ def _controller(method):
         mirror.mpc_params["sampling_method"] = "mppi"
 
 
+def test_set_state_warns_when_device_part_dropped():
+    """A fresh controller cannot take a checkpoint's device-resident part: it says so (RuntimeWarning)."""
+    mpc = _controller("mppi")
+    st = mpc.get_state()
+    st["device_best"] = np.zeros(mpc.num_control_parameters, f32)
+    st["device_key"] = np.array([42, 3], np.uint64)
+    with pytest.warns(RuntimeWarning, match="device-resident part"):
+        mpc.set_state(st)
+    assert mpc.master_key[1] == st["master_key"][1]
+
+
 @pytest.mark.parametrize("method", ["random_sampling", "mppi", "cem_mppi"])
 def test_controller_state_round_trip_without_device(method):
     """get_state -> np.savez -> np.load (no pickle) -> set_state restores every evolving attribute."""
