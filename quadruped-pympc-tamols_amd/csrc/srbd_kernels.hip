@@ -221,7 +221,18 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     // instead of the whole horizon up front -- the terms' extra live values otherwise push the unrolled
     // horizon past 256 VGPRs into scratch.
     constexpr int PW = (EXT && KIND == SRBD_ZERO_ORDER) ? (NPRE < 4 ? NPRE : 4) : NPRE;
-    if constexpr (CT) {
+    // CEM cubic splines with S > 1: chunk q's four slots are loaded SRBD_CLEAD steps before its first step
+    // instead of up front.  C3 (H16 CEM): 80 -> 16 B of scratch per lane, rollout 41.8 -> 37.9 us, device
+    // step 73.1 -> 65.5 us (r3d); leads 3 / 4 spill again (80 / 144 B), and the plain cubic kernels spill
+    // more with the window (H16: 48 -> 144 B at lead 2), so they keep the up-front loads.
+#ifndef SRBD_CLEAD
+#define SRBD_CLEAD 2
+#endif
+    constexpr bool CWIN = CT && CEMT && KIND == SRBD_CUBIC_SPLINE && ST > 1 && SRBD_CLEAD > 0;
+    if constexpr (CWIN) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) load_slot(i);
+    } else if constexpr (CT) {
         // slot-major issue order: step n's operands are the first to return (loads complete in order),
         // so the horizon starts while the later steps' parameters are still in flight
 #pragma unroll
@@ -232,6 +243,15 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     auto step = [&](const int n, auto EX) __attribute__((always_inline)) {  // EX: as rollout_kernel
         if constexpr (CT && PW < NPRE)
             if (n + PW < NPRE) load_slot(n + PW);  // n is a compile-time constant here (unrolled horizon)
+        if constexpr (CWIN) {
+#pragma unroll
+            for (int q = 1; q < (CWIN ? ST : 1); ++q) {
+                const int at = q * HT / ST - SRBD_CLEAD;
+                if (n == (at > 0 ? at : 0))
+#pragma unroll
+                    for (int i = 4 * q; i < 4 * q + 4; ++i) load_slot(i);
+            }
+        }
         // this step's scalars through step_ptr: loaded per step, not hoisted across the unrolled horizon
         // (hoisted: SGPR spills to VGPR lanes, ~150 v_readlane per step in the cubic CEM kernel)
         const auto is = step_ptr(in, dep);
