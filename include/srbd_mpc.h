@@ -265,7 +265,8 @@ int srbd_xgmi_disconnect(srbd_ctx* ctx);
 
 /* Diagnostic: mean duration (us) of the merge kernel's 5 phases (s_memrealtime stamps), then (staged merge)
  * the times from its start at which the records were in LDS and the tail prep was done, then the
- * shader clock in MHz over the kernel, then 16 finer marks (us from the start; 0 = unset): 24 floats. */
+ * shader clock in MHz over the kernel, then 16 finer marks (us from the start; 0 = unset): 24 floats for
+ * block 0, then the same 24 for block 1 of a column-split merge (a slice block; zeros when unsplit): 48. */
 int srbd_debug_merge_phases(srbd_ctx* ctx, int32_t iters, float* out_us);
 
 /* Self-test of the correctly rounded division used in the rollout (a/b; b == 3 uses the constant

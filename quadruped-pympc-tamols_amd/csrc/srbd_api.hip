@@ -1654,24 +1654,30 @@ extern "C" int srbd_debug_merge_phases(srbd_ctx* c, int32_t iters, float* out_us
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step once first");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     uint64_t* d = nullptr;
-    HIP_TRY(c, hipMalloc((void**)&d, 32 * sizeof(uint64_t)));
-    HIP_TRY(c, hipMemsetAsync(d, 0, 32 * sizeof(uint64_t), c->stream));
-    double acc[24] = {};
+    HIP_TRY(c, hipMalloc((void**)&d, 64 * sizeof(uint64_t)));
+    HIP_TRY(c, hipMemsetAsync(d, 0, 64 * sizeof(uint64_t), c->stream));
+    double acc[48] = {};
     for (int i = 0; i < iters; ++i) {
         launch_merge(c->mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, 0, c->d_noise[c->cur], nullptr,
                      c->d_out, 0, c->stream, d);
-        uint64_t h[32];
-        HIP_TRY(c, hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+        uint64_t hh[64];
+        HIP_TRY(c, hipMemcpyAsync(hh, d, sizeof(hh), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
-        for (int k = 0; k < 5; ++k) acc[k] += (double)(h[k + 1] - h[k]) * 0.01;  // 100 MHz ticks -> us
-        // staged merge: records in LDS, tail lanes' force-independent step done (from the start)
-        for (int k = 5; k < 7; ++k) acc[k] += h[k + 1] > h[0] ? (double)(h[k + 1] - h[0]) * 0.01 : 0.0;
-        // shader clock (MHz): s_memtime ticks over the same span as the 100 MHz s_memrealtime stamps
-        acc[7] += h[5] > h[0] ? (double)(h[9] - h[8]) / ((double)(h[5] - h[0]) * 0.01) : 0.0;
-        for (int k = 0; k < 16; ++k) acc[8 + k] += h[16 + k] > h[0] ? (double)(h[16 + k] - h[0]) * 0.01 : 0.0;
+        for (int b = 0; b < 2; ++b) {  // block 0, block 1 (a column-split merge's first slice block)
+            const uint64_t* h = hh + 32 * b;
+            double* a = acc + 24 * b;
+            if (!h[0]) continue;
+            for (int k = 0; k < 5; ++k) a[k] += (double)(h[k + 1] - h[k]) * 0.01;  // 100 MHz ticks -> us
+            // staged merge: records in LDS, tail lanes' force-independent step done (from the start)
+            for (int k = 5; k < 7; ++k) a[k] += h[k + 1] > h[0] ? (double)(h[k + 1] - h[0]) * 0.01 : 0.0;
+            // shader clock (MHz): s_memtime ticks over the same span as the 100 MHz s_memrealtime stamps
+            a[7] += h[5] > h[0] ? (double)(h[9] - h[8]) / ((double)(h[5] - h[0]) * 0.01) : 0.0;
+            for (int k = 0; k < 16; ++k) a[8 + k] += h[16 + k] > h[0] ? (double)(h[16 + k] - h[0]) * 0.01 : 0.0;
+        }
+        HIP_TRY(c, hipMemsetAsync(d, 0, 64 * sizeof(uint64_t), c->stream));
     }
     (void)hipFree(d);
-    for (int k = 0; k < 24; ++k) out_us[k] = (float)(acc[k] / iters);
+    for (int k = 0; k < 48; ++k) out_us[k] = (float)(acc[k] / iters);
     return SRBD_OK;
 }
 

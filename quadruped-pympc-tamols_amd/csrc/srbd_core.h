@@ -260,9 +260,11 @@ struct LdsConst {
 template <class KC>
 SRBD_HD void integrate_k(const KC& kc, float x[12], const float feet[12], const float F[12], const float c[4],
                          float dt) {
+    // leg sums pairwise, (leg0 + leg1) + (leg2 + leg3): the four-lane kernel forms them with one quad
+    // butterfly over leg-parallel lanes (rollout_quad_kernel), and every layout uses this order
     float temp[3], lin_acc[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) temp[k] = F[k] * c[0] + F[3 + k] * c[1] + F[6 + k] * c[2] + F[9 + k] * c[3];
+    for (int k = 0; k < 3; ++k) temp[k] = (F[k] * c[0] + F[3 + k] * c[1]) + (F[6 + k] * c[2] + F[9 + k] * c[3]);
     const float inv_m = kc.inv_m();
     lin_acc[0] = inv_m * temp[0] + 0.0f;
     lin_acc[1] = inv_m * temp[1] + 0.0f;
@@ -273,20 +275,18 @@ SRBD_HD void integrate_k(const KC& kc, float x[12], const float feet[12], const 
     sincos_(x[7], &sp, &cp);
     sincos_(x[8], &sy, &cy);
 
-    float temp2[3];
+    float tc[4][3];  // (p_i - p_com) x f_i * c_i per leg
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const float v[3] = {feet[3 * i] - x[0], feet[3 * i + 1] - x[1], feet[3 * i + 2] - x[2]};
         float t[3];
         skew_dot(v, F + 3 * i, t);
-        if (i == 0) {
 #pragma unroll
-            for (int k = 0; k < 3; ++k) temp2[k] = t[k] * c[0];
-        } else {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) temp2[k] = temp2[k] + t[k] * c[i];
-        }
+        for (int k = 0; k < 3; ++k) tc[i][k] = t[k] * c[i];
     }
+    float temp2[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) temp2[k] = (tc[0][k] + tc[1][k]) + (tc[2][k] + tc[3][k]);
 
     float er[3];
     euler_rates(sr, cr, sp, cp, x[9], x[10], x[11], er);

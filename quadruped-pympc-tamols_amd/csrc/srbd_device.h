@@ -462,17 +462,36 @@ __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepI
     const int tid = threadIdx.x;
     const int k0 = blockIdx.x * SPB;
     const uint64_t key = (sib >= 0 && valid) ? cost_key(cost, (uint32_t)(mc.row0 + k0 + sib)) : ~0ull;
-    const uint64_t bkey = block_min_u64(key, red);
-    const float m = u2f((uint32_t)(bkey >> 32));
     float* rec = recs + (size_t)blockIdx.x * rec_stride;
     const int P = mc.P, K = mc.K;
-    if (tid == 0) elite_sh[0] = bkey;
-    uint64_t last = bkey;
-    for (int r = 1; r < K; ++r) {
-        const uint64_t cand = key > last ? key : ~0ull;
-        last = block_min_u64(cand, red);
-        if (tid == 0) elite_sh[r] = last;
+    uint64_t bkey;
+    if (K == 1) {
+        bkey = block_min_u64(key, red);
+        if (tid == 0) elite_sh[0] = bkey;
+    } else {
+        // The block's K smallest keys by rank: every sample counts the block's keys below its own (the
+        // `lps` lanes of a sample -- 4 in the four-lane layouts, else 1 -- split the count, summed by DPP),
+        // and a sample of rank < K stores its key at elite_sh[rank] (keys are unique; invalid samples all
+        // carry ~0 and can only fill the tail with ~0).  Two barriers, where K rounds of a block minimum
+        // took 2K (C3 rollout: see DESIGN.md).
+        __shared__ uint64_t ks[256];
+        const int lps = (int)blockDim.x / SPB, part = tid & (lps - 1), s = tid / lps;
+        if (sib >= 0) ks[sib] = key;
+        if (tid < K) elite_sh[tid] = ~0ull;
+        __syncthreads();
+        const uint64_t mine = ks[s];
+        const int span = SPB / lps, i0 = part * span;
+        int cnt = 0;
+        for (int i = 0; i < span; ++i) cnt += ks[i0 + i] < mine ? 1 : 0;
+        if (lps == 4) {
+            cnt += __builtin_amdgcn_mov_dpp(cnt, 0xB1, 0xF, 0xF, true);  // quad lanes (1, 0, 3, 2)
+            cnt += __builtin_amdgcn_mov_dpp(cnt, 0x4E, 0xF, 0xF, true);  // quad lanes (2, 3, 0, 1)
+        }
+        if (part == 0 && cnt < K) elite_sh[cnt] = mine;
+        __syncthreads();
+        bkey = elite_sh[0];
     }
+    const float m = u2f((uint32_t)(bkey >> 32));
     SRBD_RSTAMP(3);
     if (mc.method != SRBD_RANDOM_SAMPLING) {
         if (sib >= 0) e_sh[sib] = valid ? expf(-1.0f * (cost - m)) : 0.0f;

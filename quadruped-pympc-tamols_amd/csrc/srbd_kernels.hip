@@ -48,6 +48,8 @@ __global__ void __launch_bounds__(256) transpose_kernel(const float* __restrict_
 constexpr int QP_B0 = 0x00, QP_B1 = 0x55, QP_B2 = 0xAA;  // quad_perm broadcast of lane 0/1/2
 constexpr int QP_NEXT = 0x09;   // lanes (0,1,2,3) <- (1,2,0,0): component c+1 (mod 3)
 constexpr int QP_NEXT2 = 0x52;  // lanes (0,1,2,3) <- (2,0,1,1): component c+2 (mod 3)
+constexpr int QP_XOR1 = 0xB1;   // lanes (0,1,2,3) <- (1,0,3,2)
+constexpr int QP_XOR2 = 0x4E;   // lanes (0,1,2,3) <- (2,3,0,1)
 
 template <int CTRL>
 __device__ __forceinline__ float qp(float v) {
@@ -126,6 +128,21 @@ __device__ __forceinline__ void quad_rb_apply(const ModelConst& mc, const QuadLa
     r = rn;
     w = wn;
 }
+// quad_rb_apply with the torque sum's three components already on every lane (the leg-parallel force phase):
+// the same float operations, no broadcasts.
+__device__ __forceinline__ void quad_rb_apply3(const ModelConst& mc, const QuadLane& L, const QuadRB& q, float temp,
+                                               float t2x, float t2y, float t2z, float dt, float& p, float& v, float& r,
+                                               float& w) {
+    const float lin = mc.inv_m * temp + L.g;
+    const float Rt = q.R0 * t2x + q.R1 * t2y + q.R2 * t2z;
+    const float a2 = L.Ii0 * qp<QP_B0>(Rt) + L.Ii1 * qp<QP_B1>(Rt) + L.Ii2 * qp<QP_B2>(Rt);
+    const float aa = -q.a1 + a2;
+    const float pn = p + v * dt, vn = v + lin * dt, rn = r + q.er * dt, wn = w + aa * dt;
+    p = pn;
+    v = vn;
+    r = rn;
+    w = wn;
+}
 __device__ __forceinline__ void quad_rigid_body(const ModelConst& mc, const QuadLane& L, float temp, float temp2,
                                                 float dt, float& p, float& v, float& r, float& w) {
     quad_rb_apply(mc, L, quad_rb_prep(L, r, w), temp, temp2, dt, p, v, r, w);
@@ -190,24 +207,43 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     // EXT: opt-in cost terms (srbd_set_cost_terms), this lane's component of extra_cost_step
     const float rwc = sel3(c, mc.cost_r[0], mc.cost_r[1], mc.cost_r[2]);
     float fprev[4];
+    // LEGP (every kernel but EXT): the force phase runs leg-parallel.  Lane q4 decodes, shapes and clips the
+    // three components of leg q4 and forms its force and torque contributions f c, ((p_foot - p) x f) c;
+    // one quad butterfly sums them over the legs in integrate()'s order (leg0 + leg1) + (leg2 + leg3),
+    // leaving all six sums on every lane; the rigid-body step then runs component-parallel as before.
+    // Lane 3 does real work in the force phase, the fz broadcast and the per-leg cross-product DPP moves
+    // go away (C2 ZO step: see DESIGN.md).  EXT keeps the component-parallel form (its terms are per
+    // component, in leg order).
+    constexpr bool LEGP = !EXT;
+    const int lq = q4;  // this lane's leg in the force phase
+    float footL[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) footL[q] = st[12 + 3 * lq + q];
 
     // Specialised shapes: every parameter this lane reads over the horizon (its component's block
     // of each leg) is loaded before the first step, so the horizon chain pays one memory round trip
     // instead of one per step (at N = 10 000 there is < 1 wave per SIMD to hide the latency).
     // ZO: H values per leg; linear: S + 1; cubic: 4 per chunk (start 10 * chunk, NMPC:225).
     constexpr int NPRE = !CT ? 1 : (KIND == SRBD_ZERO_ORDER ? HT : (KIND == SRBD_LINEAR_SPLINE ? ST + 1 : 4 * ST));
-    float pre[4][NPRE];
-    // noise through a buffer descriptor: per-lane part (component block + sample) in voffset, the
+    // LEGP: pre[q][i] = component q's slot i of this lane's leg; else pre[l][i] = this lane's component's
+    // slot i of leg l
+    float pre[LEGP ? 3 : 4][NPRE];
+    // noise through a buffer descriptor: per-lane part (leg or component block + sample) in voffset, the
     // uniform row in soffset -> no per-load address arithmetic (launch_rollout checks P*ldn*4 < 2^31)
-    const int cblk = KIND == SRBD_ZERO_ORDER ? c * HT : (KIND == SRBD_LINEAR_SPLINE ? c * (ST + 1) : 4 * c);
+    const int cblk = LEGP ? lq * PL
+                          : (KIND == SRBD_ZERO_ORDER ? c * HT : (KIND == SRBD_LINEAR_SPLINE ? c * (ST + 1) : 4 * c));
     const auto nrs = __builtin_amdgcn_make_buffer_rsrc((void*)noise, (short)0, mc.P * mc.ldn * 4, 0x00020000);
     const int voff = (cblk * mc.ldn + k) * 4;
     const float* __restrict__ bl = best + cblk;
     const float* __restrict__ sl = in->sigma + cblk;
     auto load_slot = [&](const int i) __attribute__((always_inline)) {
 #pragma unroll
-        for (int l = 0; l < 4; ++l) {
-            const int jr = l * PL + (KIND == SRBD_CUBIC_SPLINE ? 10 * (i >> 2) + (i & 3) : i);  // row - cblk
+        for (int l = 0; l < (LEGP ? 3 : 4); ++l) {
+            // row - cblk: LEGP component l of this leg (ZO l H + i, linear l (S + 1) + i, cubic 10 chunk + 4 l +
+            // k); else leg l's block of this lane's component
+            const int jr = LEGP ? (KIND == SRBD_ZERO_ORDER ? l * HT + i
+                                   : (KIND == SRBD_LINEAR_SPLINE ? l * (ST + 1) + i : 10 * (i >> 2) + 4 * l + (i & 3)))
+                                : l * PL + (KIND == SRBD_CUBIC_SPLINE ? 10 * (i >> 2) + (i & 3) : i);
             const float nzv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(nrs, voff, jr * mc.ldn * 4, 0));
             if constexpr (CEMT) {  // unscaled CEM device draws: Z * sigma_j (z * 1 == z; the load unconditional)
                 const float sj = sl[jr];
@@ -260,10 +296,58 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
         const float dt = mc.dts[n];
         const float sq = mc.sq[n], somq = mc.somq[n], sa = mc.sa[n], sb = mc.sb[n], scc = mc.sc[n], sd = mc.sd[n];
         const int idx = CT && KIND != SRBD_ZERO_ORDER ? chunk_index(n, HT, ST) : mc.sidx[n];
-        // force and torque sums in leg order (integrate(): temp = sum_i f_i c_i, temp2 = sum_i t_i c_i;
-        // 0 + x == x).  No per-leg branch on the contact flags: the straight-line horizon schedules
-        // better than it saves (measured 15.9 -> 17.1 us at C2 with the branches)
-        float temp = 0.0f, temp2 = 0.0f, ex = 0.0f;
+        // force and torque sums over the legs, (leg0 + leg1) + (leg2 + leg3) as integrate() forms them.  No
+        // per-leg branch on the contact flags: the straight-line horizon schedules better than it saves
+        // (measured 15.9 -> 17.1 us at C2 with the branches)
+        float temp, temp2, ex = 0.0f;
+        if constexpr (LEGP) {
+            const float clq = lq == 0 ? cl[0] : (lq == 1 ? cl[1] : (lq == 2 ? cl[2] : cl[3]));
+            const int lbase = lq * PL;
+            // component q of this leg's decoded force (slot i, parameter j of the leg when not prefetched)
+            auto PQ = [&](int q, int i, int j) {
+                if constexpr (CT) {
+                    return pre[q][i];
+                } else {
+                    const float z = nz[(size_t)(lbase + j) * ldn];
+                    return best[lbase + j] + (zs ? z * in->sigma[lbase + j] : z);
+                }
+            };
+            float rq[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                if (KIND == SRBD_ZERO_ORDER) {
+                    rq[q] = PQ(q, n, n + q * H);
+                } else if (KIND == SRBD_LINEAR_SPLINE) {
+                    const int o = idx + q * (S + 1);
+                    rq[q] = somq * PQ(q, idx, o) + sq * PQ(q, idx + 1, o + 1);
+                } else {
+                    const int o = 10 * idx + 4 * q;
+                    const float p0 = PQ(q, 4 * idx, o), p1 = PQ(q, 4 * idx + 1, o + 1), p2 = PQ(q, 4 * idx + 2, o + 2),
+                                p3 = PQ(q, 4 * idx + 3, o + 3);
+                    const float phi = 0.5f * ((p2 - p1) + (p1 - p0));
+                    const float phin = 0.5f * ((p3 - p2) + (p2 - p1));
+                    rq[q] = sa * p1 + sb * phi + scc * p2 + sd * phin;
+                }
+            }
+            // shape_leg / clip_leg (srbd_core.h), this lane's leg
+            const float fz = clamp_cs((fref + rq[2]) * clq, mc.grf_min, mc.grf_max);
+            const float lo = mc.neg_mu * fz, hi = mc.mu * fz;
+            const float fx = clamp_cs(third(rq[0] * clq), lo, hi), fy = clamp_cs(third(rq[1] * clq), lo, hi);
+            // integrate(): skew_dot(p_foot - p, f) * c (the position's components from their lanes)
+            const float vx = footL[0] - qp<QP_B0>(p), vy = footL[1] - qp<QP_B1>(p), vz = footL[2] - qp<QP_B2>(p);
+            float sm[6] = {fx * clq, fy * clq, fz * clq, ((-vz) * fy + vy * fz) * clq, (vz * fx + (-vx) * fz) * clq,
+                           ((-vy) * fx + vx * fy) * clq};
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {  // quad butterfly: (l0 + l1) + (l2 + l3) on every lane (adds commute)
+                sm[i] = sm[i] + qp<QP_XOR1>(sm[i]);
+                sm[i] = sm[i] + qp<QP_XOR2>(sm[i]);
+            }
+            temp = sel3(c, sm[0], sm[1], sm[2]);
+            temp2 = sel3(c, sm[3], sm[4], sm[5]);
+            dep = sm[5];  // the next step's scalar loads issue from here on (step_ptr)
+            quad_rb_apply3(mc, L, quad_rb_prep(L, r, w), temp, sm[3], sm[4], sm[5], dt, p, v, r, w);
+        } else {
+        float tf[4], tt[4];
 #pragma unroll
         for (int l = 0; l < 4; ++l) {
             const int base = l * PL;
@@ -296,8 +380,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
             const float xy = third(raw * cl[l]);
             const float fz = qp<QP_B2>(c == 2 ? zp : xy);
             const float f = c == 2 ? fz : clamp_cs(xy, mc.neg_mu * fz, mc.mu * fz);
-            temp = temp + f * cl[l];
-            temp2 = temp2 + quad_cross(feet[l] - p, f) * cl[l];
+            tf[l] = f * cl[l];
+            tt[l] = quad_cross(feet[l] - p, f) * cl[l];
             if constexpr (decltype(EX)::value) {
                 const float u = c == 2 ? f - (cl[l] != 0.0f ? fref : 0.0f) : f;
                 float term = (u * rwc) * u;
@@ -315,8 +399,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
                 fprev[l] = f;
             }
         }
+        temp = (tf[0] + tf[1]) + (tf[2] + tf[3]);
+        temp2 = (tt[0] + tt[1]) + (tt[2] + tt[3]);
         dep = temp2;  // the next step's scalar loads issue from here on (step_ptr)
         quad_rigid_body(mc, L, temp, temp2, dt, p, v, r, w);
+        }
         // tracking cost (NMPC:451), accumulated per component lane: cost_c += ((tp + tv) + tr) + tw,
         // the three lanes summed once after the horizon (see rollout_kernel for the same order)
         const float ep = p - rp, ev = v - rv, er_ = r - rr, ew = w - rw;
@@ -416,7 +503,7 @@ __global__ void __launch_bounds__(512) rollout_ga_quad_kernel(const ModelConst m
         }
         const float ns = ((cl[0] + cl[1]) + cl[2]) + cl[3];
         const float fref = mc.fz_ns[(int)ns];
-        float temp = 0.0f, temp2 = 0.0f;
+        float tf[4], tt[4];  // per-leg force / torque contributions, summed pairwise (integrate()'s order)
 #pragma unroll
         for (int l = 0; l < 4; ++l) {
             const int base = l * PL;
@@ -455,9 +542,10 @@ __global__ void __launch_bounds__(512) rollout_ga_quad_kernel(const ModelConst m
             const float xy = third(raw * cl[l]);
             const float fz = qp<QP_B2>(c == 2 ? zp : xy);
             const float fo = c == 2 ? fz : clamp_cs(xy, mc.neg_mu * fz, mc.mu * fz);
-            temp = temp + fo * cl[l];
-            temp2 = temp2 + quad_cross(feet[l] - p, fo) * cl[l];
+            tf[l] = fo * cl[l];
+            tt[l] = quad_cross(feet[l] - p, fo) * cl[l];
         }
+        const float temp = (tf[0] + tf[1]) + (tf[2] + tf[3]), temp2 = (tt[0] + tt[1]) + (tt[2] + tt[3]);
         quad_rigid_body(mc, L, temp, temp2, mc.dts[n], p, v, r, w);
         const float ep = p - rp, ev = v - rv, er_ = r - rr, ew = w - rw;
         const float tp = (ep * Qp) * ep, tv = (ev * Qv) * ev, tr = (er_ * Qr) * er_, tw = (ew * Qw) * ew;
@@ -479,8 +567,10 @@ __device__ __forceinline__ uint64_t rec_key(const float* R, int P, int q) {
 }
 
 constexpr int MERGE_THREADS = 1024;
-constexpr int MERGE_WAVES = MERGE_THREADS / 64;
-constexpr int MERGE_PREF = 24;  // record values of the weighted sums loaded per thread before beta is known
+#ifndef SRBD_MERGE_PREF
+#define SRBD_MERGE_PREF 24
+#endif
+constexpr int MERGE_PREF = SRBD_MERGE_PREF;  // record values of the weighted sums loaded per thread before beta is known
 constexpr int MERGE_RPT = 8;    // record headers per thread (nrec <= MERGE_RPT * MERGE_THREADS)
 // The LDS-staged merge runs two waves per SIMD: its phases are short dependent chains that every
 // wave repeats (index math, the beta reduction), so 16 waves pay ~2x the issue of 8, while fewer
@@ -488,36 +578,83 @@ constexpr int MERGE_RPT = 8;    // record headers per thread (nrec <= MERGE_RPT 
 #ifndef MERGE_STAGE_THREADS
 #define MERGE_STAGE_THREADS 512
 #endif
-// Block-wide K smallest record keys (ascending) into `elite`, K <= KM: every thread's list starts as
-// its first record's keys (a record's keys ascend already), later records insert; per-wave K-round
-// minima; then one wave over the MERGE_WAVES wave lists.  Caller syncs afterwards.
-template <int KM, int NW = MERGE_WAVES>
-__device__ __forceinline__ void block_topk(const float* __restrict__ recs, int nrec, int rec_stride, int P, int K,
-                                           uint64_t (*wlist)[MAXK], uint64_t* elite) {
-    const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wv = tid >> 6;
-    uint64_t lk[KM];
-#pragma unroll
-    for (int i = 0; i < KM; ++i) lk[i] = KEY_NONE;
-    for (int r = tid; r < nrec; r += T) {
-        const float* R = recs + (size_t)r * rec_stride;
-        uint64_t keys[KM];  // all of the record's keys in one memory round trip
-#pragma unroll
-        for (int q = 0; q < KM; ++q) keys[q] = q < K ? rec_key(R, P, q) : KEY_NONE;
-        if (r == tid) {
-#pragma unroll
-            for (int q = 0; q < KM; ++q) lk[q] = keys[q];
-        } else {
-#pragma unroll
-            for (int q = 0; q < KM; ++q)
-                if (keys[q] < lk[K - 1]) lk_insert(lk, keys[q]);  // later keys fail too
-        }
+// Block-wide K smallest record keys (ascending) into `elite`, by selection and ranks.  Every record's
+// key list is the sorted K smallest keys of its samples, so its first key is its minimum, and the K
+// smallest keys overall lie in the K records with the smallest minima (any other record's minimum already
+// exceeds K keys of those records).  Keys are unique (cost bits, row); only the ~0 padding repeats.
+//  1. the K smallest record minima, with their records: per chunk of NT records, every record's rank in
+//     its wave's 64 minima (64 independent LDS-broadcast compares) sends the wave's K smallest to a
+//     candidate list, then the candidates' ranks among themselves and the K carried from the chunks
+//     before (<= NW K + K compares) keep the K smallest;
+//  2. those records' K-key lists (K x K keys), ranked among themselves, give the K smallest keys.
+// Compares are independent, so the phase is issue-bound (~4 us at C3's 1024 records) where K dependent
+// rounds of DPP wave minima per level were latency-bound (10 us).  Caller syncs afterwards.
+template <int NT>
+struct TopkLds {
+    uint64_t keys[NT > MAXK * MAXK ? NT : MAXK * MAXK];  // a chunk's record minima, then step 2's K x K keys
+    uint64_t cand[(NT / 64) * MAXK + MAXK];
+    int cand_r[(NT / 64) * MAXK + MAXK];
+    uint64_t top[MAXK], ntop[MAXK];         // carried K smallest minima (and the next chunk's)
+    int top_r[MAXK], ntop_r[MAXK];
+};
+template <int NT>
+__device__ __forceinline__ void block_topk_rank(const float* __restrict__ recs, int nrec, int rec_stride, int P, int K,
+                                                uint64_t* elite, TopkLds<NT>& t) {
+    constexpr int NW = NT / 64;
+    const int tid = threadIdx.x, T = NT, wv = tid >> 6;
+    const int NC = NW * K + K;  // candidates per chunk: the waves' K smallest + the carried K
+    if (tid < K) {
+        t.top[tid] = KEY_NONE;
+        t.top_r[tid] = 0;
     }
-    wave_topk(lk, K, wlist[wv]);
+    for (int base = 0; base < nrec; base += T) {
+        const int r = base + tid;
+        const uint64_t x = r < nrec ? rec_key(recs + (size_t)r * rec_stride, P, 0) : KEY_NONE;
+        t.keys[tid] = x;
+        for (int i = tid; i < NW * K; i += T) t.cand[i] = KEY_NONE;
+        __syncthreads();
+        const uint64_t* wk = t.keys + (wv << 6);
+        int cnt = 0;
+#pragma unroll 16
+        for (int j = 0; j < 64; ++j) cnt += wk[j] < x ? 1 : 0;
+        if (cnt < K && x != KEY_NONE) {
+            t.cand[wv * K + cnt] = x;
+            t.cand_r[wv * K + cnt] = r;
+        }
+        if (tid < K) {
+            t.cand[NW * K + tid] = t.top[tid];
+            t.cand_r[NW * K + tid] = t.top_r[tid];
+            t.ntop[tid] = KEY_NONE;
+        }
+        __syncthreads();
+        if (tid < NC) {
+            const uint64_t y = t.cand[tid];
+            int c2 = 0;
+            for (int j = 0; j < NC; ++j) c2 += t.cand[j] < y ? 1 : 0;
+            if (c2 < K && y != KEY_NONE) {
+                t.ntop[c2] = y;
+                t.ntop_r[c2] = t.cand_r[tid];
+            }
+        }
+        __syncthreads();
+        if (tid < K) {
+            t.top[tid] = t.ntop[tid];
+            t.top_r[tid] = t.ntop_r[tid];
+        }
+        __syncthreads();
+    }
+    const int KK = K * K;
+    for (int i = tid; i < KK; i += T) {
+        const int e = i / K, q = i - e * K;
+        t.keys[i] = t.top[e] != KEY_NONE ? rec_key(recs + (size_t)t.top_r[e] * rec_stride, P, q) : KEY_NONE;
+    }
+    if (tid < K) elite[tid] = KEY_NONE;
     __syncthreads();
-    if (wv == 0) {
-#pragma unroll
-        for (int i = 0; i < KM; ++i) lk[i] = (lane < NW && i < K) ? wlist[lane][i] : KEY_NONE;
-        wave_topk(lk, K, elite);
+    for (int i = tid; i < KK; i += T) {
+        const uint64_t y = t.keys[i];
+        int c3 = 0;
+        for (int j = 0; j < KK; ++j) c3 += t.keys[j] < y ? 1 : 0;
+        if (c3 < K && y != KEY_NONE) elite[c3] = y;
     }
 }
 
@@ -552,9 +689,9 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     extern __shared__ float smem[];  // [STAGE: records] | scale[nrec_pad] | part[G*(ncol+1)] | erow[K*ncol]
     constexpr int NW = NT / 64;
     __shared__ uint64_t red[NW];
-    __shared__ uint64_t wlist[NW][MAXK];
     __shared__ uint64_t elite[MAXK];
     __shared__ int elite_src[MAXK];
+    __shared__ TopkLds<NT> tk;  // block_topk_rank
     __shared__ float Vs[MAXP + 1];
     __shared__ float nb[MAXP];
     __shared__ float tag_sh;  // header tag (gait-adaptive step frequency) of the record holding beta's row
@@ -562,11 +699,11 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     // uses (16) -- read back in one batch (kernarg fields re-read lazily are serial scalar loads)
     __shared__ float tail_sh[4][40];
 #define MERGE_STAMP(i) \
-    if (dbg && threadIdx.x == 0 && blockIdx.x == 0) dbg[i] = __builtin_amdgcn_s_memrealtime()
+    if (dbg && threadIdx.x == 0 && blockIdx.x < 2) dbg[32 * blockIdx.x + (i)] = __builtin_amdgcn_s_memrealtime()
     // finer marks (diagnostic build of the phases call only: dbg[16 + i])
 #define MERGE_MARK(i) MERGE_STAMP(16 + (i))
     MERGE_STAMP(0);
-    if (dbg && threadIdx.x == 0 && blockIdx.x == 0) dbg[8] = __builtin_amdgcn_s_memtime();  // shader clock
+    if (dbg && threadIdx.x == 0 && blockIdx.x < 2) dbg[32 * blockIdx.x + 8] = __builtin_amdgcn_s_memtime();  // clock
 
     // T: the launch's block size, a template constant (blockDim.x is a dependent load)
     const int tid = threadIdx.x, T = NT, lane = tid & 63, wv = tid >> 6;
@@ -793,10 +930,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         if (tid == 0) elite[0] = bkey;
         for (int e = 1 + tid; e < K; e += T) elite[e] = KEY_NONE;
     } else {
-        if (K <= 10)
-            block_topk<10, NW>(recs, nrec, rec_stride, P, K, wlist, elite);
-        else
-            block_topk<MAXK, NW>(recs, nrec, rec_stride, P, K, wlist, elite);
+        block_topk_rank<NT>(recs, nrec, rec_stride, P, K, elite, tk);
     }
     __syncthreads();
     // record slot of every elite key (needed when rows travel inside the records)
@@ -930,11 +1064,9 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
             }
             float p = tail_pre[5], v = tail_pre[6], r = tail_pre[7], w = tail_pre[8];
             const float c0 = tail_pre[1], c1 = tail_pre[2], c2 = tail_pre[3], c3 = tail_pre[4];
-            const float temp = f[0] * c0 + f[1] * c1 + f[2] * c2 + f[3] * c3;  // integrate()'s order
-            float temp2 = quad_cross(tail_pre[9] - p, f[0]) * c0;
-            temp2 = temp2 + quad_cross(tail_pre[10] - p, f[1]) * c1;
-            temp2 = temp2 + quad_cross(tail_pre[11] - p, f[2]) * c2;
-            temp2 = temp2 + quad_cross(tail_pre[12] - p, f[3]) * c3;
+            const float temp = (f[0] * c0 + f[1] * c1) + (f[2] * c2 + f[3] * c3);  // integrate()'s order
+            const float temp2 = (quad_cross(tail_pre[9] - p, f[0]) * c0 + quad_cross(tail_pre[10] - p, f[1]) * c1) +
+                                (quad_cross(tail_pre[11] - p, f[2]) * c2 + quad_cross(tail_pre[12] - p, f[3]) * c3);
             {  // quad_rb_apply with the LDS copies of inv_m / dt and this lane's constants
                 const float lin = ts[33] * temp + ts[39];
                 const float Rt = rb.R0 * qp<QP_B0>(temp2) + rb.R1 * qp<QP_B1>(temp2) + rb.R2 * qp<QP_B2>(temp2);
@@ -995,7 +1127,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     }
     MERGE_STAMP(5);
     MERGE_MARK(8);
-    if (dbg && threadIdx.x == 0 && blockIdx.x == 0) dbg[9] = __builtin_amdgcn_s_memtime();
+    if (dbg && threadIdx.x == 0 && blockIdx.x < 2) dbg[32 * blockIdx.x + 9] = __builtin_amdgcn_s_memtime();
 #undef MERGE_STAMP
 #undef MERGE_MARK
     if (flag) {  // every thread's output writes have completed before thread 0 publishes `seq`
@@ -1279,7 +1411,9 @@ int merge_blocks(const ModelConst& mc) {
 // LDS staging of the records (merge_body<true>): when the block's records fit beside the merge's own
 // dynamic LDS.  SRBD_MERGE_STAGE=2 turns it off (measurement), SRBD_MERGE_FENCE=2 drops the system
 // fence before the publish flag (outputs are system-scope stores; 1 keeps it).
-constexpr size_t MERGE_LDS_DYN_MAX = 150 * 1024;
+constexpr size_t MERGE_LDS_DYN_MAX = 140 * 1024;  // + the staged merge's static LDS (block_topk_rank) <= 160 KB
+// the exchange kernel's static LDS holds both passes' merge_body arrays: its dynamic limit is this much lower
+constexpr size_t XCHG_LDS_STATIC = 24 * 1024;
 static bool merge_stage_fits(int nrec_block, int rec_stride, int P, int K, size_t* smem) {
     static const int knob = tune_knob("SRBD_MERGE_STAGE", 1);
     const size_t base = merge_smem_bytes(nrec_block, P, K);
@@ -1296,9 +1430,9 @@ static bool merge_stage_fits(int nrec_block, int rec_stride, int P, int K, size_
 void merge_prepare() {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&merge_kernel<MERGE_STAGE_THREADS, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)MERGE_LDS_DYN_MAX);
-    // its static LDS holds both passes' arrays (11 KB): 16 KB less dynamic LDS (launch_merge_xchg)
+    // its static LDS holds both passes' arrays (21 KB): XCHG_LDS_STATIC less dynamic LDS (launch_merge_xchg)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&merge_xchg_kernel<MERGE_STAGE_THREADS, true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(MERGE_LDS_DYN_MAX - 16 * 1024));
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(MERGE_LDS_DYN_MAX - XCHG_LDS_STATIC));
 }
 static int merge_fence_sys() {
     static const int knob = tune_knob("SRBD_MERGE_FENCE", 2);
@@ -1379,10 +1513,10 @@ void launch_merge_xchg(const ModelConst& mc, StepInput* in, const float* recs, i
                        const float* noise, const XchgArgs& x, StepOutput* out, int chain, hipStream_t s, int ctr_inc,
                        Publish pub) {
     // the kernel holds both passes' static LDS (two merge_body instantiations), so the staged records
-    // get 16 KB less dynamic LDS than merge_kernel's
+    // get XCHG_LDS_STATIC less dynamic LDS than merge_kernel's
     size_t smem = 0;
     bool stage = merge_stage_fits(nrec, rec_stride, mc.P, mc.K, &smem);
-    if (stage && smem > MERGE_LDS_DYN_MAX - 16 * 1024) {
+    if (stage && smem > MERGE_LDS_DYN_MAX - XCHG_LDS_STATIC) {
         stage = false;
         smem = merge_smem_bytes(nrec, mc.P, mc.K);
     }

@@ -441,11 +441,19 @@ class Context:
         return out
 
     def merge_phases(self, iters: int = 50):
-        out = np.zeros(24, np.float32)
+        """Merge phase durations (us) of block 0; `slice_block`: the same for block 1 of a column-split merge."""
+        out = np.zeros(48, np.float32)
         self.check(lib.srbd_debug_merge_phases(self.h, int(iters), fptr(out)), "srbd_debug_merge_phases")
-        d = dict(zip(("min_key", "weighted_sums", "elite", "outputs", "tail", "staged_at", "tail_prep_at",
-                      "shader_mhz"), (round(float(x), 3) for x in out[:8])))
-        d["marks_us"] = [round(float(x), 3) for x in out[8:]]  # finer marks from the start (0: unset)
+
+        def one(o):
+            d = dict(zip(("min_key", "weighted_sums", "elite", "outputs", "tail", "staged_at", "tail_prep_at",
+                          "shader_mhz"), (round(float(x), 3) for x in o[:8])))
+            d["marks_us"] = [round(float(x), 3) for x in o[8:24]]  # finer marks from the start (0: unset)
+            return d
+
+        d = one(out[:24])
+        if out[24:].any():
+            d["slice_block"] = one(out[24:])
         return d
 
     def set_gait(self, timing, pgg_dt: float, duty_factor: float, freq_set, freq_local=None):
