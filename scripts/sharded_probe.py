@@ -77,7 +77,7 @@ def main():
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
-    w = CONFIGS["c2"]
+    w = CONFIGS[os.environ.get("SHARD_CFG", "c2")]  # e.g. SHARD_CFG=ns: the 8-rank C5 per-rank shape
     transport = sys.argv[1] if len(sys.argv) > 1 else "rccl"
     mpc = ShardedSamplingMPC(make_cfg(_lib, w, w.num_samples, 0, 1, 0), 0, 1, 0, transport=transport)
     s, r, c = inputs(w, 0)
@@ -86,6 +86,7 @@ def main():
         best, _, _ = mpc.step(s, r, c, best, seed=42, counter=k)
     res = {}
     res["transport"] = transport
+    res["workload"] = w.name
     mpc.device_steps(50)
     torch.cuda.synchronize()
     n = 2000
