@@ -37,16 +37,16 @@ int rollout_mode(int kind, int n_local) {
     const char* e = getenv("SRBD_ROLLOUT");
     if (e && !strcmp(e, "thread")) return ROLLOUT_THREAD;
     if (e && !strcmp(e, "quad")) return ROLLOUT_QUAD;
+    if (e && !strcmp(e, "pair")) return ROLLOUT_PAIR;
     const int quad_max = kind == SRBD_ZERO_ORDER ? 65536 : 524288;
     return n_local <= quad_max ? ROLLOUT_QUAD : ROLLOUT_THREAD;
 }
 // Four-lane kernel: 64 samples (4 waves, one per SIMD) per block.  128 samples (2 waves per SIMD)
 // halves the block records but measured 15.7 -> 21.3 us for the C2 rollout (the two waves do slow
-// each other); SRBD_QUAD_SPB=128 selects it for experiments.
+// each other), and the zero-order kernel's LDS noise stage is sized for 64.
 int quad_samples_per_block(int n_local) {
-    const char* e = getenv("SRBD_QUAD_SPB");
     (void)n_local;
-    return (e && atoi(e) == 128) ? 128 : 64;
+    return 64;
 }
 constexpr int MAX_RECORDS = 8192;  // merge_kernel holds 8 record minima per thread x 1024 threads
 }  // namespace
@@ -351,8 +351,9 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     c->mode = rollout_mode(mc.kind, mc.n_local);
     // the four-lane kernel addresses noise through a buffer descriptor (31-bit byte offsets)
     if ((long long)mc.P * mc.ldn * 4 >= (1LL << 31)) c->mode = ROLLOUT_THREAD;
-    c->threads = c->mode == ROLLOUT_QUAD ? 4 * quad_samples_per_block(mc.n_local) : rollout_threads(mc.n_local);
-    const int spb = c->mode == ROLLOUT_QUAD ? c->threads / 4 : c->threads;  // samples per rollout block
+    c->threads = c->mode == ROLLOUT_QUAD ? 4 * quad_samples_per_block(mc.n_local)
+                                         : (c->mode == ROLLOUT_PAIR ? 256 : rollout_threads(mc.n_local));
+    const int spb = rollout_spb(c->mode, c->threads);  // samples per rollout block
     c->nblocks = (mc.n_local + spb - 1) / spb;
     if (c->nblocks > MAX_RECORDS) {
         delete c;

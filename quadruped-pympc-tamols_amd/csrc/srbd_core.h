@@ -257,14 +257,12 @@ struct LdsConst {
 
 // Centroidal_Model_JAX.fd + integrate_jax (CMJ:93-174).  x: 12 evolving states, feet: 12
 // (constant over the rollout), F: 12 clipped foot forces, c: 4 contact flags.
+// The rigid-body part of the step, from the contact-weighted force sum temp = sum_i f_i c_i and torque sum
+// temp2 = sum_i (p_i - p_com) x f_i c_i (integrate_k forms both; the two-lane kernel forms them split over
+// its lanes, rollout_pair_kernel).
 template <class KC>
-SRBD_HD void integrate_k(const KC& kc, float x[12], const float feet[12], const float F[12], const float c[4],
-                         float dt) {
-    // leg sums pairwise, (leg0 + leg1) + (leg2 + leg3): the four-lane kernel forms them with one quad
-    // butterfly over leg-parallel lanes (rollout_quad_kernel), and every layout uses this order
-    float temp[3], lin_acc[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) temp[k] = (F[k] * c[0] + F[3 + k] * c[1]) + (F[6 + k] * c[2] + F[9 + k] * c[3]);
+SRBD_HD void integrate_rb_k(const KC& kc, float x[12], const float temp[3], const float temp2[3], float dt) {
+    float lin_acc[3];
     const float inv_m = kc.inv_m();
     lin_acc[0] = inv_m * temp[0] + 0.0f;
     lin_acc[1] = inv_m * temp[1] + 0.0f;
@@ -274,19 +272,6 @@ SRBD_HD void integrate_k(const KC& kc, float x[12], const float feet[12], const 
     sincos_(x[6], &sr, &cr);
     sincos_(x[7], &sp, &cp);
     sincos_(x[8], &sy, &cy);
-
-    float tc[4][3];  // (p_i - p_com) x f_i * c_i per leg
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const float v[3] = {feet[3 * i] - x[0], feet[3 * i + 1] - x[1], feet[3 * i + 2] - x[2]};
-        float t[3];
-        skew_dot(v, F + 3 * i, t);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) tc[i][k] = t[k] * c[i];
-    }
-    float temp2[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) temp2[k] = (tc[0][k] + tc[1][k]) + (tc[2][k] + tc[3][k]);
 
     float er[3];
     euler_rates(sr, cr, sp, cp, x[9], x[10], x[11], er);
@@ -305,6 +290,31 @@ SRBD_HD void integrate_k(const KC& kc, float x[12], const float feet[12], const 
                          er[0], er[1], er[2], -a1[0] + a2[0], -a1[1] + a2[1], -a1[2] + a2[2]};
 #pragma unroll
     for (int k = 0; k < 12; ++k) x[k] = x[k] + d[k] * dt;
+}
+// (p_i - p_com) x f_i * c_i of one leg (CMJ:100-101).
+SRBD_HD void leg_torque(const float foot[3], const float x[3], const float f[3], float c, float tc[3]) {
+    const float v[3] = {foot[0] - x[0], foot[1] - x[1], foot[2] - x[2]};
+    float t[3];
+    skew_dot(v, f, t);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) tc[k] = t[k] * c;
+}
+template <class KC>
+SRBD_HD void integrate_k(const KC& kc, float x[12], const float feet[12], const float F[12], const float c[4],
+                         float dt) {
+    // leg sums pairwise, (leg0 + leg1) + (leg2 + leg3): the four-lane kernel forms them with one quad
+    // butterfly over leg-parallel lanes (rollout_quad_kernel), the two-lane kernel as one pair sum per
+    // lane plus one exchange (rollout_pair_kernel), and every layout uses this order
+    float temp[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) temp[k] = (F[k] * c[0] + F[3 + k] * c[1]) + (F[6 + k] * c[2] + F[9 + k] * c[3]);
+    float tc[4][3];  // (p_i - p_com) x f_i * c_i per leg
+#pragma unroll
+    for (int i = 0; i < 4; ++i) leg_torque(feet + 3 * i, x, F + 3 * i, c[i], tc[i]);
+    float temp2[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) temp2[k] = (tc[0][k] + tc[1][k]) + (tc[2][k] + tc[3][k]);
+    integrate_rb_k(kc, x, temp, temp2, dt);
 }
 SRBD_HD void integrate(const ModelConst& mc, float x[12], const float feet[12], const float F[12], const float c[4],
                        float dt) {

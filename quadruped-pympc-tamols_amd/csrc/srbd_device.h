@@ -268,10 +268,11 @@ __device__ __forceinline__ void group_topk(const float* st, int rec_stride, int 
     wave_topk(lk, K, out);
 }
 
-__device__ __forceinline__ void group_reduce(const ModelConst& mc, const float* __restrict__ recs, int rec_stride,
-                                             const GroupArgs& grp, int nroll) {
+// st: GROUP_LDS_FLOATS of LDS for the staged records (a kernel that stages its noise in LDS passes that
+// buffer, dead by now; the others a static array of their own, group_reduce below).
+__device__ __forceinline__ void group_reduce_in(const ModelConst& mc, const float* __restrict__ recs, int rec_stride,
+                                                const GroupArgs& grp, int nroll, float* st) {
     __shared__ int last_sh;
-    __shared__ float st[GROUP_LDS_FLOATS];
     __shared__ float sc_sh[GROUP_MAX];
     __shared__ float gh_sh[2];  // beta_g, tag
     __shared__ uint64_t gk_sh[MAXK + 1];
@@ -351,6 +352,11 @@ __device__ __forceinline__ void group_reduce(const ModelConst& mc, const float* 
         G[REC_HDR + P + 2 * tid] = __uint_as_float((uint32_t)kk);
         G[REC_HDR + P + 2 * tid + 1] = __uint_as_float((uint32_t)(kk >> 32));
     }
+}
+__device__ __forceinline__ void group_reduce(const ModelConst& mc, const float* __restrict__ recs, int rec_stride,
+                                             const GroupArgs& grp, int nroll) {
+    __shared__ float st[GROUP_LDS_FLOATS];
+    group_reduce_in(mc, recs, rec_stride, grp, nroll, st);
 }
 
 // Wave sum in a fixed DPP tree (row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15/31); the total
@@ -449,28 +455,55 @@ __device__ __forceinline__ void block_wsum(const ModelConst& mc, const StepInput
     }
 }
 
+// block_wsum with the block's noise staged in LDS, zst[s P + j] (sample-major: consecutive threads read
+// consecutive columns, no bank conflicts), SPB = 64: thread j sums its column's 64 products in sample order
+// exactly as block_wsum's SPB = 64 path does from global memory, so the record is the same bit for bit.
+__device__ __forceinline__ void block_wsum_lds(const ModelConst& mc, const StepInput* __restrict__ in, const float* zst,
+                                               bool zs, const float* e_sh, float* rec) {
+    const int tid = threadIdx.x, T = blockDim.x, P = mc.P;
+    for (int j = tid; j <= P; j += T) {
+        float a = 0.0f;
+        if (j < P) {
+            const float sj = zs ? in->sigma[j] : 1.0f;  // x * 1 == x
+#pragma unroll 16
+            for (int i = 0; i < 64; ++i) a = a + e_sh[i] * (zst[i * P + j] * sj);
+            st_rec(&rec[REC_HDR + j], a);
+        } else {
+#pragma unroll 16
+            for (int i = 0; i < 64; ++i) a = a + e_sh[i];
+            st_rec(&rec[1], a);
+        }
+    }
+}
+
 // Per-block record (see srbd_core.h REC_*): min key, sum_k e_k, sum_k e_k * noise_k[j], top-K keys,
 // e_k = exp(-(c_k - m_b)).  SPB samples per block (multiple of 4); the thread owning sample `sib`
 // passes it (others pass sib = -1) with its `tag` (the gait-adaptive step frequency, else 0), which
 // the owner of the block's best row stores in the record header.  All threads of the block must call
 // this.
+// CEMT: a CEM kernel (K >= 2: the top-K by ranks); the others have K = 1 and carry no top-K code or LDS.
+// ZS: the block's noise is staged in LDS (sample-major, SPB = 64, block_wsum_lds), and the group
+// reduction stages its records in that buffer (>= GROUP_LDS_FLOATS floats) once the sums are formed.
+template <bool CEMT, bool ZS = false>
 __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepInput* __restrict__ in, const int SPB,
                                                int sib, bool valid, float cost, const float* __restrict__ noise,
                                                float* __restrict__ recs, int rec_stride, float* e_sh, uint64_t* red,
-                                               uint64_t* elite_sh, bool cemt, float tag, const GroupArgs& grp,
-                                               int nroll) {
+                                               uint64_t* elite_sh, float tag, const GroupArgs& grp, int nroll,
+                                               float* zst = nullptr) {
+    constexpr bool cemt = CEMT;
     const int tid = threadIdx.x;
     const int k0 = blockIdx.x * SPB;
     const uint64_t key = (sib >= 0 && valid) ? cost_key(cost, (uint32_t)(mc.row0 + k0 + sib)) : ~0ull;
     float* rec = recs + (size_t)blockIdx.x * rec_stride;
     const int P = mc.P, K = mc.K;
     uint64_t bkey;
-    if (K == 1) {
+    if (!CEMT || K == 1) {
         bkey = block_min_u64(key, red);
         if (tid == 0) elite_sh[0] = bkey;
-    } else {
+    } else if constexpr (CEMT) {
         // The block's K smallest keys by rank: every sample counts the block's keys below its own (the
-        // `lps` lanes of a sample -- 4 in the four-lane layouts, else 1 -- split the count, summed by DPP),
+        // `lps` lanes of a sample -- 4 in the four-lane layouts, 2 in the two-lane one, else 1 -- split the
+        // count, summed by DPP),
         // and a sample of rank < K stores its key at elite_sh[rank] (keys are unique; invalid samples all
         // carry ~0 and can only fill the tail with ~0).  Two barriers, where K rounds of a block minimum
         // took 2K (C3 rollout: see DESIGN.md).
@@ -483,10 +516,8 @@ __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepI
         const int span = SPB / lps, i0 = part * span;
         int cnt = 0;
         for (int i = 0; i < span; ++i) cnt += ks[i0 + i] < mine ? 1 : 0;
-        if (lps == 4) {
-            cnt += __builtin_amdgcn_mov_dpp(cnt, 0xB1, 0xF, 0xF, true);  // quad lanes (1, 0, 3, 2)
-            cnt += __builtin_amdgcn_mov_dpp(cnt, 0x4E, 0xF, 0xF, true);  // quad lanes (2, 3, 0, 1)
-        }
+        if (lps >= 2) cnt += __builtin_amdgcn_mov_dpp(cnt, 0xB1, 0xF, 0xF, true);  // quad lanes (1, 0, 3, 2)
+        if (lps == 4) cnt += __builtin_amdgcn_mov_dpp(cnt, 0x4E, 0xF, 0xF, true);  // quad lanes (2, 3, 0, 1)
         if (part == 0 && cnt < K) elite_sh[cnt] = mine;
         __syncthreads();
         bkey = elite_sh[0];
@@ -497,7 +528,10 @@ __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepI
         if (sib >= 0) e_sh[sib] = valid ? expf(-1.0f * (cost - m)) : 0.0f;
         __syncthreads();
         const bool zs = cemt && zs_scaled(mc, in);
-        block_wsum(mc, in, SPB, noise + k0, zs, e_sh, rec);
+        if constexpr (ZS)
+            block_wsum_lds(mc, in, zst, zs, e_sh, rec);
+        else
+            block_wsum(mc, in, SPB, noise + k0, zs, e_sh, rec);
     }
     __syncthreads();
     SRBD_RSTAMP(4);
@@ -512,7 +546,12 @@ __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepI
         st_rec(&rec[REC_HDR + P + 2 * tid], u2f((uint32_t)kk));
         st_rec(&rec[REC_HDR + P + 2 * tid + 1], u2f((uint32_t)(kk >> 32)));
     }
-    if (grp.gsize > 1) group_reduce(mc, recs, rec_stride, grp, nroll);
+    if (grp.gsize > 1) {
+        if constexpr (ZS)
+            group_reduce_in(mc, recs, rec_stride, grp, nroll, zst);
+        else
+            group_reduce(mc, recs, rec_stride, grp, nroll);
+    }
 }
 
 // ---- gait-adaptive rollout (centroidal_nmpc_jax_gait_adaptive.py:326-501).

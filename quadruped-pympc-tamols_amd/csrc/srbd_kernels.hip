@@ -179,6 +179,17 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     const int S = CT ? ST : mc.S;
     const int PL = CT ? (KIND == SRBD_ZERO_ORDER ? 3 * HT : (KIND == SRBD_LINEAR_SPLINE ? 3 * (ST + 1) : 12 * ST))
                       : mc.PL;
+    // ZST (zero-order, compile-time horizon): every noise value a lane reads stays in its registers raw (best is
+    // added from an LDS copy at use), and after the horizon the block's 64 x P values go to LDS, sample-major,
+    // where the epilogue's weighted sums read them (block_wsum_lds) instead of reading the noise from L2 / HBM
+    // a second time (N = 65 536: the epilogue was 11 of the rollout's 28 us; scripts/vrun.sh noepi).  64 samples
+    // per block (the launcher's quad block for zero-order).  The group reduction reuses the buffer.  H <= 12:
+    // 38.5 KB of LDS per block keeps four blocks per CU (H = 16 would need 51 KB: three).
+    constexpr bool ZST = CT && KIND == SRBD_ZERO_ORDER && !EXT && HT <= 12;
+    constexpr int PCT = ZST ? 12 * HT : 1;
+    __shared__ float zst[ZST ? (64 * PCT > GROUP_LDS_FLOATS ? 64 * PCT : GROUP_LDS_FLOATS) : 1];
+    __shared__ float bls[ZST ? PCT : 1];
+    __shared__ float sls[ZST && CEMT ? PCT : 1];
     const int tid = threadIdx.x;
     const int q4 = tid & 3;
     const int c = q4 < 3 ? q4 : 2;
@@ -216,6 +227,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     // component, in leg order).
     constexpr bool LEGP = !EXT;
     const int lq = q4;  // this lane's leg in the force phase
+    uint32_t lmask[4];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) lmask[l] = lq == l ? ~0u : 0u;
     float footL[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) footL[q] = st[12 + 3 * lq + q];
@@ -236,6 +250,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     const int voff = (cblk * mc.ldn + k) * 4;
     const float* __restrict__ bl = best + cblk;
     const float* __restrict__ sl = in->sigma + cblk;
+    if constexpr (ZST) {  // best (and sigma) -> LDS; their loads issue ahead of the noise loads (vmcnt is in order)
+        for (int j = tid; j < PCT; j += 256) {
+            bls[j] = best[j];
+            if constexpr (CEMT) sls[j] = in->sigma[j];
+        }
+    }
     auto load_slot = [&](const int i) __attribute__((always_inline)) {
 #pragma unroll
         for (int l = 0; l < (LEGP ? 3 : 4); ++l) {
@@ -244,8 +264,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
             const int jr = LEGP ? (KIND == SRBD_ZERO_ORDER ? l * HT + i
                                    : (KIND == SRBD_LINEAR_SPLINE ? l * (ST + 1) + i : 10 * (i >> 2) + 4 * l + (i & 3)))
                                 : l * PL + (KIND == SRBD_CUBIC_SPLINE ? 10 * (i >> 2) + (i & 3) : i);
+#ifdef SRBD_DIAG_NOLOAD  // diagnostic build: no noise reads (timing only)
+            const float nzv = (float)(voff + jr * mc.ldn) * 1e-9f;
+#else
             const float nzv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(nrs, voff, jr * mc.ldn * 4, 0));
-            if constexpr (CEMT) {  // unscaled CEM device draws: Z * sigma_j (z * 1 == z; the load unconditional)
+#endif
+            if constexpr (ZST) {
+                pre[l][i] = nzv;  // raw: best is added at use, the value staged for the epilogue
+            } else if constexpr (CEMT) {  // unscaled CEM device draws: Z * sigma_j (z * 1 == z; the load unconditional)
                 const float sj = sl[jr];
                 pre[l][i] = bl[jr] + nzv * (zs ? sj : 1.0f);
             } else {
@@ -274,6 +300,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
 #pragma unroll
         for (int i = 0; i < PW; ++i) load_slot(i);
     }
+    if constexpr (ZST) {  // the LDS copy of best is complete (the noise loads stay in flight)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
 
     float dep = p;  // step_ptr dependency: set part-way through each step
     auto step = [&](const int n, auto EX) __attribute__((always_inline)) {  // EX: as rollout_kernel
@@ -301,11 +331,17 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
         // (measured 15.9 -> 17.1 us at C2 with the branches)
         float temp, temp2, ex = 0.0f;
         if constexpr (LEGP) {
-            const float clq = lq == 0 ? cl[0] : (lq == 1 ? cl[1] : (lq == 2 ? cl[2] : cl[3]));
+            // this lane's leg's contact value as bit masks (lmask[l] = ~0 on the lanes of leg l): a select chain
+            // here became three nested divergent branches, each with its own scalar load and lgkmcnt(0) wait
+            const float clq = __uint_as_float((__float_as_uint(cl[0]) & lmask[0]) | (__float_as_uint(cl[1]) & lmask[1]) |
+                                              (__float_as_uint(cl[2]) & lmask[2]) | (__float_as_uint(cl[3]) & lmask[3]));
             const int lbase = lq * PL;
             // component q of this leg's decoded force (slot i, parameter j of the leg when not prefetched)
             auto PQ = [&](int q, int i, int j) {
-                if constexpr (CT) {
+                if constexpr (ZST) {  // best + z as load_slot formed it (ZO: j = q H + n, i = n)
+                    if constexpr (CEMT) return bls[lbase + j] + pre[q][i] * (zs ? sls[lbase + j] : 1.0f);
+                    return bls[lbase + j] + pre[q][i];
+                } else if constexpr (CT) {
                     return pre[q][i];
                 } else {
                     const float z = nz[(size_t)(lbase + j) * ldn];
@@ -432,8 +468,18 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     cost = cost + in->cost_feet;  // 0, or NaN when a foot term is non-finite (Q_feet = 0)
     if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
     if (valid && q4 == 0 && costs) costs[k] = cost;
-    block_epilogue(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh,
-                   CEMT, 0.0f, grp, nroll);
+    if constexpr (ZST) {  // the block's noise, sample-major (leg lq's block of columns lq PL .. lq PL + PL - 1)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int i = 0; i < NPRE; ++i) zst[sib * PCT + lq * PL + q * HT + i] = pre[q][i];
+    }
+#ifdef SRBD_DIAG_NOEPI  // diagnostic build: no block epilogue (timing only)
+    if (tid == 0) recs[blockIdx.x] = cost;
+    return;
+#endif
+    block_epilogue<CEMT, ZST>(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red,
+                              elite_sh, 0.0f, grp, nroll, zst);
     SRBD_RSTAMP(5);
 }
 
@@ -557,8 +603,8 @@ __global__ void __launch_bounds__(512) rollout_ga_quad_kernel(const ModelConst m
     cost = cost + (df * 100.0f) * df;  // GA:500
     if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
     if (valid && q4 == 0 && costs) costs[k] = cost;
-    block_epilogue(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh,
-                   false, f, grp, nroll);
+    block_epilogue<false>(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh,
+                          f, grp, nroll);
 }
 
 // ------------------------------------------------------------------ merge
@@ -1285,6 +1331,8 @@ static void launch_rollout_t(const ModelConst& mc, const StepInput* in, const fl
         else
             hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, EXT>), grid, dim3(threads), 0, s, mc, in, noise,
                                costs, recs, rec_stride, job, blocks, grp);
+    } else if (mode == ROLLOUT_PAIR) {
+        launch_rollout_pair(mc, in, noise, costs, recs, rec_stride, threads, s, next, grp);
     } else {
         launch_rollout_thread(mc, in, noise, costs, recs, rec_stride, threads, s, next, grp);
     }
@@ -1301,7 +1349,7 @@ static void launch_rollout_ga(const ModelConst& mc, const StepInput* in, const f
                               const GroupArgs& grp) {
     const RngJob job = next ? *next : RngJob{nullptr, 0, 0, 0, 0};
     const int extra = next ? (rng_grid(mc) < 1024 ? rng_grid(mc) : 1024) : 0;
-    const int spb = mode == ROLLOUT_QUAD ? threads / 4 : threads;
+    const int spb = rollout_spb(mode, threads);
     const int blocks = (mc.n_local + spb - 1) / spb;
     if (mode == ROLLOUT_QUAD && !mc.cost_on) {  // four lanes per sample, `threads` per block
         const dim3 grid(blocks + extra * 256 / threads), block(threads);

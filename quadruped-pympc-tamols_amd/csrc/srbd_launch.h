@@ -37,9 +37,13 @@ struct GroupArgs {
 // CEM, or fewer than GROUP_MIN_BLOCKS blocks); SRBD_GROUP_SIZE overrides (1 disables grouping)
 int group_size(int nblocks, int rec_stride, int method);
 
-// rollout variants: one thread per sample (block = `threads` samples) or four lanes per sample
-// (block = 256 threads = 64 samples)
-enum { ROLLOUT_THREAD = 0, ROLLOUT_QUAD = 1 };
+// rollout variants: one thread per sample (block = `threads` samples), four lanes per sample (block = 256
+// threads = 64 samples) or two lanes per sample (block = 256 threads = 128 samples)
+enum { ROLLOUT_THREAD = 0, ROLLOUT_QUAD = 1, ROLLOUT_PAIR = 2 };
+// samples per rollout block of a mode's `threads`
+inline int rollout_spb(int mode, int threads) {
+    return mode == ROLLOUT_QUAD ? threads / 4 : (mode == ROLLOUT_PAIR ? threads / 2 : threads);
+}
 bool rollout_specialised(int kind, int H, int S);
 // next != NULL: extra blocks of the same launch generate the next step's draws (RngJob) beside the
 // rollout, on the CUs it leaves idle.
@@ -49,6 +53,8 @@ void launch_rollout(const ModelConst& mc, const StepInput* in, const float* nois
 // the thread-per-sample forms (srbd_rollout_thread.hip): plain and gait-adaptive
 void launch_rollout_thread(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
                            int rec_stride, int threads, hipStream_t s, const RngJob* next, const GroupArgs& grp);
+void launch_rollout_pair(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
+                         int rec_stride, int threads, hipStream_t s, const RngJob* next, const GroupArgs& grp);
 void launch_rollout_ga_thread(const ModelConst& mc, const StepInput* in, const float* noise, float* costs,
                               float* recs, int rec_stride, int spb, hipStream_t s, const RngJob* next,
                               const GroupArgs& grp);
