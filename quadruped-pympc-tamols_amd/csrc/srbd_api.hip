@@ -104,6 +104,9 @@ struct srbd_ctx {
     int gsize = 1, ngroups = 0;
     float* d_grec = nullptr;
     uint32_t* d_gcnt = nullptr;
+    // in-launch final merge (final_merge_ok): the rollout's last group writes the host step's outputs
+    bool final_merge = false;
+    uint32_t* d_gdone = nullptr;
     float* d_part = nullptr;  // first-level merge partials (rank-record format)
     hipGraphExec_t g_dev2 = nullptr, g_dev1 = nullptr;
     float* d_ga_freq = nullptr;  // injected per-row step frequencies (gait-adaptive parity mode), ldn floats
@@ -403,6 +406,10 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
             return cleanup_fail("hipMalloc", e);
         if ((e = hipMalloc((void**)&c->d_gcnt, sizeof(uint32_t) * (size_t)c->ngroups)) != hipSuccess)
             return cleanup_fail("hipMalloc", e);
+        c->final_merge = final_merge_ok(mc, c->mode, c->ngroups, c->wrec_stride);
+        if ((e = hipMalloc((void**)&c->d_gdone, sizeof(uint32_t))) != hipSuccess ||
+            (e = hipMemsetAsync(c->d_gdone, 0, sizeof(uint32_t), c->stream)) != hipSuccess)
+            c->final_merge = false;
         if ((e = hipMemsetAsync(c->d_gcnt, 0, sizeof(uint32_t) * (size_t)c->ngroups, c->stream)) != hipSuccess)
             return cleanup_fail("hipMemset", e);
     }
@@ -443,6 +450,7 @@ extern "C" void srbd_destroy(srbd_ctx* c) {
     (void)hipFree(c->d_wrec);
     (void)hipFree(c->d_grec);
     (void)hipFree(c->d_gcnt);
+    (void)hipFree(c->d_gdone);
     (void)hipFree(c->d_part);
     (void)hipFree(c->d_ga_freq);
     if (c->h_in) (void)hipHostFree(c->h_in);
@@ -553,6 +561,19 @@ static int enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput
     const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1, pub.gate};
     GroupArgs grp = grp_of(c);
     grp.gate = pub.gate;
+    // the rollout launch merges and publishes (not for the gait-adaptive rollout or the cost terms, which
+    // srbd_set_gait / srbd_set_cost_terms can switch on after create: other kernels)
+    if (c->final_merge && !mc.ga && !mc.cost_on && out && !rank_out && !chain && pub.flag) {
+        grp.out = out;
+        grp.flag = pub.flag;
+        grp.seq = pub.seq;
+        grp.gdone = c->d_gdone;
+        grp.ngroups = c->ngroups;
+        grp.fence_sys = merge_fence_sys();
+        launch_rollout(mc, c->d_in, c->d_noise[buf], costs ? costs : c->d_costs, c->d_wrec, c->wrec_stride, c->mode,
+                       c->threads, c->stream, fuse_next ? &next : nullptr, grp);
+        return 1;
+    }
     launch_rollout(mc, c->d_in, c->d_noise[buf], costs ? costs : c->d_costs, c->d_wrec, c->wrec_stride, c->mode,
                    c->threads, c->stream, fuse_next ? &next : nullptr, grp);
     return launch_merge_tree(mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, c->d_noise[buf], c->d_part,

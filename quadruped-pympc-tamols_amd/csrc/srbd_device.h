@@ -270,7 +270,9 @@ __device__ __forceinline__ void group_topk(const float* st, int rec_stride, int 
 
 // st: GROUP_LDS_FLOATS of LDS for the staged records (a kernel that stages its noise in LDS passes that
 // buffer, dead by now; the others a static array of their own, group_reduce below).
-__device__ __forceinline__ void group_reduce_in(const ModelConst& mc, const float* __restrict__ recs, int rec_stride,
+// Returns true (every thread of the block) when this block was its group's last arriver and wrote the group
+// record (write-through stores).
+__device__ __forceinline__ bool group_reduce_in(const ModelConst& mc, const float* __restrict__ recs, int rec_stride,
                                                 const GroupArgs& grp, int nroll, float* st) {
     __shared__ int last_sh;
     __shared__ float sc_sh[GROUP_MAX];
@@ -286,7 +288,7 @@ __device__ __forceinline__ void group_reduce_in(const ModelConst& mc, const floa
         last_sh = old == (uint32_t)(nb - 1);
     }
     __syncthreads();
-    if (!last_sh) return;
+    if (!last_sh) return false;
     if (tid == 0) __hip_atomic_store(grp.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
     {  // stage the nb consecutive records (sc1 loads, U per thread in flight)
         constexpr int U = 16;
@@ -338,25 +340,26 @@ __device__ __forceinline__ void group_reduce_in(const ModelConst& mc, const floa
             const int off = j < P ? REC_HDR + j : 1;
             float a = 0.0f;
             for (int i = 0; i < nb; ++i) a = a + sc_sh[i] * st[(size_t)i * rec_stride + off];
-            G[off] = a;
+            st_rec(&G[off], a);
         }
     }
     if (tid == 0) {
-        G[0] = gh_sh[0];
-        if (rs) G[1] = 1.0f;
-        G[2] = __uint_as_float((uint32_t)gk_sh[MAXK]);
-        G[3] = gh_sh[1];
+        st_rec(&G[0], gh_sh[0]);
+        if (rs) st_rec(&G[1], 1.0f);
+        st_rec(&G[2], __uint_as_float((uint32_t)gk_sh[MAXK]));
+        st_rec(&G[3], gh_sh[1]);
     }
     if (tid < K) {
         const uint64_t kk = gk_sh[tid];
-        G[REC_HDR + P + 2 * tid] = __uint_as_float((uint32_t)kk);
-        G[REC_HDR + P + 2 * tid + 1] = __uint_as_float((uint32_t)(kk >> 32));
+        st_rec(&G[REC_HDR + P + 2 * tid], __uint_as_float((uint32_t)kk));
+        st_rec(&G[REC_HDR + P + 2 * tid + 1], __uint_as_float((uint32_t)(kk >> 32)));
     }
+    return true;
 }
 __device__ __forceinline__ void group_reduce(const ModelConst& mc, const float* __restrict__ recs, int rec_stride,
                                              const GroupArgs& grp, int nroll) {
     __shared__ float st[GROUP_LDS_FLOATS];
-    group_reduce_in(mc, recs, rec_stride, grp, nroll, st);
+    (void)group_reduce_in(mc, recs, rec_stride, grp, nroll, st);
 }
 
 // Wave sum in a fixed DPP tree (row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15/31); the total
@@ -485,7 +488,7 @@ __device__ __forceinline__ void block_wsum_lds(const ModelConst& mc, const StepI
 // ZS: the block's noise is staged in LDS (sample-major, SPB = 64, block_wsum_lds), and the group
 // reduction stages its records in that buffer (>= GROUP_LDS_FLOATS floats) once the sums are formed.
 template <bool CEMT, bool ZS = false>
-__device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepInput* __restrict__ in, const int SPB,
+__device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepInput* __restrict__ in, const int SPB,
                                                int sib, bool valid, float cost, const float* __restrict__ noise,
                                                float* __restrict__ recs, int rec_stride, float* e_sh, uint64_t* red,
                                                uint64_t* elite_sh, float tag, const GroupArgs& grp, int nroll,
@@ -548,10 +551,11 @@ __device__ __forceinline__ void block_epilogue(const ModelConst& mc, const StepI
     }
     if (grp.gsize > 1) {
         if constexpr (ZS)
-            group_reduce_in(mc, recs, rec_stride, grp, nroll, zst);
+            return group_reduce_in(mc, recs, rec_stride, grp, nroll, zst);
         else
             group_reduce(mc, recs, rec_stride, grp, nroll);
     }
+    return false;
 }
 
 // ---- gait-adaptive rollout (centroidal_nmpc_jax_gait_adaptive.py:326-501).

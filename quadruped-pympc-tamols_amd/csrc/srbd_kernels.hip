@@ -155,12 +155,21 @@ __device__ __forceinline__ float quad_cross(float vl, float fl) {
     return (-vn2) * fn1 + vn1 * fn2;
 }
 
+// The in-launch final merge of the group records (GroupArgs::out), defined after merge_body.
+template <int NT>
+__device__ void final_merge(const ModelConst& mc, const StepInput* in, const float* noise, int rec_stride,
+                            const GroupArgs& grp, float* lds);
+
 template <int KIND, int HT, int ST, bool CEMT, bool EXT>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) rollout_quad_kernel(const ModelConst mc, const StepInput* __restrict__ in,
                                                            const float* __restrict__ noise, float* __restrict__ costs,
                                                            float* __restrict__ recs, int rec_stride,
     const RngJob next_rng, int nroll, const GroupArgs grp) {
-    if (grp.gate && (*grp.gate & ARM_CANCEL)) return;  // armed chain that did not fire: nothing to compute
+    if (grp.gate && (*grp.gate & ARM_CANCEL)) {  // armed chain that did not fire: nothing to compute
+        if (grp.flag && blockIdx.x == 0 && threadIdx.x == 0)  // the in-launch final merge's cancel token
+            __hip_atomic_store(grp.flag, grp.seq | ARM_CANCEL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
     // blocks past the rollout grid generate the next step's noise on the CUs the rollout leaves idle
     SRBD_RSTAMP(0);
     if ((int)blockIdx.x >= nroll) {
@@ -478,8 +487,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     if (tid == 0) recs[blockIdx.x] = cost;
     return;
 #endif
-    block_epilogue<CEMT, ZST>(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red,
-                              elite_sh, 0.0f, grp, nroll, zst);
+    const bool glast = block_epilogue<CEMT, ZST>(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride,
+                                                 e_sh, red, elite_sh, 0.0f, grp, nroll, zst);
+    if constexpr (ZST && !CEMT)
+        if (glast && grp.out) final_merge<256>(mc, in, noise, rec_stride, grp, zst);
     SRBD_RSTAMP(5);
 }
 
@@ -725,25 +736,42 @@ __device__ __forceinline__ void block_topk_rank(const float* __restrict__ recs, 
 // Host-published outputs (flag != NULL) are stored system-scope (write-through to the mapped host
 // buffer); after every wave's vmcnt(0) and a barrier the flag store follows them, so the system-wide
 // L2 write-back of __threadfence_system is not needed for them (fence_sys = 1 keeps it).
+// The merge's fixed-size LDS, passed in so a caller can place it (the merge kernels declare it; the zero-order
+// rollout's final merge carves it from its noise stage, rollout_quad_kernel).
+template <int NT>
+struct MergeShared {
+    uint64_t red[NT / 64];
+    uint64_t elite[MAXK];
+    int elite_src[MAXK];
+    TopkLds<NT> tk;  // block_topk_rank
+    float Vs[MAXP + 1];
+    float nb[MAXP];
+    float tag_sh;  // header tag (gait-adaptive step frequency) of the record holding beta's row
+    // tail lanes: StepInput fields (13), the force-independent step (5), the ModelConst values the tail
+    // uses (16) -- read back in one batch (kernarg fields re-read lazily are serial scalar loads)
+    float tail_sh[4][40];
+    float osh[sizeof(StepOutput) / sizeof(float)];  // the step outputs assembled for the burst
+};
+// smem: [STAGE: records] | scale[nrec_pad] | part[G*(ncol+1)] | erow[K*ncol] (merge_smem_bytes).  prestaged
+// (STAGE): the records are already in smem.  The staged body's sums use G = MERGE_STAGE_THREADS / (ncol + 1)
+// record groups whatever NT is, so a 256-thread block merges bit for bit as the 512-thread kernel does.
 template <int NT, bool STAGE>
 __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __restrict__ in,
                                            const float* __restrict__ recs, int nrec, int rec_stride, int rows_in_rec,
                                            const float* __restrict__ noise, float* __restrict__ rank_out,
                                            StepOutput* __restrict__ out, int chain, int ctr_inc,
                                            uint64_t* __restrict__ dbg, uint32_t* __restrict__ flag, uint32_t seq,
-                                           int split_cs = 0, int fence_sys = 1) {
-    extern __shared__ float smem[];  // [STAGE: records] | scale[nrec_pad] | part[G*(ncol+1)] | erow[K*ncol]
+                                           int split_cs, int fence_sys, MergeShared<NT>& sh, float* smem,
+                                           bool prestaged = false) {
     constexpr int NW = NT / 64;
-    __shared__ uint64_t red[NW];
-    __shared__ uint64_t elite[MAXK];
-    __shared__ int elite_src[MAXK];
-    __shared__ TopkLds<NT> tk;  // block_topk_rank
-    __shared__ float Vs[MAXP + 1];
-    __shared__ float nb[MAXP];
-    __shared__ float tag_sh;  // header tag (gait-adaptive step frequency) of the record holding beta's row
-    // tail lanes: StepInput fields (13), the force-independent step (5), the ModelConst values the tail
-    // uses (16) -- read back in one batch (kernarg fields re-read lazily are serial scalar loads)
-    __shared__ float tail_sh[4][40];
+    uint64_t* red = sh.red;
+    uint64_t* elite = sh.elite;
+    int* elite_src = sh.elite_src;
+    TopkLds<NT>& tk = sh.tk;
+    float* Vs = sh.Vs;
+    float* nb = sh.nb;
+    float& tag_sh = sh.tag_sh;
+    auto& tail_sh = sh.tail_sh;
 #define MERGE_STAMP(i) \
     if (dbg && threadIdx.x == 0 && blockIdx.x < 2) dbg[32 * blockIdx.x + (i)] = __builtin_amdgcn_s_memrealtime()
     // finer marks (diagnostic build of the phases call only: dbg[16 + i])
@@ -761,7 +789,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     // Unsplit: the step outputs are assembled in LDS and written out in one burst at the end, so no
     // wave waits for a host store's completion mid-merge (a wave overwriting a register of a pending
     // store waits vmcnt(0), ~1 us for a PCIe write) and the publish waits for one round of them.
-    __shared__ float osh[sizeof(StepOutput) / sizeof(float)];
+    float* osh = sh.osh;
     const bool shadow = !split;
     auto ostore = [&](void* dst, float v) {
         if (shadow)
@@ -772,7 +800,9 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         else
             *reinterpret_cast<float*>(dst) = v;
     };
-    if (!split && gridDim.x > 1) {  // first level of a two-level merge: block b reduces its slice into rank_out[b]
+    // first level of a two-level merge: block b reduces its slice into rank_out[b] (a merge inside another
+    // launch -- final_merge -- has gridDim > 1 but no rank_out)
+    if (!split && rank_out && gridDim.x > 1) {
         // 32-bit: blockIdx.x * nrec < 64 * MAX_RECORDS (a 64-bit division is a ~100-instruction sequence)
         const int b0 = (int)(blockIdx.x * (uint32_t)nrec / gridDim.x),
                   b1 = (int)((blockIdx.x + 1) * (uint32_t)nrec / gridDim.x);
@@ -788,7 +818,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     auto owns = [&](int jj) { return !split || tailblk || !is_tail_col(mc, jj); };
     const bool do_tail = out && (!split || tailblk);
     const int cols = ncol + 1;
-    int G = T / cols;
+    int G = (STAGE ? MERGE_STAGE_THREADS : T) / cols;
     G = G < 1 ? 1 : (G > nrec ? nrec : G);
     const int nrec_pad = (nrec + 3) & ~3;
     float* stage = smem;
@@ -860,8 +890,12 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
                 if (i < n4) dst[i] = v[u];
             }
         };
-        chunk(0, true);
-        for (int base = U * T; base < n4; base += U * T) chunk(base, false);
+        if (prestaged) {
+            tail_prep();
+        } else {
+            chunk(0, true);
+            for (int base = U * T; base < n4; base += U * T) chunk(base, false);
+        }
         __syncthreads();
         MERGE_STAMP(6);
         recs = stage;
@@ -1206,8 +1240,73 @@ __global__ void __launch_bounds__(NT) merge_kernel(const ModelConst mc, StepInpu
                                __HIP_MEMORY_SCOPE_SYSTEM);
         return;
     }
+    __shared__ MergeShared<NT> sh;
+    extern __shared__ float dsm[];
     merge_body<NT, STAGE>(mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag,
-                      seq, split_cs, fence_sys);
+                          seq, split_cs, fence_sys, sh, dsm);
+}
+
+// In-launch final merge (zero-order four-lane rollout, host steps; launch_rollout with GroupArgs::out): a
+// group's last arriver, its group record stored write-through, counts itself in *gdone; the block that
+// completes the count (every group record is then in memory) copies the ngroups records into LDS with sc1
+// loads and runs the single-block merge on them -- merge_body<NT, STAGE> with the record groups of the
+// 512-thread kernel, so the outputs are merge_kernel's bit for bit -- writing the step outputs and
+// publishing `seq` (and resets the count for the next launch).  The merge's LDS is carved from the rollout's
+// noise stage, dead by then (final_merge_lds).  Saves the merge launch and its record staging: N = 65 536
+// (see DESIGN.md).
+template <int NT>
+__device__ void final_merge(const ModelConst& mc, const StepInput* in, const float* noise, int rec_stride,
+                            const GroupArgs& grp, float* lds) {
+    __shared__ int fin;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's group record stores have completed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(grp.gdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fin = old == (uint32_t)(grp.ngroups - 1);
+    }
+    __syncthreads();
+    if (!fin) return;
+    if (threadIdx.x == 0) __hip_atomic_store(grp.gdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    MergeShared<NT>& sh = *reinterpret_cast<MergeShared<NT>*>(lds);
+    float* smem = lds + (sizeof(MergeShared<NT>) + 15) / 16 * 4;  // 16-byte aligned
+    const int n = grp.ngroups * rec_stride;
+    constexpr int U = 16;  // sc1 loads in flight per thread (other CUs wrote the records)
+    for (int i0 = 0; i0 < n; i0 += U * NT) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * NT + (int)threadIdx.x;
+            v[u] = i < n ? ld_rec(grp.grecs + i) : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * NT + (int)threadIdx.x;
+            if (i < n) smem[i] = v[u];
+        }
+    }
+    __syncthreads();
+    merge_body<NT, true>(mc, const_cast<StepInput*>(in), smem, grp.ngroups, rec_stride, 0, noise, nullptr, grp.out, 0,
+                         0, nullptr, grp.flag, grp.seq, 0, grp.fence_sys, sh, smem, true);
+}
+
+size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride) {
+    const int cols = mc.P + 1;
+    int G = MERGE_STAGE_THREADS / cols;
+    G = G < 1 ? 1 : (G > ngroups ? ngroups : G);
+    const size_t fl = (size_t)ngroups * rec_stride + (size_t)((ngroups + 3) & ~3) + (size_t)((G * cols + 3) & ~3) +
+                      (size_t)mc.K * mc.P;
+    return (sizeof(MergeShared<256>) + 15) / 16 * 16 + sizeof(float) * fl;
+}
+
+// The zero-order four-lane kernel with the LDS noise stage (ZST: H 10 / 12, no cost terms), MPPI / random
+// sampling, grouped records, and the merge's LDS inside the stage (64 x 12 H floats).
+bool final_merge_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride) {
+    const char* e = getenv("SRBD_FINAL_MERGE");  // 0 disables (read per context: tests compare both)
+    // (the gait-adaptive rollout and the cost terms, which can be switched on later, are checked per launch)
+    if ((e && atoi(e) == 0) || mode != ROLLOUT_QUAD || mc.kind != SRBD_ZERO_ORDER) return false;
+    if ((mc.H != 10 && mc.H != 12) || mc.method == SRBD_CEM_MPPI || ngroups < 1) return false;
+    const size_t zst = sizeof(float) * (size_t)(64 * 12 * mc.H > GROUP_LDS_FLOATS ? 64 * 12 * mc.H : GROUP_LDS_FLOATS);
+    return final_merge_lds(mc, ngroups, rec_stride) <= zst;
 }
 
 // Sharded step without a collective launch (xGMI exchange).
@@ -1235,7 +1334,10 @@ __global__ void __launch_bounds__(NT) merge_xchg_kernel(const ModelConst mc, Ste
     const int stride = rec_floats_rank(mc.P, mc.K);
     const uint32_t epoch = *x.epoch + 1;
     float* mine = x.stage + (size_t)x.rank * stride;
-    merge_body<NT, STAGE1>(mc, in, recs, nrec, rec_stride, 0, noise, mine, nullptr, 0, 0, nullptr, nullptr, 0);
+    __shared__ MergeShared<NT> sh;  // both passes (they run one after the other)
+    extern __shared__ float dsm[];
+    merge_body<NT, STAGE1>(mc, in, recs, nrec, rec_stride, 0, noise, mine, nullptr, 0, 0, nullptr, nullptr, 0, 0, 1, sh,
+                           dsm);
     __syncthreads();
     // slot parity: epoch & 1.  A peer can run at most one exchange ahead of this rank (it cannot pass
     // its next wait before this rank has published that epoch, i.e. finished copying this one), so
@@ -1286,7 +1388,8 @@ __global__ void __launch_bounds__(NT) merge_xchg_kernel(const ModelConst mc, Ste
                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     }
     __syncthreads();
-    merge_body<NT, false>(mc, in, x.stage, x.world, stride, 1, noise, nullptr, out, chain, ctr_inc, nullptr, flag, seq);
+    merge_body<NT, false>(mc, in, x.stage, x.world, stride, 1, noise, nullptr, out, chain, ctr_inc, nullptr, flag, seq, 0, 1,
+                          sh, dsm);
 }
 
 __global__ void advance_kernel(const ModelConst mc, StepInput* __restrict__ in, const StepOutput* __restrict__ out) {
@@ -1482,7 +1585,7 @@ void merge_prepare() {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&merge_xchg_kernel<MERGE_STAGE_THREADS, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)(MERGE_LDS_DYN_MAX - XCHG_LDS_STATIC));
 }
-static int merge_fence_sys() {
+int merge_fence_sys() {
     static const int knob = tune_knob("SRBD_MERGE_FENCE", 2);
     return knob == 1 ? 1 : 0;
 }

@@ -32,7 +32,20 @@ struct GroupArgs {
     uint32_t* cnt;  // ngroups arrival counters, zero between launches (each group's last arriver resets its own)
     int gsize;      // blocks per group
     const uint32_t* gate;  // armed chain (Publish::gate): every block exits at once when the chain did not fire
+    // Final merge in the rollout launch (zero-order four-lane kernel, host steps): the last group arriver to
+    // finish counts itself in *gdone; the block that completes the count merges the ngroups group records
+    // into the step outputs `out` and publishes `seq` in `flag`, as merge_kernel would (launch_rollout_final).
+    StepOutput* out = nullptr;
+    uint32_t* flag = nullptr;
+    uint32_t seq = 0;
+    uint32_t* gdone = nullptr;  // zero between launches (the final merger resets it)
+    int ngroups = 0;
+    int fence_sys = 1;
 };
+// LDS the in-launch final merge needs (merge_body<256> of ngroups records) and whether the launch can do it
+size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride);
+bool final_merge_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride);
+int merge_fence_sys();
 // blocks per group for a launch of `nblocks` rollout blocks of `rec_stride`-float records (1: no grouping:
 // CEM, or fewer than GROUP_MIN_BLOCKS blocks); SRBD_GROUP_SIZE overrides (1 disables grouping)
 int group_size(int nblocks, int rec_stride, int method);

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Host-to-host srbd_step times (C-timed, srbd_bench_host_steps) of one workload under environment settings.
+
+Usage: host_ab.py WORKLOAD[:N] STEPS NAME=ENV=VAL[,ENV=VAL] ...   (GPU box; one JSON line per setting)
+Settings are applied when each context is created (knobs read per context, e.g. SRBD_FINAL_MERGE,
+SRBD_GROUP_SIZE), alternating A/B/A/B over three rounds so drift between them cancels.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "quadruped-pympc-tamols_amd"))
+from quadruped_pympc_amd import _lib  # noqa: E402
+from quadruped_pympc_amd.synthetic import CONFIGS, Workload, inputs  # noqa: E402
+
+
+def run(w, steps, env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        cfg = _lib.make_config(num_samples=w.num_samples, horizon=w.horizon, method=w.method,
+                               parametrization=w.parametrization, num_splines=w.num_splines, mass=w.mass,
+                               inertia=w.inertia, dts=np.full(w.horizon, w.dt, np.float32), sigma_mppi=w.sigma)
+        ctx = _lib.Context(cfg)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    s, r, c = inputs(w, 0)
+    states, refs, contacts = np.stack([s] * steps), np.stack([r] * steps), np.stack([c] * steps)
+    sig = np.full(ctx.P, w.sigma, np.float32) if w.method == "cem_mppi" else None
+    ctx.bench_host_steps(states[:50], refs[:50], contacts[:50], np.zeros(ctx.P, np.float32), sig, 1, 0, 50)
+    lat, _, _ = ctx.bench_host_steps(states, refs, contacts, np.zeros(ctx.P, np.float32), sig, 1, 1000, steps)
+    ctx.close()
+    lat = np.asarray(lat, np.float64)  # us
+    return float(lat.mean()), float(np.percentile(lat, 50)), float(np.percentile(lat, 99))
+
+
+def main():
+    key = sys.argv[1]
+    n = None
+    if ":" in key:
+        key, n = key.split(":")
+    w0 = CONFIGS[key]
+    w = Workload(w0.name, w0.robot, w0.gait, w0.method, w0.parametrization, int(n) if n else w0.num_samples,
+                 w0.horizon, w0.num_splines)
+    steps = int(sys.argv[2])
+    settings = []
+    for spec in sys.argv[3:]:
+        name, _, rest = spec.partition("=")
+        env = dict(kv.split("=", 1) for kv in rest.split(",") if kv)
+        settings.append((name, env))
+    res = {name: [] for name, _ in settings}
+    for _ in range(3):
+        for name, env in settings:
+            res[name].append(run(w, steps, env))
+    for name, _ in settings:
+        a = np.array(res[name])
+        print(json.dumps(dict(workload=w.name, N=w.num_samples, setting=name, mean_us=round(float(a[:, 0].mean()), 2),
+                              p50_us=round(float(np.median(a[:, 1])), 2), p99_us=round(float(np.median(a[:, 2])), 2),
+                              rounds=a[:, 1].round(2).tolist())), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -93,6 +93,8 @@ def _same(a, b):
     ("c3", "cem_mppi", "cubic_spline", 4096),
     ("c2", "mppi", "linear_spline", 65536),
     ("c2", "mppi", "zero_order", 131072),   # unfused draws: the armed chain carries the RNG kernel
+    ("c2", "mppi", "zero_order", 65536),    # the rollout launch merges and publishes (final_merge)
+    ("c2", "random_sampling", "zero_order", 40000),
     ("c3", "cem_mppi", "cubic_spline", 70000),
 ])
 def test_armed_chain_bitwise(lib, wkey, method, par, N):
@@ -213,7 +215,7 @@ def test_armed_gait_adaptive_bitwise(lib):
     assert st[0] == (9, 1), st
 
 
-@pytest.mark.parametrize("N", [10000, 131072])
+@pytest.mark.parametrize("N", [10000, 131072, 65536])  # 65 536: the rollout launch publishes the cancel token
 def test_claimed_chain_that_gave_up_reruns_unarmed(lib, N):
     """Round-2 advisor finding: a claim younger than half the deadline whose copy kernel has nevertheless
     timed out (the host was delayed between the claim and the go word) must not return the previous
