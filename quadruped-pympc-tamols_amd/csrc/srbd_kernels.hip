@@ -160,13 +160,15 @@ template <int NT>
 __device__ void final_merge(const ModelConst& mc, const StepInput* in, const float* noise, int rec_stride,
                             const GroupArgs& grp, float* lds);
 
-template <int KIND, int HT, int ST, bool CEMT, bool EXT>
+// FM: the instantiation with the in-launch final merge (launched when GroupArgs::out is set); the others carry
+// none of its code (C2's launch, which never merges in-launch, measured 0.25 us slower with it).
+template <int KIND, int HT, int ST, bool CEMT, bool EXT, bool FM = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) rollout_quad_kernel(const ModelConst mc, const StepInput* __restrict__ in,
                                                            const float* __restrict__ noise, float* __restrict__ costs,
                                                            float* __restrict__ recs, int rec_stride,
     const RngJob next_rng, int nroll, const GroupArgs grp) {
     if (grp.gate && (*grp.gate & ARM_CANCEL)) {  // armed chain that did not fire: nothing to compute
-        if (grp.flag && blockIdx.x == 0 && threadIdx.x == 0)  // the in-launch final merge's cancel token
+        if (FM && blockIdx.x == 0 && threadIdx.x == 0)  // the in-launch final merge's cancel token
             __hip_atomic_store(grp.flag, grp.seq | ARM_CANCEL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
     }
@@ -489,8 +491,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
 #endif
     const bool glast = block_epilogue<CEMT, ZST>(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride,
                                                  e_sh, red, elite_sh, 0.0f, grp, nroll, zst);
-    if constexpr (ZST && !CEMT)
-        if (glast && grp.out) final_merge<256>(mc, in, noise, rec_stride, grp, zst);
+    if constexpr (FM && ZST && !CEMT)
+        if (glast) final_merge<256>(mc, in, noise, rec_stride, grp, zst);
     SRBD_RSTAMP(5);
 }
 
@@ -738,8 +740,10 @@ __device__ __forceinline__ void block_topk_rank(const float* __restrict__ recs, 
 // L2 write-back of __threadfence_system is not needed for them (fence_sys = 1 keeps it).
 // The merge's fixed-size LDS, passed in so a caller can place it (the merge kernels declare it; the zero-order
 // rollout's final merge carves it from its noise stage, rollout_quad_kernel).
+// alignas(16): the dynamic LDS that follows it (staged records, read as float4) starts 16-byte aligned
+// (an 8-byte aligned start cost the C2 merge 1 us)
 template <int NT>
-struct MergeShared {
+struct alignas(16) MergeShared {
     uint64_t red[NT / 64];
     uint64_t elite[MAXK];
     int elite_src[MAXK];
@@ -1241,7 +1245,7 @@ __global__ void __launch_bounds__(NT) merge_kernel(const ModelConst mc, StepInpu
         return;
     }
     __shared__ MergeShared<NT> sh;
-    extern __shared__ float dsm[];
+    extern __shared__ __attribute__((aligned(16))) float dsm[];
     merge_body<NT, STAGE>(mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag,
                           seq, split_cs, fence_sys, sh, dsm);
 }
@@ -1335,7 +1339,7 @@ __global__ void __launch_bounds__(NT) merge_xchg_kernel(const ModelConst mc, Ste
     const uint32_t epoch = *x.epoch + 1;
     float* mine = x.stage + (size_t)x.rank * stride;
     __shared__ MergeShared<NT> sh;  // both passes (they run one after the other)
-    extern __shared__ float dsm[];
+    extern __shared__ __attribute__((aligned(16))) float dsm[];
     merge_body<NT, STAGE1>(mc, in, recs, nrec, rec_stride, 0, noise, mine, nullptr, 0, 0, nullptr, nullptr, 0, 0, 1, sh,
                            dsm);
     __syncthreads();
@@ -1428,6 +1432,13 @@ static void launch_rollout_t(const ModelConst& mc, const StepInput* in, const fl
         const int spb = threads / 4;
         const int blocks = (mc.n_local + spb - 1) / spb;
         const dim3 grid(blocks + extra * 256 / threads);
+        if constexpr (KIND == SRBD_ZERO_ORDER && (HT == 10 || HT == 12) && !EXT) {
+            if (grp.out && !cem) {  // final_merge_ok: the in-launch final merge
+                hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, true>), grid, dim3(threads), 0, s, mc,
+                                   in, noise, costs, recs, rec_stride, job, blocks, grp);
+                return;
+            }
+        }
         if (cem)
             hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, true, EXT>), grid, dim3(threads), 0, s, mc, in, noise,
                                costs, recs, rec_stride, job, blocks, grp);

@@ -45,7 +45,8 @@ def functions(asm):
 
 def mangled(kernel, kind, H, S, cem, ext):
     k = {"quad": "19rollout_quad_kernel", "thread": "14rollout_kernel"}[kernel]
-    return f"_ZN4srbd{k}ILi{kind}ELi{H}ELi{S}ELb{int(cem)}ELb{int(ext)}EEEvNS_10ModelConstEPKNS_9StepInputEPKfPfS7_iNS_6RngJobEiNS_9GroupArgsE"
+    fm = "ELb0" if kernel == "quad" else ""  # the quad kernel's FM (in-launch final merge) flag
+    return f"_ZN4srbd{k}ILi{kind}ELi{H}ELi{S}ELb{int(cem)}ELb{int(ext)}{fm}EEEvNS_10ModelConstEPKNS_9StepInputEPKfPfS7_iNS_6RngJobEiNS_9GroupArgsE"
 
 
 def main():
