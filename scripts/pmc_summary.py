@@ -33,6 +33,9 @@ def per_kernel(d, counter):
 
 
 def short(name):
+    # the four-lane kernel's FM instantiation (the host step's launch with the in-launch final merge) apart
+    if "rollout_quad_kernel" in name and name.split(">")[0].replace(" ", "").endswith(",true"):
+        return "rollout_quad_kernel_fm"
     for key in ("rollout_quad_kernel", "rollout_kernel", "merge_kernel", "rng_kernel", "transpose_kernel",
                 "advance_kernel", "tamols"):
         if key in name:
