@@ -107,6 +107,8 @@ struct srbd_ctx {
     // in-launch final merge (final_merge_ok): the rollout's last group writes the host step's outputs
     bool final_merge = false;
     uint32_t* d_gdone = nullptr;
+    // host steps pass the step input to the rollout as a kernel argument (ks_ok): no upload kernel
+    bool ks = false;
     float* d_part = nullptr;  // first-level merge partials (rank-record format)
     hipGraphExec_t g_dev2 = nullptr, g_dev1 = nullptr;
     float* d_ga_freq = nullptr;  // injected per-row step frequencies (gait-adaptive parity mode), ldn floats
@@ -356,6 +358,7 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     if ((long long)mc.P * mc.ldn * 4 >= (1LL << 31)) c->mode = ROLLOUT_THREAD;
     c->threads = c->mode == ROLLOUT_QUAD ? 4 * quad_samples_per_block(mc.n_local)
                                          : (c->mode == ROLLOUT_PAIR ? 256 : rollout_threads(mc.n_local));
+    c->ks = c->cfg.world_size <= 1 && ks_ok(mc, c->mode);
     const int spb = rollout_spb(c->mode, c->threads);  // samples per rollout block
     c->nblocks = (mc.n_local + spb - 1) / spb;
     if (c->nblocks > MAX_RECORDS) {
@@ -556,11 +559,12 @@ static int merge_nrec(const srbd_ctx* c) { return c->gsize > 1 ? c->ngroups : c-
 // Returns the number of merge blocks that publish (wait_published).
 static int enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput* out, int chain = 0,
                                int ctr_inc = 1, bool fuse_next = false, Publish pub = {nullptr, 0},
-                               float* costs = nullptr) {
+                               float* costs = nullptr, const StepInputK* ksi = nullptr) {
     const ModelConst& mc = c->mc;
     const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1, pub.gate};
     GroupArgs grp = grp_of(c);
     grp.gate = pub.gate;
+    grp.ksi = ksi;
     // the rollout launch merges and publishes (not for the gait-adaptive rollout or the cost terms, which
     // srbd_set_gait / srbd_set_cost_terms can switch on after create: other kernels)
     if (c->final_merge && !mc.ga && !mc.cost_on && out && !rank_out && !chain && pub.flag) {
@@ -700,13 +704,19 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
     // the unarmed launch of this call (also the fallback of a claimed chain that had already given up)
     auto launch_unarmed = [&]() -> int {
         int r;
-        if ((r = upload_input(c))) return r;
+        // the step input as the rollout's kernel argument (its block 0 writes the device copy), or uploaded
+        StepInputK ksi;
+        const bool ks = c->ks && !c->mc.ga && !c->mc.cost_on;
+        if (ks)
+            memcpy(&ksi, c->h_in, offsetof(StepInput, best) + sizeof(float) * (size_t)c->mc.P);
+        else if ((r = upload_input(c)))
+            return r;
         int buf = 0;
         if ((r = acquire_noise(c, noise, seed, counter, &buf))) return r;
         const bool fuse = !noise && fusable(c);
         const Publish pub{c->d_flag, ++c->seq, nullptr};
         seq = pub.seq;
-        nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fuse, pub);
+        nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fuse, pub, nullptr, ks ? &ksi : nullptr);
         HIP_TRY(c, hipGetLastError());
         if (fuse) {
             c->pref_valid = true;

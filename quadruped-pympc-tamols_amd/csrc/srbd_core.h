@@ -83,6 +83,20 @@ static_assert(sizeof(StepInput) % 16 == 0 && offsetof(StepInput, best) % 16 == 0
                   offsetof(StepInput, sigma) % 16 == 0,
               "StepInput is copied in 16-byte words (P is a multiple of 12, so P floats are too)");
 
+// A host step's input passed by value as a kernel argument (KS rollout launches, srbd_step): StepInput's
+// prefix up to best[KSI_MAXP] -- no sigma, so MPPI / random sampling only.  The launch's block 0 writes it to
+// the device StepInput, which the merge and any later reader use; no upload kernel runs.
+constexpr int KSI_MAXP = 192;
+struct StepInputK {
+    unsigned char head[offsetof(StepInput, best)];
+    float best[KSI_MAXP];
+};
+static_assert(offsetof(StepInputK, best) == offsetof(StepInput, best) && sizeof(StepInputK) % 16 == 0,
+              "StepInputK is StepInput's prefix, copied in 16-byte words");
+struct KsNone {  // the kernel argument of launches that read the device StepInput
+    int unused;
+};
+
 struct StepOutput {
     float best[MAXP];
     float sigma[MAXP];

@@ -162,11 +162,31 @@ __device__ void final_merge(const ModelConst& mc, const StepInput* in, const flo
 
 // FM: the instantiation with the in-launch final merge (launched when GroupArgs::out is set); the others carry
 // none of its code (C2's launch, which never merges in-launch, measured 0.25 us slower with it).
-template <int KIND, int HT, int ST, bool CEMT, bool EXT, bool FM = false>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) rollout_quad_kernel(const ModelConst mc, const StepInput* __restrict__ in,
+// KS: the host step's input arrives by value (StepInputK, GroupArgs::ksi); block 0 writes it to the device
+// StepInput `in_dev` for the merge and later readers, so the step needs no upload kernel (one dependent launch
+// and a PCIe read fewer).
+template <int KIND, int HT, int ST, bool CEMT, bool EXT, bool FM = false, bool KS = false>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) rollout_quad_kernel(
+                                                           const std::conditional_t<KS, StepInputK, KsNone> ksi,
+                                                           const ModelConst mc, const StepInput* __restrict__ in_dev,
                                                            const float* __restrict__ noise, float* __restrict__ costs,
                                                            float* __restrict__ recs, int rec_stride,
     const RngJob next_rng, int nroll, const GroupArgs grp) {
+    const StepInput* __restrict__ in;
+    if constexpr (KS) {
+        // ksi is the first kernel argument: read it where it lies in the kernarg segment (taking &ksi makes
+        // the compiler copy the struct to scratch once lanes index it)
+        (void)ksi;
+        const auto ka = (const __attribute__((address_space(4))) StepInput*)__builtin_amdgcn_kernarg_segment_ptr();
+        in = (const StepInput*)ka;
+        if (blockIdx.x == 0) {
+            const auto src = (const __attribute__((address_space(4))) uint32_t*)ka;
+            uint32_t* dst = reinterpret_cast<uint32_t*>(const_cast<StepInput*>(in_dev));
+            for (int i = threadIdx.x; i < (int)(sizeof(StepInputK) / 4); i += blockDim.x) dst[i] = src[i];
+        }
+    } else {
+        in = in_dev;
+    }
     if (grp.gate && (*grp.gate & ARM_CANCEL)) {  // armed chain that did not fire: nothing to compute
         if (FM && blockIdx.x == 0 && threadIdx.x == 0)  // the in-launch final merge's cancel token
             __hip_atomic_store(grp.flag, grp.seq | ARM_CANCEL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1304,6 +1324,14 @@ size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride) {
 
 // The zero-order four-lane kernel with the LDS noise stage (ZST: H 10 / 12, no cost terms), MPPI / random
 // sampling, grouped records, and the merge's LDS inside the stage (64 x 12 H floats).
+// The step input as a kernel argument (StepInputK): the zero-order four-lane kernel with the LDS noise stage,
+// MPPI / random sampling (no sigma in the argument), P <= KSI_MAXP; SRBD_KS=0 disables (read per context).
+bool ks_ok(const ModelConst& mc, int mode) {
+    const char* e = getenv("SRBD_KS");
+    if ((e && atoi(e) == 0) || mode != ROLLOUT_QUAD || mc.kind != SRBD_ZERO_ORDER) return false;
+    return (mc.H == 10 || mc.H == 12) && mc.method != SRBD_CEM_MPPI && mc.P <= KSI_MAXP;
+}
+
 bool final_merge_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride) {
     const char* e = getenv("SRBD_FINAL_MERGE");  // 0 disables (read per context: tests compare both)
     // (the gait-adaptive rollout and the cost terms, which can be switched on later, are checked per launch)
@@ -1433,17 +1461,27 @@ static void launch_rollout_t(const ModelConst& mc, const StepInput* in, const fl
         const int blocks = (mc.n_local + spb - 1) / spb;
         const dim3 grid(blocks + extra * 256 / threads);
         if constexpr (KIND == SRBD_ZERO_ORDER && (HT == 10 || HT == 12) && !EXT) {
+            if (!cem && grp.ksi) {  // ks_ok: the step input as a kernel argument
+                if (grp.out)
+                    hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, true, true>), grid, dim3(threads),
+                                       0, s, *grp.ksi, mc, in, noise, costs, recs, rec_stride, job, blocks, grp);
+                else
+                    hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, false, true>), grid,
+                                       dim3(threads), 0, s, *grp.ksi, mc, in, noise, costs, recs, rec_stride, job, blocks,
+                                       grp);
+                return;
+            }
             if (grp.out && !cem) {  // final_merge_ok: the in-launch final merge
-                hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, true>), grid, dim3(threads), 0, s, mc,
-                                   in, noise, costs, recs, rec_stride, job, blocks, grp);
+                hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, true>), grid, dim3(threads), 0, s, KsNone{},
+                                   mc, in, noise, costs, recs, rec_stride, job, blocks, grp);
                 return;
             }
         }
         if (cem)
-            hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, true, EXT>), grid, dim3(threads), 0, s, mc, in, noise,
+            hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, true, EXT>), grid, dim3(threads), 0, s, KsNone{}, mc, in, noise,
                                costs, recs, rec_stride, job, blocks, grp);
         else
-            hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, EXT>), grid, dim3(threads), 0, s, mc, in, noise,
+            hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, EXT>), grid, dim3(threads), 0, s, KsNone{}, mc, in, noise,
                                costs, recs, rec_stride, job, blocks, grp);
     } else if (mode == ROLLOUT_PAIR) {
         launch_rollout_pair(mc, in, noise, costs, recs, rec_stride, threads, s, next, grp);
@@ -1495,7 +1533,12 @@ static void launch_rollout_ga(const ModelConst& mc, const StepInput* in, const f
 }
 
 void launch_rollout(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
-                    int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next, const GroupArgs& grp) {
+                    int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next, const GroupArgs& grp_in) {
+    GroupArgs grp = grp_in;
+    if (grp.ksi && (mc.ga || mc.cost_on || !ks_ok(mc, mode))) {  // no KS kernel for this launch: upload instead
+        (void)hipMemcpyAsync(const_cast<StepInput*>(in), grp.ksi, sizeof(StepInputK), hipMemcpyHostToDevice, s);
+        grp.ksi = nullptr;
+    }
     if (mc.ga) return launch_rollout_ga(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next, grp);
     const int H = mc.H, S = mc.S;
     // the opt-in cost terms (mc.cost_on): the EXT instantiations, on the same compile-time shapes (with

@@ -41,7 +41,11 @@ struct GroupArgs {
     uint32_t* gdone = nullptr;  // zero between launches (the final merger resets it)
     int ngroups = 0;
     int fence_sys = 1;
+    // host steps: the step input by value (host memory, read by the launcher): the rollout takes it as a
+    // kernel argument and writes the device StepInput itself (ks_ok), no upload kernel
+    const StepInputK* ksi = nullptr;
 };
+bool ks_ok(const ModelConst& mc, int mode);
 // LDS the in-launch final merge needs (merge_body<256> of ngroups records) and whether the launch can do it
 size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride);
 bool final_merge_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride);
