@@ -358,7 +358,7 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     if ((long long)mc.P * mc.ldn * 4 >= (1LL << 31)) c->mode = ROLLOUT_THREAD;
     c->threads = c->mode == ROLLOUT_QUAD ? 4 * quad_samples_per_block(mc.n_local)
                                          : (c->mode == ROLLOUT_PAIR ? 256 : rollout_threads(mc.n_local));
-    c->ks = c->cfg.world_size <= 1 && ks_ok(mc, c->mode);
+    c->ks = ks_ok(mc, c->mode);  // srbd_step, and the xGMI sharded step (xg_step)
     const int spb = rollout_spb(c->mode, c->threads);  // samples per rollout block
     c->nblocks = (mc.n_local + spb - 1) / spb;
     if (c->nblocks > MAX_RECORDS) {
@@ -1363,11 +1363,14 @@ extern "C" int srbd_xgmi_disconnect(srbd_ctx* c) {
 }
 
 // rollout (+ next draws) -> merge_xchg (rank record out to every mailbox, wait, merge the W records)
-static void enqueue_xchg_step(srbd_ctx* c, int buf, StepOutput* out, int chain, bool fuse_next, Publish pub) {
+static void enqueue_xchg_step(srbd_ctx* c, int buf, StepOutput* out, int chain, bool fuse_next, Publish pub,
+                              const StepInputK* ksi = nullptr) {
     const ModelConst& mc = c->mc;
     const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1};
+    GroupArgs grp = grp_of(c);
+    grp.ksi = ksi;  // the step input as the rollout's kernel argument (its block 0 writes the device copy)
     launch_rollout(mc, c->d_in, c->d_noise[buf], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
-                   c->stream, fuse_next ? &next : nullptr, grp_of(c));
+                   c->stream, fuse_next ? &next : nullptr, grp);
     launch_merge_xchg(mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, c->d_noise[buf], c->xa, out, chain,
                       c->stream, 1, pub);
 }
@@ -1422,12 +1425,17 @@ static int xg_step(srbd_ctx* c, const float* state, const float* ref, const floa
     int rc = fill_input(&c->cfg, c->mc, c->h_in, state, ref, contact, contact_stride, best, sigma, seed, counter);
     if (rc) return fail(c, rc, "invalid step arguments");
     c->h_in->noise_scaled = noise_local ? 1 : 0;
-    if ((rc = upload_input(c))) return rc;
+    StepInputK ksi;  // as srbd_step: the rollout's kernel argument, or the upload kernel
+    const bool ks = c->ks && !c->mc.ga && !c->mc.cost_on;
+    if (ks)
+        memcpy(&ksi, c->h_in, offsetof(StepInput, best) + sizeof(float) * (size_t)c->mc.P);
+    else if ((rc = upload_input(c)))
+        return rc;
     int buf = 0;
     if ((rc = acquire_noise(c, noise_local, seed, counter, &buf))) return rc;
     const bool fuse = !noise_local && fusable(c);
     const Publish pub{c->d_flag, ++c->seq};
-    enqueue_xchg_step(c, buf, c->d_out_host, 0, fuse, pub);
+    enqueue_xchg_step(c, buf, c->d_out_host, 0, fuse, pub, ks ? &ksi : nullptr);
     HIP_TRY(c, hipGetLastError());
     if (fuse) {
         c->pref_valid = true;
