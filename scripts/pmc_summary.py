@@ -33,9 +33,12 @@ def per_kernel(d, counter):
 
 
 def short(name):
-    # the four-lane kernel's FM instantiation (the host step's launch with the in-launch final merge) apart
-    if "rollout_quad_kernel" in name and name.split(">")[0].replace(" ", "").endswith(",true"):
-        return "rollout_quad_kernel_fm"
+    # the four-lane kernel's instantiations apart: <KIND, H, S, CEM, EXT, FM, KS> -- FM the in-launch final
+    # merge, KS the step input as kernel argument (both: the host step's launch)
+    if "rollout_quad_kernel<" in name:
+        args = name.split("<", 1)[1].split(">")[0].replace(" ", "").split(",")
+        tag = ("_fm" if len(args) > 5 and args[5] == "true" else "") + ("_ks" if len(args) > 6 and args[6] == "true" else "")
+        return "rollout_quad_kernel" + tag
     for key in ("rollout_quad_kernel", "rollout_kernel", "merge_kernel", "rng_kernel", "transpose_kernel",
                 "advance_kernel", "tamols"):
         if key in name:
@@ -55,7 +58,9 @@ def main():
         k = short(name)
         kernels[k] = {"fetch_bytes": 2 * f * 1024, "write_bytes": w * 1024, "dispatches": [nf, nw],
                       "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024}
-    roll = kernels.get("rollout_quad_kernel") or kernels.get("rollout_kernel")
+    # the host step's rollout launch (fused next-step draws), as the bench's roofline times it
+    roll = (kernels.get("rollout_quad_kernel_fm_ks") or kernels.get("rollout_quad_kernel_ks")
+            or kernels.get("rollout_quad_kernel") or kernels.get("rollout_kernel"))
     res = {"kernels": kernels, "rollout_hbm_bytes_per_launch": roll["hbm_bytes_per_launch"] if roll else None,
            "note": "FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md HBM section) + WRITE_SIZE, KiB->bytes"}
     print(json.dumps(res, indent=1))
