@@ -5,8 +5,8 @@ SRBD_GROUP_SIZE): the rollout launch's last group arriver merges the group recor
 outputs itself, with no merge launch.  It runs merge_kernel's staged body with the 512-thread kernel's record
 groups, so every output must equal the separate merge's (SRBD_FINAL_MERGE=0, read per context) bit for bit:
 device draws and injected noise, MPPI and random sampling, ragged groups, H 10 and 12, many launches in a row
-(the done-counter resets), and host steps interleaved with device-resident chains (which keep the separate
-merge: they write the warm start back into the step input).
+(the done-counter resets), and host steps interleaved with device-resident chains (whose final merge writes
+the warm start back into the step input and advances the RNG counter after the launch's draw blocks).
 """
 import zlib
 
@@ -55,8 +55,9 @@ def test_final_merge_bitwise(lib, monkeypatch, method, N, H, gsize, noise):
 
 
 def test_final_merge_sequence_with_device_chains(lib, monkeypatch):
-    """Host steps (final merge) and device-resident chains (separate merge) on one context, against a context
-    with the final merge off: the done counter resets every launch and the two merges agree bit for bit."""
+    """Host steps and device-resident chains on one context (both with the in-launch final merge), against a
+    context with it off: the done counters reset every launch, the chain's warm start and RNG counter come back
+    the same (the counter advanced only after the launch's draw blocks have read it), bit for bit."""
     case = make_case("c2", N=65536, seed=21)
     ctxs = {}
     for fm in ("0", "1"):
@@ -72,8 +73,10 @@ def test_final_merge_sequence_with_device_chains(lib, monkeypatch):
                 best, _, r, costs = ctx.step(case["state"], case["ref"], case["contact"], best, seed=3, counter=k,
                                              want_costs=True)
                 seq.append((best.copy(), np.array(r.grf), r.best_index, costs))
-                if k in (4, 8):
+                if k in (4, 8):  # device chains (their final merge writes the warm start and the counter back)
                     ctx.bench_device_steps(10)
+                    b2, _, seed2, ctr2 = ctx.get_state()
+                    seq.append((np.asarray(b2), seed2, ctr2))
                     ctx.set_state(best, None, 3, 100 + k)
             outs[fm] = seq
         for x, y in zip(outs["0"], outs["1"]):
