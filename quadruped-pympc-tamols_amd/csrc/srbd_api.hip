@@ -559,7 +559,7 @@ static int merge_nrec(const srbd_ctx* c) { return c->gsize > 1 ? c->ngroups : c-
 // Returns the number of merge blocks that publish (wait_published).
 static int enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput* out, int chain = 0,
                                int ctr_inc = 1, bool fuse_next = false, Publish pub = {nullptr, 0},
-                               float* costs = nullptr, const StepInputK* ksi = nullptr) {
+                               float* costs = nullptr, const void* ksi = nullptr) {
     const ModelConst& mc = c->mc;
     const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1, pub.gate};
     GroupArgs grp = grp_of(c);
@@ -1364,7 +1364,7 @@ extern "C" int srbd_xgmi_disconnect(srbd_ctx* c) {
 
 // rollout (+ next draws) -> merge_xchg (rank record out to every mailbox, wait, merge the W records)
 static void enqueue_xchg_step(srbd_ctx* c, int buf, StepOutput* out, int chain, bool fuse_next, Publish pub,
-                              const StepInputK* ksi = nullptr) {
+                              const void* ksi = nullptr) {
     const ModelConst& mc = c->mc;
     const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1};
     GroupArgs grp = grp_of(c);

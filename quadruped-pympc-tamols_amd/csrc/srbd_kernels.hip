@@ -1328,7 +1328,8 @@ size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride) {
 // MPPI / random sampling (no sigma in the argument), P <= KSI_MAXP; SRBD_KS=0 disables (read per context).
 bool ks_ok(const ModelConst& mc, int mode) {
     const char* e = getenv("SRBD_KS");
-    if ((e && atoi(e) == 0) || mode != ROLLOUT_QUAD || mc.kind != SRBD_ZERO_ORDER) return false;
+    if ((e && atoi(e) == 0) || (mode != ROLLOUT_QUAD && mode != ROLLOUT_THREAD) || mc.kind != SRBD_ZERO_ORDER)
+        return false;
     return (mc.H == 10 || mc.H == 12) && mc.method != SRBD_CEM_MPPI && mc.P <= KSI_MAXP;
 }
 
@@ -1464,10 +1465,10 @@ static void launch_rollout_t(const ModelConst& mc, const StepInput* in, const fl
             if (!cem && grp.ksi) {  // ks_ok: the step input as a kernel argument
                 if (grp.out)
                     hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, true, true>), grid, dim3(threads),
-                                       0, s, *grp.ksi, mc, in, noise, costs, recs, rec_stride, job, blocks, grp);
+                                       0, s, *static_cast<const StepInputK*>(grp.ksi), mc, in, noise, costs, recs, rec_stride, job, blocks, grp);
                 else
                     hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, false, true>), grid,
-                                       dim3(threads), 0, s, *grp.ksi, mc, in, noise, costs, recs, rec_stride, job, blocks,
+                                       dim3(threads), 0, s, *static_cast<const StepInputK*>(grp.ksi), mc, in, noise, costs, recs, rec_stride, job, blocks,
                                        grp);
                 return;
             }

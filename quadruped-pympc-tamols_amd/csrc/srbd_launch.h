@@ -43,7 +43,7 @@ struct GroupArgs {
     int fence_sys = 1;
     // host steps: the step input by value (host memory, read by the launcher): the rollout takes it as a
     // kernel argument and writes the device StepInput itself (ks_ok), no upload kernel
-    const StepInputK* ksi = nullptr;
+    const void* ksi = nullptr;  // a StepInputK
 };
 bool ks_ok(const ModelConst& mc, int mode);
 // LDS the in-launch final merge needs (merge_body<256> of ngroups records) and whether the launch can do it

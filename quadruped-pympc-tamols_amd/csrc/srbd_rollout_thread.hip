@@ -13,11 +13,28 @@
 namespace srbd {
 
 // One thread per sample.  Best throughput when samples fill the GPU (>= ~1 wave per SIMD).
-template <int KIND, int HT, int ST, bool CEMT, bool EXT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == SRBD_ZERO_ORDER ? 4 : 1))) rollout_kernel(const ModelConst mc, const StepInput* __restrict__ in,
+// KS: the host step's input by value (the first kernel argument, read in place from the kernarg segment; block
+// 0 writes the device StepInput `in_dev`), as rollout_quad_kernel does.
+template <int KIND, int HT, int ST, bool CEMT, bool EXT, bool KS = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == SRBD_ZERO_ORDER ? 4 : 1))) rollout_kernel(
+                                                      const std::conditional_t<KS, StepInputK, KsNone> ksi,
+                                                      const ModelConst mc, const StepInput* __restrict__ in_dev,
                                                       const float* __restrict__ noise, float* __restrict__ costs,
                                                       float* __restrict__ recs, int rec_stride,
     const RngJob next_rng, int nroll, const GroupArgs grp) {
+    const StepInput* __restrict__ in;
+    if constexpr (KS) {
+        (void)ksi;
+        const auto ka = (const __attribute__((address_space(4))) StepInput*)__builtin_amdgcn_kernarg_segment_ptr();
+        in = (const StepInput*)ka;
+        if (blockIdx.x == 0) {
+            const auto src = (const __attribute__((address_space(4))) uint32_t*)ka;
+            uint32_t* dst = reinterpret_cast<uint32_t*>(const_cast<StepInput*>(in_dev));
+            for (int i = threadIdx.x; i < (int)(sizeof(StepInputK) / 4); i += blockDim.x) dst[i] = src[i];
+        }
+    } else {
+        in = in_dev;
+    }
     if (grp.gate && (*grp.gate & ARM_CANCEL)) return;  // armed chain that did not fire: nothing to compute
     // blocks past the rollout grid generate the next step's noise on the CUs the rollout leaves idle
     if ((int)blockIdx.x >= nroll) {
@@ -505,12 +522,20 @@ static void launch_thread_t(const ModelConst& mc, const StepInput* in, const flo
     const dim3 grid(blocks + extra * (256 / threads));
     // thread form with the cost terms: runtime shapes only (the four-lane kernel is the default)
     constexpr int HTT = EXT ? 0 : HT, STT = EXT ? 0 : ST;
+    if constexpr (KIND == SRBD_ZERO_ORDER && (HT == 10 || HT == 12) && !EXT) {
+        if (grp.ksi && mc.method != SRBD_CEM_MPPI) {  // ks_ok: the step input as the first kernel argument
+            hipLaunchKernelGGL((rollout_kernel<KIND, HT, ST, false, false, true>), grid, dim3(threads), 0, s,
+                               *static_cast<const StepInputK*>(grp.ksi), mc, in, noise, costs, recs, rec_stride, job,
+                               blocks, grp);
+            return;
+        }
+    }
     if (mc.method == SRBD_CEM_MPPI)
-        hipLaunchKernelGGL((rollout_kernel<KIND, HTT, STT, true, EXT>), grid, dim3(threads), 0, s, mc, in, noise, costs,
-                           recs, rec_stride, job, blocks, grp);
-    else
-        hipLaunchKernelGGL((rollout_kernel<KIND, HTT, STT, false, EXT>), grid, dim3(threads), 0, s, mc, in, noise,
+        hipLaunchKernelGGL((rollout_kernel<KIND, HTT, STT, true, EXT>), grid, dim3(threads), 0, s, KsNone{}, mc, in, noise,
                            costs, recs, rec_stride, job, blocks, grp);
+    else
+        hipLaunchKernelGGL((rollout_kernel<KIND, HTT, STT, false, EXT>), grid, dim3(threads), 0, s, KsNone{}, mc, in,
+                           noise, costs, recs, rec_stride, job, blocks, grp);
 }
 
 void launch_rollout_thread(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,

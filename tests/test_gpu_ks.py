@@ -1,6 +1,6 @@
 """Host steps with the step input as the rollout's kernel argument (StepInputK, srbd_kernels.hip KS).
 
-Zero-order four-lane shapes (H 10 / 12, MPPI / random sampling): srbd_step passes the step input by value
+Zero-order shapes (H 10 / 12, MPPI / random sampling), four-lane and thread-per-sample rollouts: srbd_step passes the step input by value
 to the rollout launch, whose block 0 writes the device StepInput for the merge and later readers, and runs
 no upload kernel.  Every output must equal the uploaded input's (SRBD_KS=0, read per context) bit for bit:
 device draws and injected noise, with and without the in-launch final merge, H 10; and sequences of host
@@ -19,27 +19,34 @@ pytestmark = pytest.mark.gpu
 KEYS = ("costs", "best", "grf", "pred")
 
 
-def both(lib, monkeypatch, case, **kw):
+def both(lib, monkeypatch, case, rollout=None, **kw):
     out = {}
+    if rollout:
+        monkeypatch.setenv("SRBD_ROLLOUT", rollout)
     for ks in ("0", "1"):
         monkeypatch.setenv("SRBD_KS", ks)
         try:
             out[ks] = run_gpu(lib, case, **kw)
         finally:
             monkeypatch.delenv("SRBD_KS")
+    if rollout:
+        monkeypatch.delenv("SRBD_ROLLOUT")
     return out["0"], out["1"]
 
 
-@pytest.mark.parametrize("method,N,H,noise", [
-    ("mppi", 10000, 12, False),           # C2: the headline host step
-    ("mppi", 10000, 12, True),            # injected noise
-    ("random_sampling", 3001, 10, False),
-    ("mppi", 65536, 12, False),           # with the in-launch final merge
-    ("mppi", 40000, 10, True),
+@pytest.mark.parametrize("method,N,H,noise,rollout", [
+    ("mppi", 10000, 12, False, None),           # C2: the headline host step
+    ("mppi", 10000, 12, True, None),            # injected noise
+    ("random_sampling", 3001, 10, False, None),
+    ("mppi", 65536, 12, False, None),           # with the in-launch final merge
+    ("mppi", 40000, 10, True, None),
+    ("mppi", 10000, 12, False, "thread"),       # thread-per-sample rollout
+    ("random_sampling", 2999, 10, True, "thread"),
+    ("mppi", 131072, 12, False, None),          # past the four-lane range: thread form by default
 ])
-def test_ks_bitwise(lib, monkeypatch, method, N, H, noise):
+def test_ks_bitwise(lib, monkeypatch, method, N, H, noise, rollout):
     case = make_case("c2", N=N, method=method, H=H, seed=zlib.crc32(f"ks{method}{N}{H}".encode()))
-    a, b = both(lib, monkeypatch, case, noise=noise, seed=11, counter=7)
+    a, b = both(lib, monkeypatch, case, rollout=rollout, noise=noise, seed=11, counter=7)
     for k in KEYS:
         np.testing.assert_array_equal(a[k], b[k])
     assert a["best_index"] == b["best_index"] and a["best_cost"] == b["best_cost"]
@@ -47,7 +54,7 @@ def test_ks_bitwise(lib, monkeypatch, method, N, H, noise):
         check_reduction(case, b)
 
 
-@pytest.mark.parametrize("N", [10000, 65536])
+@pytest.mark.parametrize("N", [10000, 65536, 131072])
 def test_ks_sequence_with_device_chains(lib, monkeypatch, N):
     case = make_case("c2", N=N, seed=31)
     ctxs = {}
