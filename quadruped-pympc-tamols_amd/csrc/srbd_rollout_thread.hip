@@ -7,6 +7,9 @@
 #ifndef SRBD_KC_LDS
 #define SRBD_KC_LDS 0
 #endif
+#ifndef SRBD_THREAD_WPE  // minimum waves per SIMD the zero-order thread form is compiled for
+#define SRBD_THREAD_WPE 4
+#endif
 #undef SRBD_ROLLOUT_STAMPS  // the timeline probe stamps the four-lane kernel (srbd_kernels.hip) only
 #include "srbd_device.h"
 
@@ -16,7 +19,7 @@ namespace srbd {
 // KS: the host step's input by value (the first kernel argument, read in place from the kernarg segment; block
 // 0 writes the device StepInput `in_dev`), as rollout_quad_kernel does.
 template <int KIND, int HT, int ST, bool CEMT, bool EXT, bool KS = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == SRBD_ZERO_ORDER ? 4 : 1))) rollout_kernel(
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == SRBD_ZERO_ORDER ? SRBD_THREAD_WPE : 1))) rollout_kernel(
                                                       const std::conditional_t<KS, StepInputK, KsNone> ksi,
                                                       const ModelConst mc, const StepInput* __restrict__ in_dev,
                                                       const float* __restrict__ noise, float* __restrict__ costs,
