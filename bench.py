@@ -60,6 +60,9 @@ def parse_args(argv=None):
                          "rocprofv3 --pmc, whose serialised dispatch makes an armed copy kernel wait out its deadline)")
     ap.add_argument("--targets", type=int, default=1000,
                     help="one GPU, c2: steps of the supplementary north_star_65536 / c3 lines (0: skip)")
+    ap.add_argument("--rng", default="philox", choices=["philox", "jax", "jax_legacy"],
+                    help="device noise stream of the timed steps (srbd_set_rng): this library's Philox, or the "
+                         "reference's jax.random stream (threefry, partitionable / legacy counter layout)")
     ap.add_argument("--extras", type=int, default=200,
                     help="steps of the supplementary interface / TAMOLS latency probes (0: skip)")
     return ap.parse_args(argv)
@@ -112,6 +115,26 @@ def step_inputs(w, count):
     return out
 
 
+class KeyChain:
+    """The RNG key of step k: Philox (seed 42, counter k), or the reference's jax.random schedule -- the key of
+    the interface's first call, with_newkey(PRNGKey(42)), then split(key)[0] per step (NMPC:167, 498-501) --
+    packed as srbd_step's seed.  srbd_bench_host_steps advances the key the same way from (at(k), k)."""
+
+    def __init__(self, _lib, rng: str):
+        self.lib, self.rng = _lib, rng
+        self.keys = []
+        if rng != "philox":
+            self.part = rng == "jax"
+            self.keys.append(_lib.jax_split(_lib.jax_prng_key(42), 2, self.part)[0])
+
+    def at(self, k: int) -> int:
+        if self.rng == "philox":
+            return 42
+        while len(self.keys) <= k:
+            self.keys.append(self.lib.jax_split(self.keys[-1], 2, self.part)[0])
+        return self.lib.pack_key(self.keys[k])
+
+
 def make_cfg(_lib, w, n_total: int, rank: int, world: int, device: int):
     import numpy as np
 
@@ -122,23 +145,33 @@ def make_cfg(_lib, w, n_total: int, rank: int, world: int, device: int):
 
 
 def roofline(w, n_local: int, kern: dict, traffic):
-    """Dominant kernel = the rollout launch the step runs (with the next step's Philox blocks when fused).
+    """Dominant kernel = the rollout launch exactly as the timed srbd_step calls issue it (srbd_time_launch
+    SRBD_TL_STEP_ROLLOUT: the step input by value (KS), the in-launch final merge (FM) and the next step's
+    draws (fused) where they apply), so the rocprofv3 row of the same instantiation agrees (profiles/).
 
     achieved = ALGORITHMIC bytes (each noise row read once + one cost written, 4P+4 per
-    rollout, x the rows one launch processes) / the launch's average duration (srbd_time_kernels: one
-    hipEvent pair on the context stream around back-to-back launches; agrees with rocprofv3's
-    kernel-trace average, profiles/).  The fused next-step draws (N*4P stored) are work the launch
-    also does but not algorithmic bytes of the rollout: reported as launch_bytes beside it.
-    traffic = HBM bytes per launch from the rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE).
+    rollout, x the rows one launch processes) / the launch's average duration (one hipEvent pair on the
+    context stream around back-to-back launches).  The fused next-step draws (N*4P stored) are work the
+    launch also does but not algorithmic bytes of the rollout: reported as launch_bytes beside it.
+    traffic = HBM bytes per launch of that instantiation from the rocprofv3 PMC passes (FETCH_SIZE x2 +
+    WRITE_SIZE, profiles/pmc_traffic.json).
     """
     P = w.num_params()
-    fused = kern.get("fused_rollout_us", 0.0) > 0
-    us = kern["fused_rollout_us"] if fused else kern["rollout_us"]
+    if "step_rollout_us" in kern:
+        form = int(kern.get("step_rollout_form", 0))
+        us = kern["step_rollout_us"]
+    else:  # sharded contexts: the rollout launch of the step (+ draws when fused)
+        form = 1 if kern.get("fused_rollout_us", 0.0) > 0 else 0
+        us = kern["fused_rollout_us"] if form else kern["rollout_us"]
+    fused = bool(form & 1)
     algo = n_local * (4 * P + 4)
     achieved = algo / (us * 1e-6) / 1e9
+    tags = [t for b, t in ((2, "step input by value (KS)"), (4, "in-launch final merge (FM)"),
+                           (1, "+ next-step draw blocks")) if form & b]
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-            "kernel": "rollout_quad_kernel / rollout_kernel" + (" (+ next-step Philox blocks)" if fused else ""),
+            "kernel": ("rollout_kernel" if form & 8 else "rollout_quad_kernel") + " as srbd_step launches it"
+                      + (" (" + ", ".join(tags) + ")" if tags else ""),
             "kernel_us": round(us, 3), "algorithmic_bytes_per_launch": algo,
             "launch_bytes": algo + (n_local * 4 * P if fused else 0), "bytes_per_rollout": 4 * P + 4}
 
@@ -154,28 +187,32 @@ def pmc_traffic(workload_name: str):
         return None
 
 
-def supplementary(_lib, key: str, steps: int, pmc_key=None):
-    """A target shape beside the headline line (one GPU): BASELINE north_star's MPPI ZO N=65 536 H=12
-    ("ns") or C3 (CEM cubic N=65 536 H=16).  Host-to-host srbd_step latencies timed from C, the device-
-    resident chain, per-kernel averages and the rollout roofline, measured as for the headline."""
+def supplementary(_lib, key: str, steps: int, rng: str = "philox"):
+    """A shape beside the headline line (one GPU): BASELINE north_star's MPPI ZO N=65 536 H=12 ("ns"), C3 (CEM
+    cubic N=65 536 H=16), C5's 524 288 rows on one GPU (the denominator of the strong-scaling ratio), or C2 on
+    another noise stream.  Host-to-host srbd_step latencies timed from C, the device-resident chain,
+    per-kernel averages and the rollout roofline, measured as for the headline."""
     import numpy as np
 
     from quadruped_pympc_amd.synthetic import CONFIGS
 
     w = CONFIGS[key]
     ctx = _lib.Context(make_cfg(_lib, w, w.num_samples, 0, 1, 0))
+    if rng != "philox":
+        ctx.set_rng(rng)
+    keys = KeyChain(_lib, rng)
     ins = step_inputs(w, 32)
     best = np.zeros(ctx.P, np.float32)
     sigma = np.full(ctx.P, 3.0, np.float32) if w.method == "cem_mppi" else None
     arrs = (np.stack([x[0] for x in ins]), np.stack([x[1] for x in ins]), np.stack([x[2] for x in ins]))
-    _, best, sigma = ctx.bench_host_steps(*arrs, best, sigma, 42, 0, 20)  # warm-up
-    t_us, best, sigma = ctx.bench_host_steps(*arrs, best, sigma, 42, 20, steps)
+    _, best, sigma = ctx.bench_host_steps(*arrs, best, sigma, keys.at(0), 0, 20)  # warm-up
+    t_us, best, sigma = ctx.bench_host_steps(*arrs, best, sigma, keys.at(20), 20, steps)
     ctx.bench_device_steps(20)
     ms = ctx.bench_device_steps(steps)
     kern = ctx.time_kernels(200)
     ctx.close()
     return {"workload": w.name, "num_samples": w.num_samples, "horizon": w.horizon, "method": w.method,
-            "parametrization": w.parametrization,
+            "parametrization": w.parametrization, "rng": rng,
             "value": round(w.num_samples / (float(t_us.mean()) * 1e-6), 1), "unit": "rollouts/s",
             "ms_per_step": round(float(t_us.mean()) * 1e-3, 5),
             "p50_step_ms": round(float(np.percentile(t_us, 50)) * 1e-3, 4),
@@ -326,13 +363,16 @@ def bench_single(_lib, w, args):
     import numpy as np
 
     ctx = _lib.Context(make_cfg(_lib, w, w.num_samples, 0, 1, 0))
+    if args.rng != "philox":
+        ctx.set_rng(args.rng)
+    keys = KeyChain(_lib, args.rng)
     ins = step_inputs(w, 32)
     best = np.zeros(ctx.P, np.float32)
     sigma = np.full(ctx.P, 3.0, np.float32) if w.method == "cem_mppi" else None
     state = {"sigma": sigma}
 
     def step(s, r, c, b, k):
-        b, sg, _, _ = ctx.step(s, r, c, b, sigma=state["sigma"], seed=42, counter=k)
+        b, sg, _, _ = ctx.step(s, r, c, b, sigma=state["sigma"], seed=keys.at(k), counter=k)
         if sg is not None:
             state["sigma"] = sg
         return b
@@ -349,12 +389,12 @@ def bench_single(_lib, w, args):
     contacts = np.stack([x[2] for x in ins])
     lat = []
     if args.steps < args.latency_steps:  # latency sample of >= latency_steps steps besides the timed region
-        l_us, best, state["sigma"] = ctx.bench_host_steps(states, refs, contacts, best, state["sigma"], 42, k,
+        l_us, best, state["sigma"] = ctx.bench_host_steps(states, refs, contacts, best, state["sigma"], keys.at(k), k,
                                                           args.latency_steps)
         lat = list(l_us * 1e-6)
         k += args.latency_steps
     t0 = time.perf_counter()
-    t_us, best, state["sigma"] = ctx.bench_host_steps(states, refs, contacts, best, state["sigma"], 42, k,
+    t_us, best, state["sigma"] = ctx.bench_host_steps(states, refs, contacts, best, state["sigma"], keys.at(k), k,
                                                       args.steps)
     wall = time.perf_counter() - t0
     k += args.steps
@@ -365,7 +405,7 @@ def bench_single(_lib, w, args):
     if args.other_steps > 0:
         ctx.set_armed(not armed, 0)
         n_other = max(200, min(args.steps, args.other_steps))
-        o_us, best, state["sigma"] = ctx.bench_host_steps(states, refs, contacts, best, state["sigma"], 42, k,
+        o_us, best, state["sigma"] = ctx.bench_host_steps(states, refs, contacts, best, state["sigma"], keys.at(k), k,
                                                           n_other)
         k += n_other
         o_us = o_us[min(20, n_other // 10):]
@@ -401,14 +441,15 @@ def bench_multi(_lib, w, args, rank, world, local_rank, scaling):
     dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     n_total = w.num_samples if scaling == "strong" else w.num_samples * world
     mpc = ShardedSamplingMPC(make_cfg(_lib, w, n_total, rank, world, local_rank), rank, world, local_rank,
-                             transport=args.transport)
+                             transport=args.transport, rng=args.rng)
+    keys = KeyChain(_lib, args.rng)
     ins = step_inputs(w, 32)
     best = np.zeros(mpc.P, np.float32)
     sigma = np.full(mpc.P, 3.0, np.float32) if w.method == "cem_mppi" else None
     state = {"sigma": sigma}
 
     def step(s, r, c, b, k):
-        b, sg, _ = mpc.step(s, r, c, b, sigma=state["sigma"], seed=42, counter=k)
+        b, sg, _ = mpc.step(s, r, c, b, sigma=state["sigma"], seed=keys.at(k), counter=k)
         if sg is not None:
             state["sigma"] = sg
         return b
@@ -429,7 +470,7 @@ def bench_multi(_lib, w, args, rank, world, local_rank, scaling):
     timed = []
     t0 = time.perf_counter()
     if c_timed:  # rollout -> xGMI record exchange -> merge, srbd_step_sharded from C
-        t_us, best, state["sigma"] = mpc.ctx.bench_host_steps(*arrs, best, state["sigma"], 42, k, args.steps)
+        t_us, best, state["sigma"] = mpc.ctx.bench_host_steps(*arrs, best, state["sigma"], keys.at(k), k, args.steps)
         timed = list(t_us * 1e-6)
     else:
         best = run_steps(step, ins, best, k, args.steps, timed)
@@ -503,7 +544,9 @@ def main(argv=None):
         "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (fixed-seed robot states / references, PGG contact sequences, device Philox noise)",
+        "data": "synthetic (fixed-seed robot states / references, PGG contact sequences, device "
+                + ("Philox noise" if args.rng == "philox" else "jax.random (threefry) noise") + ")",
+        "rng": args.rng,
         "config": {"workload": w.name, "num_samples": out["n_total"], "rows_per_gpu": out["n_local"],
                    "horizon": w.horizon, "method": w.method, "parametrization": w.parametrization,
                    "robot": w.robot, "gait": w.gait,
@@ -528,9 +571,14 @@ def main(argv=None):
         line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
     else:
         line["cpu_baseline"] = None
-    if world == 1 and args.targets > 0 and args.config == "c2":  # the north-star shape and C3 beside the headline
-        line["north_star_65536"] = supplementary(_lib, "ns", args.targets)
-        line["c3"] = supplementary(_lib, "c3", args.targets)
+    if world == 1 and args.targets > 0 and args.config == "c2":  # the north-star shape, C3 and C5 beside the headline
+        line["north_star_65536"] = supplementary(_lib, "ns", args.targets, args.rng)
+        line["c3"] = supplementary(_lib, "c3", args.targets, args.rng)
+        # C5's 524 288 rows on one GPU: the denominator of the driver's C5 strong-scaling ratio
+        line["c5_1gpu"] = supplementary(_lib, "c5", args.targets, args.rng)
+        # the headline shape on the other noise stream (Philox <-> the reference's jax.random stream)
+        other = "jax" if args.rng == "philox" else "philox"
+        line["c2_rng_" + other] = supplementary(_lib, "c2", args.targets, other)
     if world == 1 and args.extras and args.config in ("c2", "c4"):  # the callers either side of the path
         line["interface_step"] = interface_latency(w, args.extras)
         line["interface_step_armed"] = interface_latency(w, args.extras, armed=True)

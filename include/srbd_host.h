@@ -98,6 +98,14 @@ int srbd_shm_publish(uint64_t* seq, double* payload, const srbd_shm_msg* msg);
  * 0 when the writer was active (caller keeps its previous values), negative on bad arguments. */
 int srbd_shm_read(const uint64_t* seq, const double* payload, srbd_shm_msg* msg, uint64_t* seq_out);
 
+/* jax.random keys of the reference's noise stream (srbd_set_rng SRBD_RNG_JAX / SRBD_RNG_JAX_LEGACY; the
+ * draws themselves are made on the device).  partitionable: jax_threefry_partitionable (1 = JAX's default
+ * since 0.5.0, 0 = earlier JAX).  A key is uint32[2]; srbd_step's `seed` packs it as key[0] << 32 | key[1].
+ *   srbd_jax_prng_key <- jax.random.PRNGKey(seed)   quadruped_pympc/controllers/sampling/centroidal_nmpc_jax.py:167
+ *   srbd_jax_split    <- jax.random.split(key, num) (with_newkey = split(key)[0], centroidal_nmpc_jax.py:498-501) */
+int srbd_jax_prng_key(uint64_t seed, uint32_t key_out[2]);
+int srbd_jax_split(const uint32_t key[2], int32_t num, int32_t partitionable, uint32_t* keys_out /* num x 2 */);
+
 #ifdef __cplusplus
 }
 #endif

@@ -104,7 +104,8 @@ int srbd_set_stream(srbd_ctx* ctx, void* hip_stream);
  *   contact           : 4 rows x contact_stride floats, row-major; the first H columns are used
  *   best_params       : P floats, in: previous best, out: updated best (reassigned by the interface)
  *   sigma             : P floats (CEM only, in/out; NULL otherwise)
- *   noise             : NULL -> device Philox4x32-10 RNG keyed by (seed, counter);
+ *   noise             : NULL -> device RNG: Philox4x32-10 keyed by (seed, counter), or the reference's
+ *                       jax.random stream keyed by seed (srbd_set_rng);
  *                       else N x P row-major additional_random_parameters (row 0 must be zero)
  *   out_costs         : N floats (saturated) or NULL
  */
@@ -172,6 +173,21 @@ int srbd_clear_gait(srbd_ctx* ctx);
  */
 int srbd_set_cost_terms(srbd_ctx* ctx, const float r_force[3], float w_smooth, float w_cone);
 
+/*
+ * Device noise stream of every following step of the context (default SRBD_RNG_PHILOX):
+ *   SRBD_RNG_PHILOX     : Philox4x32-10 + Box-Muller keyed by (seed, counter) (this library's own stream)
+ *   SRBD_RNG_JAX        : the reference's jax.random stream (centroidal_nmpc_jax.py:654-676, 811, 957;
+ *                         gait-adaptive choice :692, 836), jax_threefry_partitionable = True (JAX >= 0.5)
+ *   SRBD_RNG_JAX_LEGACY : the same with jax_threefry_partitionable = False (earlier JAX)
+ * In the JAX modes the `seed` of srbd_step is the step's key (uint32[2] packed key[0] << 32 | key[1], the
+ * key the reference's interface passes: master_key after with_newkey, srbd_controller_interface.py:126-164);
+ * `counter` only numbers the steps.  The draws made ahead (fused next-step draws, device-resident chains,
+ * armed steps) assume the next key is with_newkey's split(key)[0] (srbd_jax_split, include/srbd_host.h).
+ */
+enum { SRBD_RNG_PHILOX = 0, SRBD_RNG_JAX = 1, SRBD_RNG_JAX_LEGACY = 2 };
+int srbd_set_rng(srbd_ctx* ctx, int32_t kind);
+int srbd_get_rng(const srbd_ctx* ctx);
+
 /* Sharded form.  Record size in floats (identical on every rank). */
 int srbd_record_floats(const srbd_ctx* ctx);
 /* Rows of this rank only; writes this rank's partial record to d_record (device pointer).
@@ -220,6 +236,15 @@ int srbd_bench_host_steps(srbd_ctx* ctx, const float* state, const float* ref, c
 int srbd_time_kernels(srbd_ctx* ctx, int32_t iters, float* rollout_us, float* rng_us, float* reduce_us,
                       float* fused_rollout_us, float* event_floor_us);
 
+/* Measurement: average duration (us) of one kind of launch, `iters` back to back (one hipEvent pair), alone, so
+ * a rocprofv3 pass over the call sees only it.  SRBD_TL_STEP_ROLLOUT is the rollout launch exactly as srbd_step
+ * issues it (*form: 1 fused next-step draws | 2 step input by value | 4 in-launch final merge | 8 thread-per-sample
+ * rollout kernel, else four lanes per sample); SRBD_TL_STEP_MERGE
+ * the merge launch srbd_step issues after it (0 when the rollout launch merges).  form may be NULL. */
+enum { SRBD_TL_RNG = 0, SRBD_TL_ROLLOUT = 1, SRBD_TL_ROLLOUT_FUSED = 2, SRBD_TL_STEP_ROLLOUT = 3,
+       SRBD_TL_STEP_MERGE = 4, SRBD_TL_EMPTY = 5 };
+int srbd_time_launch(srbd_ctx* ctx, int32_t which, int32_t iters, float* us, int32_t* form);
+
 /* Device-resident sharded chain (benchmark / pipelined callers): reuses the inputs of the last
  * srbd_step_local on the device.  srbd_device_step_local: RNG -> rollout -> rank record into d_record;
  * srbd_device_step_finish: merge -> outputs -> warm start (best/sigma/counter) written back on
@@ -228,6 +253,10 @@ int srbd_device_step_local(srbd_ctx* ctx, void* d_record);
 int srbd_device_step_finish(srbd_ctx* ctx, const void* d_records, int32_t num_records);
 /* Block until the context stream is idle and copy the last step's outputs. */
 int srbd_sync_result(srbd_ctx* ctx, float* best_params, float* sigma, srbd_result* out);
+/* Test / diagnostic: the device draws a step keyed by (seed, counter) uses (the context's stream,
+ * srbd_set_rng): this shard's rows of additional_random_parameters, n_local x P row-major (row 0 of the
+ * problem is zero; CEM: the unscaled standard normals the step multiplies by sigma).  Blocks. */
+int srbd_draw_noise(srbd_ctx* ctx, uint64_t seed, uint64_t counter, float* out_rows);
 /* Saturated costs of this rank's rows from the last step (lazy materialisation). */
 int srbd_copy_costs(srbd_ctx* ctx, float* out_costs);
 

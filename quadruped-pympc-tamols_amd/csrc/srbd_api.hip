@@ -19,6 +19,7 @@
 
 #include <rccl/rccl.h>  // types only: RCCL is dlopen'ed (the caller's copy, e.g. torch's)
 
+#include "srbd_jaxrng.h"
 #include "srbd_launch.h"
 
 using namespace srbd;
@@ -432,6 +433,7 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
 }
 
 static void comm_release(srbd_ctx* c);
+static uint64_t next_seed(const srbd_ctx* c, uint64_t seed);
 static void xg_drop_graphs(srbd_ctx* c);
 
 extern "C" void srbd_destroy(srbd_ctx* c) {
@@ -551,6 +553,14 @@ static int upload_input(srbd_ctx* c) {
     return SRBD_OK;
 }
 
+// The step input as the rollout's kernel argument: StepInput's prefix and best[P] from the staging, the
+// unused tail of best zeroed (the whole struct is the argument, and block 0 copies all of it to d_in).
+static void fill_ksi(const srbd_ctx* c, StepInputK* k) {
+    const size_t used = offsetof(StepInput, best) + sizeof(float) * (size_t)c->mc.P;
+    memcpy(k, c->h_in, used);
+    memset(reinterpret_cast<unsigned char*>(k) + used, 0, sizeof(StepInputK) - used);
+}
+
 // The records the merge reads: the group records when the rollout launch reduces its blocks in groups.
 static GroupArgs grp_of(const srbd_ctx* c) { return GroupArgs{c->d_grec, c->d_gcnt, c->gsize}; }
 static const float* merge_src(const srbd_ctx* c) { return c->gsize > 1 ? c->d_grec : c->d_wrec; }
@@ -614,6 +624,10 @@ static int wait_published(srbd_ctx* c, uint32_t seq, int nflags = 1, int* cancel
                     *cancelled = 1;
                     return SRBD_OK;
                 }
+                // a launch that stopped part-way can leave group / final-merge arrival counts behind: clear them
+                // so the next step starts from zero (they are zero between completed launches)
+                if (c->d_gcnt) (void)hipMemsetAsync(c->d_gcnt, 0, sizeof(uint32_t) * (size_t)c->ngroups, c->stream);
+                if (c->d_gdone) (void)hipMemsetAsync(c->d_gdone, 0, sizeof(uint32_t), c->stream);
                 return fail(c, SRBD_E_HIP, "step completed without publishing its outputs");
             }
             if (e != hipErrorNotReady) HIP_TRY(c, e);
@@ -708,7 +722,7 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
         StepInputK ksi;
         const bool ks = c->ks && !c->mc.ga && !c->mc.cost_on;
         if (ks)
-            memcpy(&ksi, c->h_in, offsetof(StepInput, best) + sizeof(float) * (size_t)c->mc.P);
+            fill_ksi(c, &ksi);
         else if ((r = upload_input(c)))
             return r;
         int buf = 0;
@@ -721,7 +735,7 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
         if (fuse) {
             c->pref_valid = true;
             c->pref_buf = 1 - buf;
-            c->pref_seed = seed;
+            c->pref_seed = next_seed(c, seed);
             c->pref_ctr = counter + 1;
         }
         return SRBD_OK;
@@ -730,8 +744,8 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
     // the copy-back goes first (it would queue behind the armed copy kernel)
     // fused: the next step's draws are in pref_buf; unfused: the chain redraws into this step's buffer
     auto arm = [&]() {
-        if (c->pref_valid) arm_next(c, seed, counter + 1, c->pref_buf, true);
-        else if (!fusable(c)) arm_next(c, seed, counter + 1, c->cur, false);
+        if (c->pref_valid) arm_next(c, next_seed(c, seed), counter + 1, c->pref_buf, true);
+        else if (!fusable(c)) arm_next(c, next_seed(c, seed), counter + 1, c->cur, false);
     };
     const int claimed_buf = c->arm_buf;
     const bool claimed_fused = c->arm_fused;
@@ -745,7 +759,7 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
         c->pref_valid = c->arm_fused;
         if (c->arm_fused) {
             c->pref_buf = 1 - c->arm_buf;
-            c->pref_seed = seed;
+            c->pref_seed = next_seed(c, seed);
             c->pref_ctr = counter + 1;
         }
     } else if ((rc = launch_unarmed())) {
@@ -761,9 +775,12 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
         // never the previous input's outputs (round-2 advisor finding).
         std::swap(c->d_costs, c->d_costs_arm);
         arm_cancel(c);
-        ++c->arm_refired;
-        --c->arm_served;  // counted as served at the claim
-        ++c->arm_cancelled;
+        {
+            std::lock_guard<std::mutex> lk(g_arm_mu);  // srbd_armed_stats reads them under the lock
+            ++c->arm_refired;
+            --c->arm_served;  // counted as served at the claim
+            ++c->arm_cancelled;
+        }
         c->pref_valid = claimed_fused;  // this call's draws are in the claimed chain's buffer
         c->pref_buf = claimed_buf;
         c->pref_seed = seed;
@@ -847,7 +864,7 @@ extern "C" int srbd_step_local(srbd_ctx* c, const float* state, const float* ref
     if (fuse) {
         c->pref_valid = true;
         c->pref_buf = 1 - buf;
-        c->pref_seed = seed;
+        c->pref_seed = next_seed(c, seed);
         c->pref_ctr = counter + 1;
     }
     c->chain_started = false;
@@ -918,6 +935,26 @@ extern "C" int srbd_sync_result(srbd_ctx* c, float* best, float* sigma, srbd_res
     HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(StepOutput), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return copy_out(c, best, sigma, out);
+}
+
+// The device draws of a step keyed by (seed, counter): this shard's additional_random_parameters rows,
+// row-major n_local x P (CEM: the unscaled standard normals; the step multiplies them by sigma).
+extern "C" int srbd_draw_noise(srbd_ctx* c, uint64_t seed, uint64_t counter, float* out) {
+    if (!c || !out) return SRBD_E_INVALID;
+    arm_cancel(c);
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    const ModelConst& mc = c->mc;
+    c->pref_valid = false;  // the buffer the prefetched draws were in is overwritten
+    c->cur = 0;
+    launch_rng(mc, c->d_in, seed, counter, 0, 0, c->d_noise[0], c->stream);
+    HIP_TRY(c, hipGetLastError());
+    std::vector<float> soa((size_t)mc.P * mc.n_local);
+    HIP_TRY(c, hipMemcpy2DAsync(soa.data(), sizeof(float) * mc.n_local, c->d_noise[0], sizeof(float) * mc.ldn,
+                                sizeof(float) * mc.n_local, mc.P, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (int j = 0; j < mc.P; ++j)
+        for (int k = 0; k < mc.n_local; ++k) out[(size_t)k * mc.P + j] = soa[(size_t)j * mc.n_local + k];
+    return SRBD_OK;
 }
 
 extern "C" int srbd_copy_costs(srbd_ctx* c, float* out_costs) {
@@ -1008,6 +1045,32 @@ extern "C" int srbd_set_cost_terms(srbd_ctx* c, const float* r_force, float w_sm
         drop_graphs(c);  // kernels take ModelConst by value: recapture
     }
     return SRBD_OK;
+}
+
+// Device noise stream: Philox (seed, counter) or the reference's jax.random stream (srbd_jaxrng.h).
+extern "C" int srbd_set_rng(srbd_ctx* c, int32_t kind) {
+    if (!c) return SRBD_E_INVALID;
+    if (kind != SRBD_RNG_PHILOX && kind != SRBD_RNG_JAX && kind != SRBD_RNG_JAX_LEGACY)
+        return fail(c, SRBD_E_INVALID, "unknown RNG kind");
+    if (kind != SRBD_RNG_PHILOX && (uint64_t)(c->mc.N - 1) * (uint64_t)c->mc.P >= (1ull << 32))
+        return fail(c, SRBD_E_INVALID, "the jax.random stream counts draws in 32 bits: (N - 1) * P must be < 2^32");
+    arm_cancel(c);
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->mc.rng != kind) {
+        c->mc.rng = kind;
+        c->pref_valid = false;  // prefetched draws belong to the other stream
+        drop_graphs(c);          // kernels take ModelConst by value: recapture
+    }
+    return SRBD_OK;
+}
+
+extern "C" int srbd_get_rng(const srbd_ctx* c) { return c ? c->mc.rng : SRBD_E_INVALID; }
+
+// The key of the step after one keyed `seed`: the same seed for Philox (the counter advances), with_newkey
+// (split(key)[0]) for the JAX stream.
+static uint64_t next_seed(const srbd_ctx* c, uint64_t seed) {
+    return c->mc.rng == SRBD_RNG_PHILOX ? seed : jax_next_key(seed, c->mc.rng == SRBD_RNG_JAX);
 }
 
 // ------------------------------------------------------------------ host merge (no device)
@@ -1428,7 +1491,7 @@ static int xg_step(srbd_ctx* c, const float* state, const float* ref, const floa
     StepInputK ksi;  // as srbd_step: the rollout's kernel argument, or the upload kernel
     const bool ks = c->ks && !c->mc.ga && !c->mc.cost_on;
     if (ks)
-        memcpy(&ksi, c->h_in, offsetof(StepInput, best) + sizeof(float) * (size_t)c->mc.P);
+        fill_ksi(c, &ksi);
     else if ((rc = upload_input(c)))
         return rc;
     int buf = 0;
@@ -1440,7 +1503,7 @@ static int xg_step(srbd_ctx* c, const float* state, const float* ref, const floa
     if (fuse) {
         c->pref_valid = true;
         c->pref_buf = 1 - buf;
-        c->pref_seed = seed;
+        c->pref_seed = next_seed(c, seed);
         c->pref_ctr = counter + 1;
     }
     c->chain_started = false;
@@ -1604,14 +1667,15 @@ extern "C" int srbd_bench_device_steps(srbd_ctx* c, int32_t steps, float* ms) {
 
 // Host-to-host srbd_step latency at the C-ABI boundary: `steps` calls cycling through n_in input sets
 // (state / ref 24 floats, contact 4 x stride each), the warm start fed back, counters consecutive from
-// counter0 (so the fused next-step draws are used, as a controller at 100 Hz does); each call timed with
-// the steady clock.  lat_us: `steps` floats.  sigma: CEM in/out or NULL.
+// counter0 and (JAX stream) each key with_newkey of the last (so the fused next-step draws are used, as a
+// controller at 100 Hz does); each call timed with the steady clock.  lat_us: `steps` floats.  sigma: CEM
+// in/out or NULL.
 extern "C" int srbd_bench_host_steps(srbd_ctx* c, const float* state, const float* ref, const float* contact,
                                      int32_t contact_stride, int32_t n_in, float* best, float* sigma, uint64_t seed,
                                      uint64_t counter0, int32_t steps, float* lat_us) {
     if (!c || !state || !ref || !contact || !best || !lat_us || n_in < 1 || steps < 1) return SRBD_E_INVALID;
     srbd_result res;
-    for (int32_t i = 0; i < steps; ++i) {
+    for (int32_t i = 0; i < steps; ++i, seed = next_seed(c, seed)) {
         const int k = i % n_in;
         const auto t0 = std::chrono::steady_clock::now();
         const float* st = state + 24 * k;
@@ -1684,6 +1748,88 @@ extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, 
     (void)hipEventDestroy(e1);
     if (!rc) HIP_TRY(c, hipGetLastError());
     return rc;
+}
+
+// Average duration of ONE kind of launch, `iters` back to back between one hipEvent pair (as srbd_time_kernels),
+// so a rocprofv3 pass over this call sees only that launch (a PMC A/B of two launches of one kernel name).
+//   SRBD_TL_STEP_ROLLOUT: the rollout launch exactly as srbd_step issues it -- the step input by value (KS), the
+//     in-launch final merge (FM, publishing into the host-mapped outputs) and the next step's draws (fused) where
+//     they apply; *form = 1 fused | 2 KS | 4 FM | 8 thread-per-sample rollout (else four lanes per sample).
+//   SRBD_TL_STEP_MERGE: the merge launch srbd_step issues after it (0 us when the rollout launch merges).
+extern "C" int srbd_time_launch(srbd_ctx* c, int32_t which, int32_t iters, float* us, int32_t* form) {
+    if (!c || iters < 1 || !us) return SRBD_E_INVALID;
+    arm_cancel(c);
+    if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step once before timing");
+    if (c->cfg.world_size > 1) return fail(c, SRBD_E_STATE, "needs an unsharded context");
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    c->pref_valid = false;
+    c->cur = 0;
+    if (int rc = reset_noise_scaled(c)) return rc;
+    const ModelConst& mc = c->mc;
+    const bool fuse = fusable(c);
+    const bool ks = c->ks && !mc.ga && !mc.cost_on;
+    const bool fm = c->final_merge && !mc.ga && !mc.cost_on;
+    StepInputK ksi;
+    if (ks) fill_ksi(c, &ksi);
+    if (form)
+        *form = (which == SRBD_TL_STEP_ROLLOUT)
+                    ? ((fuse ? 1 : 0) | (ks ? 2 : 0) | (fm ? 4 : 0) | (c->mode == ROLLOUT_THREAD ? 8 : 0))
+                    : 0;
+    const RngJob next{c->d_noise[1], 0, 0, 1, 1, nullptr};
+    int nflags = 0;  // publish flags of the last launch (0: it publishes nothing)
+    auto launch = [&]() {
+        switch (which) {
+            case SRBD_TL_RNG: launch_rng(mc, c->d_in, 0, 0, 1, 0, c->d_noise[0], c->stream); break;
+            case SRBD_TL_ROLLOUT:
+            case SRBD_TL_ROLLOUT_FUSED:
+                launch_rollout(mc, c->d_in, c->d_noise[0], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
+                               c->stream, which == SRBD_TL_ROLLOUT_FUSED && fuse ? &next : nullptr, grp_of(c));
+                break;
+            case SRBD_TL_STEP_ROLLOUT: {
+                GroupArgs grp = grp_of(c);
+                grp.ksi = ks ? &ksi : nullptr;
+                if (fm) {
+                    grp.out = c->d_out_host;
+                    grp.flag = c->d_flag;
+                    grp.seq = ++c->seq;
+                    grp.gdone = c->d_gdone;
+                    grp.ngroups = c->ngroups;
+                    grp.fence_sys = merge_fence_sys();
+                }
+                launch_rollout(mc, c->d_in, c->d_noise[0], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
+                               c->stream, fuse ? &next : nullptr, grp);
+                nflags = fm ? 1 : 0;
+                break;
+            }
+            case SRBD_TL_STEP_MERGE:
+                nflags = launch_merge_tree(mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, c->d_noise[0],
+                                           c->d_part, nullptr, c->d_out_host, 0, c->stream, 0,
+                                           Publish{c->d_flag, ++c->seq, nullptr});
+                break;
+            default: launch_empty(c->stream); break;
+        }
+    };
+    if (which < SRBD_TL_RNG || which > SRBD_TL_EMPTY) return fail(c, SRBD_E_INVALID, "unknown launch");
+    if (which == SRBD_TL_STEP_MERGE && fm) {
+        *us = 0.0f;
+        return SRBD_OK;
+    }
+    hipEvent_t e0, e1;
+    HIP_TRY(c, hipEventCreate(&e0));
+    HIP_TRY(c, hipEventCreate(&e1));
+    launch();  // warm
+    HIP_TRY(c, hipEventRecord(e0, c->stream));
+    for (int i = 0; i < iters; ++i) launch();
+    HIP_TRY(c, hipEventRecord(e1, c->stream));
+    HIP_TRY(c, hipEventSynchronize(e1));
+    float ms = 0.0f;
+    HIP_TRY(c, hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    HIP_TRY(c, hipGetLastError());
+    *us = ms * 1000.0f / (float)iters;
+    if (nflags > 0) return wait_published(c, c->seq, nflags);  // the launches published into h_flag
+    return SRBD_OK;
 }
 
 // Diagnostic: average duration (us) of the merge kernel's phases from s_memrealtime stamps (100 MHz):

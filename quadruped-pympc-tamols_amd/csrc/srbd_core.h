@@ -52,6 +52,9 @@ struct ModelConst {
     // opt-in cost terms (srbd_set_cost_terms); cost_on == 0: the reference's cost, terms skipped
     int cost_on;
     float cost_r[3], cost_smooth, cost_cone;
+    // device noise stream (srbd_set_rng): RNG_PHILOX (Philox4x32-10, keyed by (seed, counter)) or the
+    // reference's jax.random stream (RNG_JAX / RNG_JAX_LEGACY, keyed by the packed key `seed`; srbd_jaxrng.h)
+    int rng;
 };
 SRBD_HD bool is_tail_col(const ModelConst& mc, int j) { return (mc.tailmask[j >> 5] >> (j & 31)) & 1u; }
 

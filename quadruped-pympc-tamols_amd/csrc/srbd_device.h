@@ -4,6 +4,7 @@
 
 #include <utility>
 
+#include "srbd_jaxrng.h"
 #include "srbd_launch.h"
 
 namespace srbd {
@@ -197,6 +198,63 @@ __device__ __forceinline__ void rng_item(const ModelConst& mc, const float* __re
         __hip_atomic_store(&o[i * ldn], r > 0 ? v[i] : 0.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The reference's jax.random stream (srbd_set_rng, srbd_jaxrng.h): element (row r, column j) of the
+// sampler's draw, as NMPC:647-677 (random sampling: the two Gaussian blocks share key and shape, so block
+// 2 reuses block 1's normals; the uniform block is a draw of its own shape from the same key), :806-812
+// (MPPI: sigma * Z) and :951-958 (CEM: Z, scaled by sigma_j on read as for Philox).  One item per element,
+// enumerated k-fastest like the Philox items (coalesced stores).
+__device__ __forceinline__ float jax_noise_value(const ModelConst& mc, uint32_t k0, uint32_t k1, int r, int j,
+                                                 bool part) {
+    const uint64_t P = (uint64_t)mc.P;
+    if (mc.method != SRBD_RANDOM_SAMPLING) {
+        const float z = jax_normal(jax_bits(k0, k1, (uint64_t)(r - 1) * P + j, (uint64_t)(mc.N - 1) * P, part));
+        return mc.method == SRBD_MPPI ? mc.sigma_mppi * z : z;
+    }
+    const int t = mc.N / 3;
+    if (r <= 2 * t) {
+        const int d = r <= t ? r - 1 : r - 1 - t;
+        const float z = jax_normal(jax_bits(k0, k1, (uint64_t)d * P + j, (uint64_t)t * P, part));
+        return (r <= t ? mc.sigma_rs[0] : mc.sigma_rs[1]) * z;
+    }
+    const float s2 = mc.sigma_rs[2], lo = -s2;
+    return jax_uniform(jax_bits(k0, k1, (uint64_t)(r - 1 - 2 * t) * P + j, (uint64_t)(mc.N - 1 - 2 * t) * P, part),
+                       lo, s2 - lo);
+}
+
+__device__ __forceinline__ void jax_rng_items(const ModelConst& mc, uint64_t key, const RngJob& job, int first,
+                                              int stride) {
+    const bool part = mc.rng == RNG_JAX;
+    const uint32_t k0 = (uint32_t)(key >> 32), k1 = (uint32_t)key;
+    const int n = mc.n_local, P = mc.P;
+    const size_t ldn = (size_t)mc.ldn;
+    int j = first / n, k = first - j * n;
+    const int sj = stride / n, sk = stride - sj * n;
+    while (j < P) {
+        const int r = mc.row0 + k;
+        const float v = r > 0 ? jax_noise_value(mc, k0, k1, r, j, part) : 0.0f;  // row 0: the warm start
+        __hip_atomic_store(&job.noise[(size_t)j * ldn + k], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        k += sk;
+        j += sj;
+        if (k >= n) {
+            k -= n;
+            ++j;
+        }
+    }
+}
+
+// Device-resident chains: the next step's RNG key -- counter + inc, and for the JAX stream also the
+// key itself, with_newkey inc times (NMPC:498-501).
+__device__ __forceinline__ void advance_key(const ModelConst& mc, StepInput* in, int inc) {
+    const uint64_t cc = (((uint64_t)in->ctr_hi << 32) | in->ctr_lo) + (uint64_t)inc;
+    in->ctr_lo = (uint32_t)cc;
+    in->ctr_hi = (uint32_t)(cc >> 32);
+    if (mc.rng != RNG_PHILOX) {
+        const uint64_t key = jax_next_key(((uint64_t)in->seed_hi << 32) | in->seed_lo, mc.rng == RNG_JAX, inc);
+        in->seed_lo = (uint32_t)key;
+        in->seed_hi = (uint32_t)(key >> 32);
+    }
+}
+
 // Items (k, q) enumerated k-fastest so consecutive lanes store consecutive floats; the item index is
 // advanced incrementally (no per-item division).  P is a multiple of 12, so quads are whole.
 __device__ __forceinline__ void rng_items(const ModelConst& mc, const StepInput* __restrict__ in, const RngJob& job,
@@ -205,7 +263,10 @@ __device__ __forceinline__ void rng_items(const ModelConst& mc, const StepInput*
     if (job.dev_ctr) {
         seed = ((uint64_t)in->seed_hi << 32) | in->seed_lo;
         ctr = (((uint64_t)in->ctr_hi << 32) | in->ctr_lo) + (uint64_t)job.ctr_offset;
+        // the JAX key of a later step of the chain: with_newkey ctr_offset times
+        if (mc.rng != RNG_PHILOX) seed = jax_next_key(seed, mc.rng == RNG_JAX, job.ctr_offset);
     }
+    if (mc.rng != RNG_PHILOX) return jax_rng_items(mc, seed, job, first, stride);
     const int n = mc.n_local, nq = mc.P / 4;
     int q = first / n, k = first - q * n;
     const int sq = stride / n, sk = stride - sq * n;
@@ -574,6 +635,9 @@ constexpr uint32_t GA_FREQ_LANE = 0x10000u;  // Philox counter word 1 of the fre
 __device__ __forceinline__ float ga_sample_freq(const ModelConst& mc, const StepInput* __restrict__ in, int k) {
     if (in->ga_explicit) return mc.ga_freq[k];
     const uint64_t seed = ((uint64_t)in->seed_hi << 32) | in->seed_lo;
+    if (mc.rng != RNG_PHILOX)  // jax.random.choice(key, freqs, (N,)) at the sample's global row
+        return in->ga_freqs[jax_choice_index((uint32_t)(seed >> 32), (uint32_t)seed, (uint64_t)(mc.row0 + k),
+                                             (uint64_t)mc.N, (uint32_t)in->ga_nfreq, mc.rng == RNG_JAX)];
     uint32_t c[4] = {(uint32_t)(mc.row0 + k), GA_FREQ_LANE, in->ctr_lo, in->ctr_hi};
     philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
     const uint32_t i = (uint32_t)(((uint64_t)c[0] * (uint32_t)in->ga_nfreq) >> 32);  // uniform in [0, n)

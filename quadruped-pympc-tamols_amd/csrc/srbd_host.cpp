@@ -9,6 +9,7 @@
 
 #include "../../include/srbd_host.h"
 #include "../../include/srbd_mpc.h"
+#include "srbd_jaxrng.h"
 
 namespace {
 
@@ -189,4 +190,30 @@ extern "C" int srbd_shm_read(const uint64_t* seq, const double* payload, srbd_sh
     m->stamp = d[SRBD_SHM_STAMP];
     if (seq_out) *seq_out = s2;
     return 1;
+}
+
+// ------------------------------------------------------------------ jax.random keys (srbd_jaxrng.h)
+extern "C" int srbd_jax_prng_key(uint64_t seed, uint32_t key_out[2]) {  // threefry_seed
+    if (!key_out) return SRBD_E_INVALID;
+    key_out[0] = (uint32_t)(seed >> 32);
+    key_out[1] = (uint32_t)seed;
+    return SRBD_OK;
+}
+
+extern "C" int srbd_jax_split(const uint32_t key[2], int32_t num, int32_t partitionable, uint32_t* out) {
+    if (!key || !out || num < 1) return SRBD_E_INVALID;
+    // partitionable: key i = threefry(key, (0, i)); legacy: the 2 num bits of iota(2 num), reshaped (num, 2)
+    for (int32_t i = 0; i < num; ++i) {
+        if (partitionable) {
+            uint32_t x0 = 0, x1 = (uint32_t)i;
+            srbd::threefry2x32_20(key[0], key[1], x0, x1);
+            out[2 * i] = x0;
+            out[2 * i + 1] = x1;
+        } else {
+            const uint64_t M = 2 * (uint64_t)num;
+            out[2 * i] = srbd::jax_bits(key[0], key[1], 2 * (uint64_t)i, M, false);
+            out[2 * i + 1] = srbd::jax_bits(key[0], key[1], 2 * (uint64_t)i + 1, M, false);
+        }
+    }
+    return SRBD_OK;
 }

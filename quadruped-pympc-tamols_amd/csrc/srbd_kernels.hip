@@ -1201,11 +1201,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
             // chain: the next draws come from the device RNG.  (Split: slices read noise_scaled too, but a
             // chain's steps all run with it 0 already -- reset_noise_scaled -- so this store never changes it.)
             if (chain) in->noise_scaled = 0;
-            if (chain && ctr_inc) {
-                const uint64_t cc = (((uint64_t)in->ctr_hi << 32) | in->ctr_lo) + (uint64_t)ctr_inc;
-                in->ctr_lo = (uint32_t)cc;
-                in->ctr_hi = (uint32_t)(cc >> 32);
-            }
+            if (chain && ctr_inc) advance_key(mc, in, ctr_inc);
         }
         if (chain)
             for (int i = tid; i < ncol; i += T) {
@@ -1326,11 +1322,13 @@ size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride) {
 // sampling, grouped records, and the merge's LDS inside the stage (64 x 12 H floats).
 // The step input as a kernel argument (StepInputK): the zero-order four-lane kernel with the LDS noise stage,
 // MPPI / random sampling (no sigma in the argument), P <= KSI_MAXP; SRBD_KS=0 disables (read per context).
+static bool ks_shape_ok(const ModelConst& mc, int mode) {
+    if ((mode != ROLLOUT_QUAD && mode != ROLLOUT_THREAD) || mc.kind != SRBD_ZERO_ORDER) return false;
+    return (mc.H == 10 || mc.H == 12) && mc.method != SRBD_CEM_MPPI && mc.P <= KSI_MAXP;
+}
 bool ks_ok(const ModelConst& mc, int mode) {
     const char* e = getenv("SRBD_KS");
-    if ((e && atoi(e) == 0) || (mode != ROLLOUT_QUAD && mode != ROLLOUT_THREAD) || mc.kind != SRBD_ZERO_ORDER)
-        return false;
-    return (mc.H == 10 || mc.H == 12) && mc.method != SRBD_CEM_MPPI && mc.P <= KSI_MAXP;
+    return !(e && atoi(e) == 0) && ks_shape_ok(mc, mode);
 }
 
 bool final_merge_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride) {
@@ -1430,11 +1428,7 @@ __global__ void advance_kernel(const ModelConst mc, StepInput* __restrict__ in, 
         in->best[j] = out->best[j];
         if (mc.method == SRBD_CEM_MPPI) in->sigma[j] = out->sigma[j];
     }
-    if (threadIdx.x == 0) {
-        const uint64_t c = (((uint64_t)in->ctr_hi << 32) | in->ctr_lo) + 1;
-        in->ctr_lo = (uint32_t)c;
-        in->ctr_hi = (uint32_t)(c >> 32);
-    }
+    if (threadIdx.x == 0) advance_key(mc, in, 1);
 }
 
 __global__ void div_selftest_kernel(const float* a, const float* b, int n, float* o) {
@@ -1536,8 +1530,12 @@ static void launch_rollout_ga(const ModelConst& mc, const StepInput* in, const f
 void launch_rollout(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
                     int rec_stride, int mode, int threads, hipStream_t s, const RngJob* next, const GroupArgs& grp_in) {
     GroupArgs grp = grp_in;
-    if (grp.ksi && (mc.ga || mc.cost_on || !ks_ok(mc, mode))) {  // no KS kernel for this launch: upload instead
-        (void)hipMemcpyAsync(const_cast<StepInput*>(in), grp.ksi, sizeof(StepInputK), hipMemcpyHostToDevice, s);
+    // No KS kernel for this launch: copy the input up instead.  Not reached from the library (the context
+    // decides KS once, at create, with this same shape test, and passes no input to the gait-adaptive or
+    // cost-term kernels); a blocking copy, since `ksi` is the caller's stack object.
+    if (grp.ksi && (mc.ga || mc.cost_on || !ks_shape_ok(mc, mode))) {
+        (void)hipStreamSynchronize(s);
+        (void)hipMemcpy(const_cast<StepInput*>(in), grp.ksi, sizeof(StepInputK), hipMemcpyHostToDevice);
         grp.ksi = nullptr;
     }
     if (mc.ga) return launch_rollout_ga(mc, in, noise, costs, recs, rec_stride, mode, threads, s, next, grp);
@@ -1581,7 +1579,8 @@ int group_size(int nblocks, int rec_stride, int method) {
 }
 
 int rng_grid(const ModelConst& mc) {
-    const long items = (long)mc.n_local * ((mc.P + 3) / 4);
+    // Philox: one item per (row, column quad); the JAX stream: one per element
+    const long items = (long)mc.n_local * (mc.rng != RNG_PHILOX ? mc.P : (mc.P + 3) / 4);
     const long blocks = (items + 255) / 256;
     return (int)(blocks < 2048 ? blocks : 2048);
 }

@@ -27,6 +27,11 @@ constexpr int GROUP_MAX = 64;      // records one group merges (one wave's lanes
 constexpr int GROUP_TARGET = 32;   // groups per launch the sizing aims at (group_size)
 constexpr int GROUP_LDS_FLOATS = 6144;  // the last arriver stages its group's records in LDS (24 KB)
 constexpr int GROUP_MIN_BLOCKS = 512;   // grouping pays from here on (MPPI / random sampling)
+// Memory-model note: the hand-off (record stores write-through, `s_waitcnt vmcnt(0)`, a block barrier, one
+// relaxed agent-scope fetch_add; the last arriver reads the records with sc1 loads) relies on gfx950's codegen
+// for agent-scope relaxed atomics (sc1 stores / loads that go past the per-CU caches and the per-XCD L2s, which
+// are not coherent with each other, and complete device-wide before vmcnt drops: a group's blocks sit on all
+// eight XCDs), the pattern of MI355X_MICROARCH.md's hand-off table, not on HIP release / acquire ordering.
 struct GroupArgs {
     float* grecs;   // ngroups x rec_stride
     uint32_t* cnt;  // ngroups arrival counters, zero between launches (each group's last arriver resets its own)

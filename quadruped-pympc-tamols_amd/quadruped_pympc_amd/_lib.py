@@ -152,7 +152,20 @@ SIGNATURES.update({
                                      C.POINTER(TamolsParams), _P, _P, _P, _P, _P, _P]),
     "srbd_tamols_phases": (_I, [_P, _I, _FP]),
     "srbd_tamols_phases_raw": (_I, [_P, _P]),
+    "srbd_set_rng": (_I, [_P, _I]),
+    "srbd_get_rng": (_I, [_P]),
+    "srbd_draw_noise": (_I, [_P, C.c_uint64, C.c_uint64, _FP]),
+    "srbd_time_launch": (_I, [_P, _I, _I, _FP, _IP]),
+    "srbd_jax_prng_key": (_I, [C.c_uint64, _P]),
+    "srbd_jax_split": (_I, [_P, _I, _I, _P]),
 })
+
+# srbd_time_launch kinds (include/srbd_mpc.h)
+TL_RNG, TL_ROLLOUT, TL_ROLLOUT_FUSED, TL_STEP_ROLLOUT, TL_STEP_MERGE, TL_EMPTY = range(6)
+
+# device noise streams (include/srbd_mpc.h srbd_set_rng)
+RNG_PHILOX, RNG_JAX, RNG_JAX_LEGACY = 0, 1, 2
+RNG_CODES = {"philox": RNG_PHILOX, "jax": RNG_JAX, "jax_legacy": RNG_JAX_LEGACY}
 
 LIB_NAME = "libsrbd_hip.so"
 LIB_PATH = os.environ.get("SRBD_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
@@ -258,6 +271,28 @@ def make_config(*, num_samples, horizon, method, parametrization, num_splines=2,
     for i in range(3):
         cfg.sigma_random_sampling[i] = float(np.float32(sigma_random_sampling[i]))
     return cfg
+
+
+def jax_prng_key(seed: int) -> np.ndarray:
+    """srbd_jax_prng_key: jax.random.PRNGKey(seed) as uint32[2] (centroidal_nmpc_jax.py:167)."""
+    key = np.zeros(2, np.uint32)
+    check(lib.srbd_jax_prng_key(int(seed) & 0xFFFFFFFFFFFFFFFF, key.ctypes.data), None, "srbd_jax_prng_key")
+    return key
+
+
+def jax_split(key, num: int = 2, partitionable: bool = True) -> np.ndarray:
+    """srbd_jax_split: jax.random.split(key, num) -> (num, 2) uint32 (with_newkey, centroidal_nmpc_jax.py:498-501)."""
+    k = np.ascontiguousarray(np.asarray(key, np.uint32).reshape(2))
+    out = np.zeros((int(num), 2), np.uint32)
+    check(lib.srbd_jax_split(k.ctypes.data, int(num), 1 if partitionable else 0, out.ctypes.data), None,
+          "srbd_jax_split")
+    return out
+
+
+def pack_key(key) -> int:
+    """The `seed` argument of srbd_step in a JAX stream mode: key[0] << 32 | key[1]."""
+    k = np.asarray(key, np.uint32).reshape(2)
+    return (int(k[0]) << 32) | int(k[1])
 
 
 def num_params(cfg: SrbdConfig) -> int:
@@ -438,7 +473,19 @@ class Context:
         out = {"rollout_us": r.value, "rng_us": g.value, "merge_us": m.value, "event_floor_us": fl.value}
         if f.value > 0:  # rollout launch carrying the next step's draws (what the step chain runs)
             out["fused_rollout_us"] = f.value
+        if self.cfg.world_size <= 1:  # the two launches srbd_step issues, exactly as it issues them
+            us, form = self.time_launch(TL_STEP_ROLLOUT, iters)
+            out["step_rollout_us"] = us
+            out["step_rollout_form"] = form
+            out["step_merge_us"] = self.time_launch(TL_STEP_MERGE, iters)[0]
         return out
+
+    def time_launch(self, which: int, iters: int = 200):
+        """srbd_time_launch: (average us of `iters` back-to-back launches of one kind, form bits)."""
+        us, form = _F(0), _I(0)
+        self.check(lib.srbd_time_launch(self.h, int(which), int(iters), C.byref(us), C.byref(form)),
+                   "srbd_time_launch")
+        return float(us.value), int(form.value)
 
     def merge_phases(self, iters: int = 50):
         """Merge phase durations (us) of block 0; `slice_block`: the same for block 1 of a column-split merge."""
@@ -502,3 +549,18 @@ class Context:
 
     def record_floats(self) -> int:
         return int(lib.srbd_record_floats(self.h))
+
+    def set_rng(self, kind):
+        """srbd_set_rng: 'philox' (default), 'jax' (the reference's jax.random stream, partitionable threefry) or
+        'jax_legacy' (jax_threefry_partitionable=False).  In the JAX modes `seed` is the packed key (pack_key)."""
+        code = RNG_CODES[kind] if isinstance(kind, str) else int(kind)
+        self.check(lib.srbd_set_rng(self.h, code), "srbd_set_rng")
+
+    def rng(self) -> int:
+        return int(lib.srbd_get_rng(self.h))
+
+    def draw_noise(self, seed: int, counter: int = 0) -> np.ndarray:
+        """srbd_draw_noise: the device draws of a step keyed by (seed, counter), (n_local, P) row-major."""
+        out = np.zeros((self.n_local, self.P), np.float32)
+        self.check(lib.srbd_draw_noise(self.h, int(seed), int(counter), fptr(out)), "srbd_draw_noise")
+        return out

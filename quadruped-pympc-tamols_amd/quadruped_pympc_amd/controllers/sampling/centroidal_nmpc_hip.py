@@ -15,14 +15,20 @@ that produces the GRFs, the predicted state and the updated parameters.  The
 HIP context is created on the first compute call (so construction is fork- and
 thread-safe, like the reference's lazy XLA compile); there is no CPU fallback.
 
-Differences from the reference, by design:
+Noise streams (``mpc_params['rng']``, not a reference key):
 
-* ``master_key`` is ``np.uint64[2] = (seed, counter)`` for the device Philox RNG
-  (JAX's threefry stream cannot be reproduced offline); ``with_newkey`` advances
-  the counter.  Pass ``noise=`` (the (N, P) ``additional_random_parameters``) to
-  any compute call to inject the sampled perturbations exactly.
-* ``costs`` (unused by every reference caller) is returned as a lazy array that
-  copies from the device on first access.
+* ``'jax'`` (default): the reference's own ``jax.random`` stream, drawn on the device
+  (``include/srbd_mpc.h`` ``srbd_set_rng``).  ``master_key`` is ``jax.random.PRNGKey(42)``
+  as ``np.uint32[2]`` and ``with_newkey`` is ``split(master_key)[0]``, as in the
+  reference (centroidal_nmpc_jax.py:167, :498-501), so the same key gives the same
+  noise.  ``mpc_params['jax_threefry_partitionable']`` (default True, JAX >= 0.5)
+  selects the counter layout of older JAX releases when False.
+* ``'philox'``: this library's Philox4x32-10 stream; ``master_key`` is
+  ``np.uint64[2] = (seed, counter)`` and ``with_newkey`` advances the counter.
+
+Pass ``noise=`` (the (N, P) ``additional_random_parameters``) to any compute call to
+inject the sampled perturbations exactly.  ``costs`` (unused by every reference
+caller) is returned as a lazy array that copies from the device on first access.
 """
 from __future__ import annotations
 
@@ -140,7 +146,17 @@ class Sampling_MPC:
         self.f_z_min = mp["grf_min"]
 
         self.best_control_parameters = np.zeros((self.num_control_parameters,), dtype=f32)
-        self.master_key = np.array([42, 0], dtype=np.uint64)
+        rng = mp.get("rng", "jax")
+        if rng == "jax" and not mp.get("jax_threefry_partitionable", True):
+            rng = "jax_legacy"
+        if rng not in _lib.RNG_CODES:
+            raise ValueError(f"mpc_params['rng'] must be one of {sorted(_lib.RNG_CODES)}")
+        self.rng = rng
+        if rng == "philox":
+            self.master_key = np.array([42, 0], dtype=np.uint64)
+        else:
+            self.master_key = _lib.jax_prng_key(42)  # jax.random.PRNGKey(42), centroidal_nmpc_jax.py:167
+        self._calls = 0  # numbers the device steps (the draws made ahead are keyed by the next key and call)
         self._ctx = None
 
     # ------------------------------------------------------------------ device
@@ -170,14 +186,24 @@ class Sampling_MPC:
             # controller process that owns its GPU queue; 'armed_deadline_us' bounds the wait (default 50 ms)
             if self._cfg.mpc_params.get("armed_steps", False):
                 self._ctx.set_armed(True, int(self._cfg.mpc_params.get("armed_deadline_us", 0)))
+            if self.rng != "philox":
+                self._ctx.set_rng(self.rng)
         return self._ctx
+
+    def _key_args(self, key):
+        """(seed, counter) of srbd_step for a compute call's `key`."""
+        if self.rng == "philox":
+            key = np.asarray(key, dtype=np.uint64).reshape(-1)
+            return int(key[0]), (int(key[1]) if key.shape[0] > 1 else 0)
+        self._calls += 1
+        return _lib.pack_key(np.asarray(key, dtype=np.uint32)), self._calls
 
     def _run(self, state, reference, contact_sequence, best_control_parameters, key, sigma, noise):
         ctx = self.context
-        key = np.asarray(key, dtype=np.uint64).reshape(-1)
+        seed, counter = self._key_args(key)
         best, new_sigma, res, _ = ctx.step(state, reference, np.asarray(contact_sequence, dtype=f32),
-                                           best_control_parameters, sigma=sigma, noise=noise, seed=int(key[0]),
-                                           counter=int(key[1]) if key.shape[0] > 1 else 0)
+                                           best_control_parameters, sigma=sigma, noise=noise, seed=seed,
+                                           counter=counter)
         self.last_result = res
         grf = np.array(res.grf, dtype=f32)
         pred = np.array(res.predicted_state, dtype=f32)
@@ -208,7 +234,10 @@ class Sampling_MPC:
 
     # ------------------------------------------------------------------ keys / sigma (:498-511)
     def with_newkey(self):
-        self.master_key = np.array([self.master_key[0], self.master_key[1] + np.uint64(1)], dtype=np.uint64)
+        if self.rng == "philox":
+            self.master_key = np.array([self.master_key[0], self.master_key[1] + np.uint64(1)], dtype=np.uint64)
+        else:  # newkey, subkey = jax.random.split(master_key); master_key = newkey
+            self.master_key = _lib.jax_split(self.master_key, 2, self.rng == "jax")[0]
         return self
 
     def get_key(self):
@@ -295,7 +324,7 @@ class Sampling_MPC:
         plus, once a context exists and has stepped, the device-resident chain state (``device_*``,
         ``srbd_get_state``).  ``set_state`` of it makes the following calls replay bit for bit."""
         st = {"best_control_parameters": np.array(self.best_control_parameters, dtype=f32).reshape(-1),
-              "master_key": np.array(self.master_key, dtype=np.uint64).reshape(-1)}
+              "master_key": np.array(self.master_key).reshape(-1)}  # uint32[2] (JAX key) or uint64[2] (Philox)
         if self.sampling_method == "cem_mppi":
             st["sigma_cem_mppi"] = np.array(np.broadcast_to(np.asarray(self.sigma_cem_mppi, dtype=f32),
                                                             (self.num_control_parameters,)), dtype=f32)
@@ -313,7 +342,7 @@ class Sampling_MPC:
         step, since srbd_set_state needs that step's state/reference inputs.  A fresh controller drops the
         device part with a RuntimeWarning: its compute calls start from the host part anyway."""
         self.best_control_parameters = np.array(st["best_control_parameters"], dtype=f32).reshape(-1)
-        self.master_key = np.array(st["master_key"], dtype=np.uint64).reshape(-1)
+        self.master_key = np.array(st["master_key"], dtype=np.uint64 if self.rng == "philox" else np.uint32).reshape(-1)
         if "sigma_cem_mppi" in st:
             self.sigma_cem_mppi = np.array(st["sigma_cem_mppi"], dtype=f32)
         if "device_best" in st:

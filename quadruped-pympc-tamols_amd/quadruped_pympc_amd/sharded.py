@@ -74,6 +74,8 @@ class ShardedSamplingMPC:
     transport="rccl": the library owns an RCCL communicator (rank 0's ncclUniqueId is broadcast over
     the torch process group once) and runs rollout -> ncclAllGather -> merge from C++ on its own
     stream, so no Python sits between the kernels and the collective.
+    rng: the device noise stream ('philox', or 'jax' / 'jax_legacy': the reference's jax.random stream keyed
+    by the packed key, _lib.pack_key; draws are indexed by global row, so they are the same for any W).
     transport="torch": the record goes through torch.distributed.all_gather_into_tensor on a
     dedicated torch stream shared with the library (the legacy null stream cannot be handed to
     srbd_set_stream: a NULL handle selects the context's own stream).  Measured on one GPU: this
@@ -81,12 +83,14 @@ class ShardedSamplingMPC:
     """
 
     def __init__(self, cfg: _lib.SrbdConfig, rank: int, world: int, device_index: int, group=None,
-                 transport: str = "auto"):
+                 transport: str = "auto", rng: str = "philox"):
         import torch
 
         cfg.rank, cfg.world_size, cfg.device_id = int(rank), int(world), int(device_index)
         cfg.use_graph = 0
         self.ctx = _lib.Context(cfg)
+        if rng != "philox":  # the reference's jax.random stream: `seed` of step() is the packed key
+            self.ctx.set_rng(rng)
         self.rank, self.world = rank, world
         self.device = torch.device("cuda", device_index)
         self.P = self.ctx.P

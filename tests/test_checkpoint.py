@@ -11,14 +11,17 @@ from tests.helpers import make_case, product_cfg
 f32 = np.float32
 
 
-def _controller(method):
+def _controller(method, rng=None):
     from quadruped_pympc_amd.controllers.sampling.centroidal_nmpc_hip import Sampling_MPC
 
     mirror.mpc_params["sampling_method"] = method
+    if rng is not None:
+        mirror.mpc_params["rng"] = rng
     try:
         return Sampling_MPC(mirror)
     finally:
         mirror.mpc_params["sampling_method"] = "mppi"
+        mirror.mpc_params.pop("rng", None)
 
 
 def test_set_state_warns_when_device_part_dropped():
@@ -32,10 +35,11 @@ def test_set_state_warns_when_device_part_dropped():
     assert mpc.master_key[1] == st["master_key"][1]
 
 
+@pytest.mark.parametrize("stream", ["jax", "philox"])
 @pytest.mark.parametrize("method", ["random_sampling", "mppi", "cem_mppi"])
-def test_controller_state_round_trip_without_device(method):
+def test_controller_state_round_trip_without_device(method, stream):
     """get_state -> np.savez -> np.load (no pickle) -> set_state restores every evolving attribute."""
-    mpc = _controller(method)
+    mpc = _controller(method, stream)
     rng = np.random.default_rng(3)
     mpc.best_control_parameters = rng.standard_normal(mpc.num_control_parameters).astype(f32)
     mpc.with_newkey().with_newkey()
@@ -48,11 +52,17 @@ def test_controller_state_round_trip_without_device(method):
     buf.seek(0)
     loaded = dict(np.load(buf, allow_pickle=False))
 
-    other = _controller(method)
+    other = _controller(method, stream)
     other.set_state(loaded)
     np.testing.assert_array_equal(other.best_control_parameters, mpc.best_control_parameters)
     np.testing.assert_array_equal(other.master_key, mpc.master_key)
-    assert other.master_key[1] == 2
+    assert other.master_key.dtype == mpc.master_key.dtype
+    if stream == "philox":
+        assert other.master_key[1] == 2
+    else:  # two with_newkey calls from PRNGKey(42)
+        from oracle import jax_random_oracle as jr
+
+        np.testing.assert_array_equal(other.master_key, jr.with_newkey(jr.with_newkey(jr.prng_key(42))))
     if method == "cem_mppi":
         np.testing.assert_array_equal(other.sigma_cem_mppi, mpc.sigma_cem_mppi)
 

@@ -120,8 +120,9 @@ def test_sampling_mpc_attributes(method, par, P):
         assert m.sigma_cem_mppi.shape == (P,) and np.all(m.sigma_cem_mppi == 3)
     assert m._ctx is None  # no device work at construction
     k0 = m.master_key.copy()
+    np.testing.assert_array_equal(k0, [0, 42])  # jax.random.PRNGKey(42) (NMPC:167), the default 'jax' stream
     assert m.with_newkey() is m
-    assert m.master_key[1] == k0[1] + 1 and m.master_key[0] == k0[0]
+    np.testing.assert_array_equal(m.master_key, _lib.jax_split(k0, 2)[0])  # NMPC:498-501
     assert m.with_newsigma(np.full(P, 2.0)) is m and np.all(m.get_sigma() == 2.0)
     cfg = m._srbd_config()
     assert _lib.num_params(cfg) == P
@@ -244,7 +245,11 @@ def test_interface_masks_grfs_and_reassigns_params():
     contact[1, 0] = 0
     grfs, fh, _, _, _, freq, pred = itf.compute_control(sc, rs, contact, None, None, 1.4, 0)
     assert len(calls) == 3
-    assert [int(k[1]) for k, _ in calls] == [1, 2, 3]  # with_newkey before each iteration
+    # with_newkey before each iteration: master_key <- split(master_key)[0] from PRNGKey(42) (NMPC:498-501)
+    k = _lib.jax_prng_key(42)
+    for key, _ in calls:
+        k = _lib.jax_split(k, 2)[0]
+        np.testing.assert_array_equal(key, k)
     np.testing.assert_array_equal(calls[2][1], calls[0][1] + 2)  # best reassigned between iterations
     np.testing.assert_array_equal(grfs.FR, np.zeros(3))
     np.testing.assert_array_equal(grfs.FL, [1, 2, 3])
