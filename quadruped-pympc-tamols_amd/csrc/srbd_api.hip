@@ -33,12 +33,12 @@ int rollout_threads(int n_local) {
     return 256;
 }
 // Four lanes per sample unless the samples alone fill the GPU (measured crossover: zero-order
-// N ~ 65536, splines beyond 262144; scripts/kernel_sweep.py).  Override with SRBD_ROLLOUT=thread|quad.
+// N ~ 65536, splines beyond 262144; scripts/kernel_sweep.py).  SRBD_ROLLOUT=thread|quad (read at create)
+// picks the other of the two forms at a shape (tests: both give the same costs bit for bit; measurement).
 int rollout_mode(int kind, int n_local) {
     const char* e = getenv("SRBD_ROLLOUT");
     if (e && !strcmp(e, "thread")) return ROLLOUT_THREAD;
     if (e && !strcmp(e, "quad")) return ROLLOUT_QUAD;
-    if (e && !strcmp(e, "pair")) return ROLLOUT_PAIR;
     const int quad_max = kind == SRBD_ZERO_ORDER ? 65536 : 524288;
     return n_local <= quad_max ? ROLLOUT_QUAD : ROLLOUT_THREAD;
 }
@@ -357,8 +357,7 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     c->mode = rollout_mode(mc.kind, mc.n_local);
     // the four-lane kernel addresses noise through a buffer descriptor (31-bit byte offsets)
     if ((long long)mc.P * mc.ldn * 4 >= (1LL << 31)) c->mode = ROLLOUT_THREAD;
-    c->threads = c->mode == ROLLOUT_QUAD ? 4 * quad_samples_per_block(mc.n_local)
-                                         : (c->mode == ROLLOUT_PAIR ? 256 : rollout_threads(mc.n_local));
+    c->threads = c->mode == ROLLOUT_QUAD ? 4 * quad_samples_per_block(mc.n_local) : rollout_threads(mc.n_local);
     c->ks = ks_ok(mc, c->mode);  // srbd_step, and the xGMI sharded step (xg_step)
     const int spb = rollout_spb(c->mode, c->threads);  // samples per rollout block
     c->nblocks = (mc.n_local + spb - 1) / spb;
@@ -491,11 +490,9 @@ extern "C" int srbd_set_stream(srbd_ctx* c, void* s) {
 // Draw the next step's noise inside the rollout launch (extra blocks beside the rollout).  The draws
 // never depend on the step (CEM stores unscaled normals, scaled by sigma on read).  Measured per
 // step: N = 65 536 MPPI 64.2 -> 53.9 us, CEM cubic H16 98.4 -> 89.9 us, CEM N = 10 000 52.4 ->
-// 48.3 us; SRBD_FUSE_MAX overrides the row limit.
-static bool fusable(const srbd_ctx* c) {
-    static const int fuse_max = tune_knob("SRBD_FUSE_MAX", 65536);
-    return c->mc.n_local <= fuse_max;
-}
+// 48.3 us.  Above 65 536 rows the rollout fills every CU and the fused draws slow it.
+constexpr int FUSE_MAX_ROWS = 65536;
+static bool fusable(const srbd_ctx* c) { return c->mc.n_local <= FUSE_MAX_ROWS; }
 
 // Device-chain steps draw on the device: CEM draws are then unscaled (StepInput::noise_scaled = 0)
 // whatever the last host step injected.
@@ -538,18 +535,13 @@ static int acquire_noise(srbd_ctx* c, const float* noise, uint64_t seed, uint64_
 
 // rollout (+ next draws, counter + 1 from the device StepInput) -> merge on noise buffer `buf`
 // The step's StepInput into device memory: a one-block copy kernel pulling it from the mapped pinned
-// staging (host step p50 36.4 -> 35.1 us, p99 51.8 -> 44.0 at C2), or with SRBD_UPLOAD_MEMCPY=1 an
-// async H2D copy.
+// staging (host step p50 36.4 -> 35.1 us, p99 51.8 -> 44.0 at C2, against an async H2D copy): the header
+// and best[P] (+ sigma[P] for CEM), the bytes the step reads.
 static int upload_input(srbd_ctx* c) {
-    static const int memcpy_upload = tune_knob("SRBD_UPLOAD_MEMCPY", 0);
-    if (!memcpy_upload) {  // the header and best[P] (+ sigma[P] for CEM): the bytes the step reads
-        const size_t P4 = sizeof(float) * (size_t)c->mc.P;
-        const size_t sig = offsetof(StepInput, sigma);
-        launch_copy16(c->d_in_host, c->d_in, offsetof(StepInput, best) + P4, sig,
-                      c->mc.method == SRBD_CEM_MPPI ? P4 : 0, c->stream);
-        return SRBD_OK;
-    }
-    HIP_TRY(c, hipMemcpyAsync(c->d_in, c->h_in, sizeof(StepInput), hipMemcpyHostToDevice, c->stream));
+    const size_t P4 = sizeof(float) * (size_t)c->mc.P;
+    const size_t sig = offsetof(StepInput, sigma);
+    launch_copy16(c->d_in_host, c->d_in, offsetof(StepInput, best) + P4, sig, c->mc.method == SRBD_CEM_MPPI ? P4 : 0,
+                  c->stream);
     return SRBD_OK;
 }
 

@@ -246,11 +246,7 @@ SRBD_HD void euler_rates(float sr, float cr, float sp, float cp, float w0, float
     er[2] = euler_rate_row(2, k[4], k[5], w0, w1, w2);
 }
 
-// Model constants as the rollout reads them: straight from ModelConst (host, merge tail, four-lane
-// kernel), or from an LDS copy (thread kernel: read per step behind a scheduling barrier, so the ~50
-// uniform values are not all held in SGPRs across the unrolled horizon; see rollout_kernel).
-// LDS layout (KC_*): inv_m | inertia[9] | Iinv[9] | grf_min, grf_max, mu, neg_mu | Q[12] | ref[12] | feet[12]
-enum { KC_INVM = 0, KC_I = 1, KC_IINV = 10, KC_LIM = 20, KC_Q = 24, KC_REF = 36, KC_FEET = 48, KC_N = 60 };
+// Model constants as the rollout reads them (the KC template parameter of integrate_k / clip_leg_k / shape_leg_k).
 struct McConst {
     const ModelConst& m;
     SRBD_HD float inv_m() const { return m.inv_m; }
@@ -261,22 +257,11 @@ struct McConst {
     SRBD_HD float mu() const { return m.mu; }
     SRBD_HD float neg_mu() const { return m.neg_mu; }
 };
-struct LdsConst {
-    const float* k;  // KC_* layout
-    SRBD_HD float inv_m() const { return k[KC_INVM]; }
-    SRBD_HD const float* inertia() const { return k + KC_I; }
-    SRBD_HD const float* Iinv() const { return k + KC_IINV; }
-    SRBD_HD float grf_min() const { return k[KC_LIM]; }
-    SRBD_HD float grf_max() const { return k[KC_LIM + 1]; }
-    SRBD_HD float mu() const { return k[KC_LIM + 2]; }
-    SRBD_HD float neg_mu() const { return k[KC_LIM + 3]; }
-};
 
 // Centroidal_Model_JAX.fd + integrate_jax (CMJ:93-174).  x: 12 evolving states, feet: 12
 // (constant over the rollout), F: 12 clipped foot forces, c: 4 contact flags.
 // The rigid-body part of the step, from the contact-weighted force sum temp = sum_i f_i c_i and torque sum
-// temp2 = sum_i (p_i - p_com) x f_i c_i (integrate_k forms both; the two-lane kernel forms them split over
-// its lanes, rollout_pair_kernel).
+// temp2 = sum_i (p_i - p_com) x f_i c_i (integrate_k forms both).
 template <class KC>
 SRBD_HD void integrate_rb_k(const KC& kc, float x[12], const float temp[3], const float temp2[3], float dt) {
     float lin_acc[3];
@@ -320,8 +305,7 @@ template <class KC>
 SRBD_HD void integrate_k(const KC& kc, float x[12], const float feet[12], const float F[12], const float c[4],
                          float dt) {
     // leg sums pairwise, (leg0 + leg1) + (leg2 + leg3): the four-lane kernel forms them with one quad
-    // butterfly over leg-parallel lanes (rollout_quad_kernel), the two-lane kernel as one pair sum per
-    // lane plus one exchange (rollout_pair_kernel), and every layout uses this order
+    // butterfly over leg-parallel lanes (rollout_quad_kernel), and every layout uses this order
     float temp[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) temp[k] = (F[k] * c[0] + F[3 + k] * c[1]) + (F[6 + k] * c[2] + F[9 + k] * c[3]);

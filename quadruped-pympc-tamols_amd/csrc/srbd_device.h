@@ -451,10 +451,7 @@ template <int SPL>
 __device__ __forceinline__ void block_wsum_tree(const ModelConst& mc, const StepInput* __restrict__ in,
                                                 const float* __restrict__ base, bool zs, const float* e_sh,
                                                 float* rec) {
-#ifndef SRBD_WSUM_CB
-#define SRBD_WSUM_CB 8
-#endif
-    constexpr int CB = SPL == 4 ? SRBD_WSUM_CB : 12;  // columns per batch of loads
+    constexpr int CB = SPL == 4 ? 8 : 12;  // columns per batch of loads (8 / 12 / 16 / 20 at SPL 4 within noise)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, NW = blockDim.x >> 6;
     const int P = mc.P;
     const size_t ldn = (size_t)mc.ldn;

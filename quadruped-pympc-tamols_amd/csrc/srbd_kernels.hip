@@ -314,14 +314,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     // instead of the whole horizon up front -- the terms' extra live values otherwise push the unrolled
     // horizon past 256 VGPRs into scratch.
     constexpr int PW = (EXT && KIND == SRBD_ZERO_ORDER) ? (NPRE < 4 ? NPRE : 4) : NPRE;
-    // CEM cubic splines with S > 1: chunk q's four slots are loaded SRBD_CLEAD steps before its first step
+    // CEM cubic splines with S > 1: chunk q's four slots are loaded CLEAD steps before its first step
     // instead of up front.  C3 (H16 CEM): 80 -> 16 B of scratch per lane, rollout 41.8 -> 37.9 us, device
     // step 73.1 -> 65.5 us (r3d); leads 3 / 4 spill again (80 / 144 B), and the plain cubic kernels spill
     // more with the window (H16: 48 -> 144 B at lead 2), so they keep the up-front loads.
-#ifndef SRBD_CLEAD
-#define SRBD_CLEAD 2
-#endif
-    constexpr bool CWIN = CT && CEMT && KIND == SRBD_CUBIC_SPLINE && ST > 1 && SRBD_CLEAD > 0;
+    constexpr int CLEAD = 2;
+    constexpr bool CWIN = CT && CEMT && KIND == SRBD_CUBIC_SPLINE && ST > 1;
     if constexpr (CWIN) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) load_slot(i);
@@ -343,7 +341,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
         if constexpr (CWIN) {
 #pragma unroll
             for (int q = 1; q < (CWIN ? ST : 1); ++q) {
-                const int at = q * HT / ST - SRBD_CLEAD;
+                const int at = q * HT / ST - CLEAD;
                 if (n == (at > 0 ? at : 0))
 #pragma unroll
                     for (int i = 4 * q; i < 4 * q + 4; ++i) load_slot(i);
@@ -646,17 +644,12 @@ __device__ __forceinline__ uint64_t rec_key(const float* R, int P, int q) {
 }
 
 constexpr int MERGE_THREADS = 1024;
-#ifndef SRBD_MERGE_PREF
-#define SRBD_MERGE_PREF 24
-#endif
-constexpr int MERGE_PREF = SRBD_MERGE_PREF;  // record values of the weighted sums loaded per thread before beta is known
+constexpr int MERGE_PREF = 24;  // record values of the weighted sums loaded per thread before beta is known
 constexpr int MERGE_RPT = 8;    // record headers per thread (nrec <= MERGE_RPT * MERGE_THREADS)
 // The LDS-staged merge runs two waves per SIMD: its phases are short dependent chains that every
 // wave repeats (index math, the beta reduction), so 16 waves pay ~2x the issue of 8, while fewer
 // waves stage the records more slowly (C2 merge 9.0 / 8.4 / 9.8 us at 1024 / 512 / 256 threads).
-#ifndef MERGE_STAGE_THREADS
-#define MERGE_STAGE_THREADS 512
-#endif
+constexpr int MERGE_STAGE_THREADS = 512;
 // Block-wide K smallest record keys (ascending) into `elite`, by selection and ranks.  Every record's
 // key list is the sorted K smallest keys of its samples, so its first key is its minimum, and the K
 // smallest keys overall lie in the K records with the smallest minima (any other record's minimum already
@@ -1322,19 +1315,14 @@ size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride) {
 // sampling, grouped records, and the merge's LDS inside the stage (64 x 12 H floats).
 // The step input as a kernel argument (StepInputK): the zero-order four-lane kernel with the LDS noise stage,
 // MPPI / random sampling (no sigma in the argument), P <= KSI_MAXP; SRBD_KS=0 disables (read per context).
-static bool ks_shape_ok(const ModelConst& mc, int mode) {
+bool ks_ok(const ModelConst& mc, int mode) {
     if ((mode != ROLLOUT_QUAD && mode != ROLLOUT_THREAD) || mc.kind != SRBD_ZERO_ORDER) return false;
     return (mc.H == 10 || mc.H == 12) && mc.method != SRBD_CEM_MPPI && mc.P <= KSI_MAXP;
 }
-bool ks_ok(const ModelConst& mc, int mode) {
-    const char* e = getenv("SRBD_KS");
-    return !(e && atoi(e) == 0) && ks_shape_ok(mc, mode);
-}
 
 bool final_merge_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride) {
-    const char* e = getenv("SRBD_FINAL_MERGE");  // 0 disables (read per context: tests compare both)
     // (the gait-adaptive rollout and the cost terms, which can be switched on later, are checked per launch)
-    if ((e && atoi(e) == 0) || mode != ROLLOUT_QUAD || mc.kind != SRBD_ZERO_ORDER) return false;
+    if (mode != ROLLOUT_QUAD || mc.kind != SRBD_ZERO_ORDER) return false;
     if ((mc.H != 10 && mc.H != 12) || mc.method == SRBD_CEM_MPPI || ngroups < 1) return false;
     const size_t zst = sizeof(float) * (size_t)(64 * 12 * mc.H > GROUP_LDS_FLOATS ? 64 * 12 * mc.H : GROUP_LDS_FLOATS);
     return final_merge_lds(mc, ngroups, rec_stride) <= zst;
@@ -1478,8 +1466,6 @@ static void launch_rollout_t(const ModelConst& mc, const StepInput* in, const fl
         else
             hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, EXT>), grid, dim3(threads), 0, s, KsNone{}, mc, in, noise,
                                costs, recs, rec_stride, job, blocks, grp);
-    } else if (mode == ROLLOUT_PAIR) {
-        launch_rollout_pair(mc, in, noise, costs, recs, rec_stride, threads, s, next, grp);
     } else {
         launch_rollout_thread(mc, in, noise, costs, recs, rec_stride, threads, s, next, grp);
     }
@@ -1533,7 +1519,7 @@ void launch_rollout(const ModelConst& mc, const StepInput* in, const float* nois
     // No KS kernel for this launch: copy the input up instead.  Not reached from the library (the context
     // decides KS once, at create, with this same shape test, and passes no input to the gait-adaptive or
     // cost-term kernels); a blocking copy, since `ksi` is the caller's stack object.
-    if (grp.ksi && (mc.ga || mc.cost_on || !ks_shape_ok(mc, mode))) {
+    if (grp.ksi && (mc.ga || mc.cost_on || !ks_ok(mc, mode))) {
         (void)hipStreamSynchronize(s);
         (void)hipMemcpy(const_cast<StepInput*>(in), grp.ksi, sizeof(StepInputK), hipMemcpyHostToDevice);
         grp.ksi = nullptr;
@@ -1567,11 +1553,10 @@ void launch_rollout(const ModelConst& mc, const StepInput* in, const float* nois
 }
 
 int group_size(int nblocks, int rec_stride, int method) {
-    const int knob = tune_knob("SRBD_GROUP_SIZE", 0);  // read per context (tests vary it)
     // measured (round 3, r3e): the group hand-off adds ~2-3 us to the rollout launch and saves 1.7 us of merge
     // at C2 (157 blocks), 4.8 at N = 65 536 (1024 blocks), 6 at C5 (2048); CEM's group top-K adds ~8 us at C3
     const bool use = method != SRBD_CEM_MPPI && nblocks >= GROUP_MIN_BLOCKS;
-    int g = knob > 0 ? knob : (use ? (nblocks + GROUP_TARGET - 1) / GROUP_TARGET : 1);
+    int g = use ? (nblocks + GROUP_TARGET - 1) / GROUP_TARGET : 1;
     const int cap = GROUP_LDS_FLOATS / rec_stride;  // the last arriver's LDS copy of its group's records
     g = g > cap ? cap : g;
     g = g > GROUP_MAX ? GROUP_MAX : g;
@@ -1602,10 +1587,9 @@ size_t merge_smem_bytes(int nrec, int P, int K) {
 }
 
 int merge_split_cols(const ModelConst& mc) {
-    static const int knob = tune_knob("SRBD_MERGE_SPLIT_COLS", MERGE_SPLIT_COLS);
-    if (knob >= mc.P) return 0;  // 0: one block (SRBD_MERGE_SPLIT_COLS >= P disables the split)
+    if (MERGE_SPLIT_COLS >= mc.P) return 0;  // 0: one block
     const int lo = (mc.P + MERGE_MAX_BLOCKS - 2) / (MERGE_MAX_BLOCKS - 1);  // at most MERGE_MAX_BLOCKS flags
-    return knob > lo ? knob : lo;
+    return MERGE_SPLIT_COLS > lo ? MERGE_SPLIT_COLS : lo;
 }
 
 int merge_blocks(const ModelConst& mc) {
@@ -1614,16 +1598,15 @@ int merge_blocks(const ModelConst& mc) {
 }
 
 // LDS staging of the records (merge_body<true>): when the block's records fit beside the merge's own
-// dynamic LDS.  SRBD_MERGE_STAGE=2 turns it off (measurement), SRBD_MERGE_FENCE=2 drops the system
-// fence before the publish flag (outputs are system-scope stores; 1 keeps it).
+// dynamic LDS.  The publish flag follows the system-scope output stores without a system fence (the
+// stores are write-through to the host; every wave waits vmcnt(0) first, merge_body).
 constexpr size_t MERGE_LDS_DYN_MAX = 140 * 1024;  // + the staged merge's static LDS (block_topk_rank) <= 160 KB
 // the exchange kernel's static LDS holds both passes' merge_body arrays: its dynamic limit is this much lower
 constexpr size_t XCHG_LDS_STATIC = 24 * 1024;
 static bool merge_stage_fits(int nrec_block, int rec_stride, int P, int K, size_t* smem) {
-    static const int knob = tune_knob("SRBD_MERGE_STAGE", 1);
     const size_t base = merge_smem_bytes(nrec_block, P, K);
     const size_t st = sizeof(float) * (size_t)nrec_block * rec_stride;
-    if (knob == 1 && (rec_stride & 3) == 0 && base + st <= MERGE_LDS_DYN_MAX &&
+    if ((rec_stride & 3) == 0 && base + st <= MERGE_LDS_DYN_MAX &&
         nrec_block <= MERGE_RPT * MERGE_STAGE_THREADS) {
         *smem = base + st;
         return true;
@@ -1639,10 +1622,7 @@ void merge_prepare() {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&merge_xchg_kernel<MERGE_STAGE_THREADS, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)(MERGE_LDS_DYN_MAX - XCHG_LDS_STATIC));
 }
-int merge_fence_sys() {
-    static const int knob = tune_knob("SRBD_MERGE_FENCE", 2);
-    return knob == 1 ? 1 : 0;
-}
+int merge_fence_sys() { return 0; }
 static void launch_merge_kernel(bool stage, dim3 grid, size_t smem, hipStream_t s, const ModelConst& mc,
                                 StepInput* in, const float* recs, int nrec, int rec_stride, int rows_in_rec,
                                 const float* noise, float* rank_out, StepOutput* out, int chain, int ctr_inc,
@@ -1735,16 +1715,10 @@ void launch_merge_xchg(const ModelConst& mc, StepInput* in, const float* recs, i
                            recs, nrec, rec_stride, noise, x, out, chain, chain ? ctr_inc : 0, pub.flag, pub.seq);
 }
 
-int tune_knob(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return (e && atoi(e) > 0) ? atoi(e) : dflt;
-}
 
 int merge_partials(int nrec, bool to_outputs) {
-    static const int direct_max = tune_knob("SRBD_MERGE_DIRECT_MAX", MERGE_DIRECT_MAX);
-    static const int per_block = tune_knob("SRBD_MERGE_PER_BLOCK", MERGE_PER_BLOCK);
-    if (nrec <= (to_outputs ? direct_max : MERGE_DIRECT_MAX_RECORD)) return 0;
-    int m = (nrec + per_block - 1) / per_block;
+    if (nrec <= (to_outputs ? MERGE_DIRECT_MAX : MERGE_DIRECT_MAX_RECORD)) return 0;
+    int m = (nrec + MERGE_PER_BLOCK - 1) / MERGE_PER_BLOCK;
     return m > MERGE_MAX_PARTIALS ? MERGE_MAX_PARTIALS : m;
 }
 

@@ -59,13 +59,11 @@ int merge_fence_sys();
 // CEM, or fewer than GROUP_MIN_BLOCKS blocks); SRBD_GROUP_SIZE overrides (1 disables grouping)
 int group_size(int nblocks, int rec_stride, int method);
 
-// rollout variants: one thread per sample (block = `threads` samples), four lanes per sample (block = 256
-// threads = 64 samples) or two lanes per sample (block = 256 threads = 128 samples)
-enum { ROLLOUT_THREAD = 0, ROLLOUT_QUAD = 1, ROLLOUT_PAIR = 2 };
+// rollout forms: one thread per sample (block = `threads` samples) or four lanes per sample (block = 256
+// threads = 64 samples)
+enum { ROLLOUT_THREAD = 0, ROLLOUT_QUAD = 1 };
 // samples per rollout block of a mode's `threads`
-inline int rollout_spb(int mode, int threads) {
-    return mode == ROLLOUT_QUAD ? threads / 4 : (mode == ROLLOUT_PAIR ? threads / 2 : threads);
-}
+inline int rollout_spb(int mode, int threads) { return mode == ROLLOUT_QUAD ? threads / 4 : threads; }
 bool rollout_specialised(int kind, int H, int S);
 // next != NULL: extra blocks of the same launch generate the next step's draws (RngJob) beside the
 // rollout, on the CUs it leaves idle.
@@ -75,8 +73,6 @@ void launch_rollout(const ModelConst& mc, const StepInput* in, const float* nois
 // the thread-per-sample forms (srbd_rollout_thread.hip): plain and gait-adaptive
 void launch_rollout_thread(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
                            int rec_stride, int threads, hipStream_t s, const RngJob* next, const GroupArgs& grp);
-void launch_rollout_pair(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
-                         int rec_stride, int threads, hipStream_t s, const RngJob* next, const GroupArgs& grp);
 void launch_rollout_ga_thread(const ModelConst& mc, const StepInput* in, const float* noise, float* costs,
                               float* recs, int rec_stride, int spb, hipStream_t s, const RngJob* next,
                               const GroupArgs& grp);
@@ -140,8 +136,6 @@ void launch_xchg_probe(const XchgArgs& x, int* ok, hipStream_t s);
 void launch_merge_xchg(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                        const float* noise, const XchgArgs& x, StepOutput* out, int chain, hipStream_t s, int ctr_inc,
                        Publish pub);
-// Integer tuning knob from the environment (read once), else `dflt`.
-int tune_knob(const char* name, int dflt);
 int launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                        const float* noise, float* partials, float* rank_out, StepOutput* out, int chain,
                        hipStream_t s, int ctr_inc = 1, Publish pub = {nullptr, 0, nullptr});

@@ -4,22 +4,17 @@
 // operand pairs cost a v_mov each and whose SGPR-pair operands spilled (C5 rollout: 1 389 v_mov and
 // 256 VGPRs + scratch with it, 97 VGPRs without; the four-lane kernels keep it: fewer instructions).
 // Float results are unchanged by either choice (the v_pk ops round per lane, contraction stays off).
-#ifndef SRBD_KC_LDS
-#define SRBD_KC_LDS 0
-#endif
-#ifndef SRBD_THREAD_WPE  // minimum waves per SIMD the zero-order thread form is compiled for
-#define SRBD_THREAD_WPE 4
-#endif
 #undef SRBD_ROLLOUT_STAMPS  // the timeline probe stamps the four-lane kernel (srbd_kernels.hip) only
 #include "srbd_device.h"
 
 namespace srbd {
 
-// One thread per sample.  Best throughput when samples fill the GPU (>= ~1 wave per SIMD).
+// One thread per sample.  Best throughput when samples fill the GPU (>= ~1 wave per SIMD).  The zero-order form
+// is compiled for at least four waves per SIMD (a fifth measured slower: DESIGN.md section 4).
 // KS: the host step's input by value (the first kernel argument, read in place from the kernarg segment; block
 // 0 writes the device StepInput `in_dev`), as rollout_quad_kernel does.
 template <int KIND, int HT, int ST, bool CEMT, bool EXT, bool KS = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == SRBD_ZERO_ORDER ? SRBD_THREAD_WPE : 1))) rollout_kernel(
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == SRBD_ZERO_ORDER ? 4 : 1))) rollout_kernel(
                                                       const std::conditional_t<KS, StepInputK, KsNone> ksi,
                                                       const ModelConst mc, const StepInput* __restrict__ in_dev,
                                                       const float* __restrict__ noise, float* __restrict__ costs,
@@ -60,29 +55,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
     const size_t ldn = (size_t)mc.ldn;
     const bool zs = CEMT && zs_scaled(mc, in);  // CEMT: CEM kernels only carry the scaling code
 
-    // the horizon's uniform constants in LDS (KC_* layout): broadcast LDS reads in each step instead of
-    // ~60 SGPRs held across the unrolled horizon (which spilled to VGPR lanes)
-    __shared__ float kc_sh[KC_N + MAXH];  // + dts (rolled horizon)
-    if (tid == 0) {
-        kc_sh[KC_INVM] = mc.inv_m;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            kc_sh[KC_I + i] = mc.inertia[i];
-            kc_sh[KC_IINV + i] = mc.Iinv[i];
-        }
-        kc_sh[KC_LIM] = mc.grf_min;
-        kc_sh[KC_LIM + 1] = mc.grf_max;
-        kc_sh[KC_LIM + 2] = mc.mu;
-        kc_sh[KC_LIM + 3] = mc.neg_mu;
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-            kc_sh[KC_Q + i] = mc.Q[i];
-            kc_sh[KC_REF + i] = in->ref[i];
-            kc_sh[KC_FEET + i] = in->state[12 + i];
-        }
-        for (int i = 0; i < MAXH; ++i) kc_sh[KC_N + i] = mc.dts[i];
-    }
-    __syncthreads();
     float x[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) x[i] = in->state[i];
@@ -96,10 +68,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
     // 2 waves per SIMD and ~300 v_readlane per step at C5.)  P * ldn * 4 < 2^31: P <= 192 here and
     // n_local <= 8192 blocks x 256.
     constexpr bool ZR = CT && KIND == SRBD_ZERO_ORDER && !EXT;
-    #ifndef SRBD_ZD
-#define SRBD_ZD 2
-#endif
-    constexpr int ZD = SRBD_ZD, ZRS = ZD + 1;
+    constexpr int ZD = 2, ZRS = ZD + 1;
     float zr[ZR ? ZRS : 1][12];
     const auto nrs = __builtin_amdgcn_make_buffer_rsrc((void*)noise, (short)0, ZR ? mc.P * mc.ldn * 4 : 0, 0x00020000);
     const int voff = k * 4;
@@ -128,9 +97,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
         const float c[4] = {is->contact[0][n], is->contact[1][n], is->contact[2][n], is->contact[3][n]};
         const float fref = is->fzref[n];
         const float dt = mc.dts[n];
-        const float* kc = kc_sh;
-        const LdsConst K{kc};
-        (void)K;
         const int idx = CT && KIND != SRBD_ZERO_ORDER ? chunk_index(n, HT, ST) : mc.sidx[n];
         float F[12], RX[4], RY[4];
 #pragma unroll
@@ -153,100 +119,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
                        fy, fz);
             RX[leg] = fx;
             RY[leg] = fy;
-            #if SRBD_KC_LDS
-            shape_leg_k(K, fref, c[leg], fx, fy, fz);
-#else
             shape_leg(mc, fref, c[leg], fx, fy, fz);
-#endif
             F[3 * leg] = fx;
             F[3 * leg + 1] = fy;
             F[3 * leg + 2] = fz;
         }
         dep = F[11];  // the next step's loads issue from here on (step_ptr)
-        #if SRBD_KC_LDS
-        integrate_k(K, x, kc + KC_FEET, F, c, dt);
-#else
         integrate(mc, x, in->state + 12, F, c, dt);
-#endif
         // tracking cost (NMPC:451) per component: cost_c += ((t_p + t_v) + t_rpy) + t_omega
         float t[12];
 #pragma unroll
         for (int i = 0; i < 12; ++i) {
-#if SRBD_KC_LDS
-            const float e = x[i] - kc[KC_REF + i];
-            t[i] = (e * kc[KC_Q + i]) * e;
-#else
             const float e = x[i] - in->ref[i];
             t[i] = (e * mc.Q[i]) * e;
-#endif
         }
 #pragma unroll
         for (int q = 0; q < 3; ++q) cost3[q] = cost3[q] + (((t[q] + t[3 + q]) + t[6 + q]) + t[9 + q]);
         if constexpr (decltype(EX)::value) extra_cost_step(mc, n, F, RX, RY, c, fref, Fprev, cost3);
     };
-#ifndef SRBD_THREAD_ROLL
-#define SRBD_THREAD_ROLL 0
-#endif
-    // rolled horizon (experiment): one step's code, next step's noise double-buffered in registers
-    auto horizon_rolled = [&]() __attribute__((always_inline)) {
-        float cur[12], nxt[12];
-        const int ldn4 = mc.ldn * 4;
-#pragma unroll
-        for (int l = 0; l < 4; ++l)
-#pragma unroll
-            for (int q = 0; q < 3; ++q)
-                cur[3 * l + q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(nrs, voff, (l * PL + q * HT) * ldn4, 0));
-#pragma unroll 1
-        for (int n = 0; n < HT; ++n) {
-            if (n + 1 < HT) {
-#pragma unroll
-                for (int l = 0; l < 4; ++l)
-#pragma unroll
-                    for (int q = 0; q < 3; ++q)
-                        nxt[3 * l + q] = __uint_as_float(
-                            __builtin_amdgcn_raw_buffer_load_b32(nrs, voff, (l * PL + q * HT + n + 1) * ldn4, 0));
-            }
-            const float c[4] = {in->contact[0][n], in->contact[1][n], in->contact[2][n], in->contact[3][n]};
-            const float fref = in->fzref[n];
-            const float dt = kc_sh[KC_N + n];
-            float F[12];
-#pragma unroll
-            for (int leg = 0; leg < 4; ++leg) {
-                const int base = leg * PL;
-                float f3[3];
-#pragma unroll
-                for (int q = 0; q < 3; ++q) {
-                    const float z = cur[3 * leg + q];
-                    const int j = base + q * HT + n;
-                    if constexpr (CEMT) {
-                        const float sj = in->sigma[j];
-                        f3[q] = in->best[j] + z * (zs ? sj : 1.0f);
-                    } else {
-                        f3[q] = in->best[j] + z;
-                    }
-                }
-                shape_leg(mc, fref, c[leg], f3[0], f3[1], f3[2]);
-                F[3 * leg] = f3[0];
-                F[3 * leg + 1] = f3[1];
-                F[3 * leg + 2] = f3[2];
-            }
-            integrate(mc, x, in->state + 12, F, c, dt);
-            float t[12];
-#pragma unroll
-            for (int i = 0; i < 12; ++i) {
-                const float e = x[i] - in->ref[i];
-                t[i] = (e * mc.Q[i]) * e;
-            }
-#pragma unroll
-            for (int q = 0; q < 3; ++q) cost3[q] = cost3[q] + (((t[q] + t[3 + q]) + t[6 + q]) + t[9 + q]);
-#pragma unroll
-            for (int i = 0; i < 12; ++i) cur[i] = nxt[i];
-        }
-    };
     auto horizon = [&](auto EX) __attribute__((always_inline)) {
-        if constexpr (ZR && SRBD_THREAD_ROLL) {
-            horizon_rolled();
-        } else if constexpr (CT) {
+        if constexpr (CT) {
             unroll_seq([&](auto nc) { step(decltype(nc)::value, EX); },
                        std::make_integer_sequence<int, (CT ? HT : 1)>{});
         } else {
@@ -264,154 +156,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
     return;
 #endif
     block_epilogue<CEMT>(mc, in, T, tid, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh, 0.0f, grp, nroll);
-}
-
-// Two lanes per sample (adjacent lanes 2s, 2s + 1; h = lane & 1), compile-time shapes, no cost terms.
-// Lane h decodes, shapes and clips legs 2h and 2h + 1 and forms their contact-weighted force and torque
-// pair sums; one DPP swap-add gives both lanes (leg0 + leg1) + (leg2 + leg3), the order integrate() uses
-// (IEEE addition commutes, so both lanes hold the same bits); the rigid-body step and the tracking cost then
-// run on both lanes as rollout_kernel runs them (integrate_rb_k), so costs equal the thread form's bit for
-// bit.  Why two lanes: measured issue costs on MI355X (scripts/valu_probe.hip) put a DPP move
-// at ~4.3 cycles per wave instruction against ~2.5 for a VGPR-only f32 op, and the four-lane layout spends
-// ~34 DPP moves per step to run the rigid body component-parallel (~46 SIMD cycles per sample-step); this
-// layout issues 6 per step at ~22 cycles per sample-step, and still gives N = 65 536 two waves per SIMD
-// where the thread form has one.
-template <int KIND, int HT, int ST, bool CEMT>
-__global__ void __launch_bounds__(256) rollout_pair_kernel(const ModelConst mc, const StepInput* __restrict__ in,
-                                                           const float* __restrict__ noise, float* __restrict__ costs,
-                                                           float* __restrict__ recs, int rec_stride,
-                                                           const RngJob next_rng, int nroll, const GroupArgs grp) {
-    if (grp.gate && (*grp.gate & ARM_CANCEL)) return;  // armed chain that did not fire: nothing to compute
-    if ((int)blockIdx.x >= nroll) {  // the next step's draws on the CUs the rollout leaves idle
-        rng_items(mc, in, next_rng, ((int)blockIdx.x - nroll) * (int)blockDim.x + (int)threadIdx.x,
-                  ((int)gridDim.x - nroll) * (int)blockDim.x);
-        return;
-    }
-    __shared__ float e_sh[128];
-    __shared__ uint64_t red[4];
-    __shared__ uint64_t elite_sh[MAXK];
-    static_assert(HT > 0 && (KIND == SRBD_ZERO_ORDER || ST > 0), "compile-time shapes only");
-    constexpr int H = HT, S = ST;
-    constexpr int PL = KIND == SRBD_ZERO_ORDER ? 3 * HT : (KIND == SRBD_LINEAR_SPLINE ? 3 * (ST + 1) : 12 * ST);
-    const int tid = threadIdx.x, h = tid & 1, sib = tid >> 1;
-    const int SPB = (int)blockDim.x >> 1;
-    const int k = blockIdx.x * SPB + sib;
-    const bool valid = k < mc.n_local;
-    const bool zs = CEMT && zs_scaled(mc, in);
-    // this lane's two legs 2h, 2h + 1: parameter block lb = 2h PL; leg i of the pair at lb + i PL
-    const int lb = 2 * h * PL;
-    const uint32_t m0 = h ? 0u : ~0u, m1 = ~m0;  // lane masks: contact of the lane's leg i = c[i] or c[2 + i]
-    float x[12], foot[2][3];
-#pragma unroll
-    for (int i = 0; i < 12; ++i) x[i] = in->state[i];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int q = 0; q < 3; ++q) foot[i][q] = in->state[12 + 3 * (2 * h + i) + q];
-    float cost3[3] = {0.0f, 0.0f, 0.0f};
-    // noise through a buffer descriptor: the lane's leg block + sample in voffset, the uniform row in soffset
-    // (the launcher keeps P ldn 4 < 2^31)
-    const auto nrs = __builtin_amdgcn_make_buffer_rsrc((void*)noise, (short)0, mc.P * mc.ldn * 4, 0x00020000);
-    const int voff = (lb * mc.ldn + k) * 4;
-    const float* __restrict__ bl = in->best + lb;
-    const float* __restrict__ sl = in->sigma + lb;
-    auto param = [&](float z, int j) __attribute__((always_inline)) {  // the decoded value of parameter j (leg-local)
-        if constexpr (CEMT) return bl[j] + z * (zs ? sl[j] : 1.0f);
-        return bl[j] + z;
-    };
-    // Zero-order: step m's 6 noise values (and best) are loaded at step m - ZD into a ring of ZD + 1 slots;
-    // splines: every parameter the horizon reads (LIN 3 (S + 1), cubic 10 (S - 1) + 12 per leg) up front.
-#ifndef SRBD_PAIR_ZD
-#define SRBD_PAIR_ZD 2
-#endif
-    constexpr bool ZO = KIND == SRBD_ZERO_ORDER;
-    constexpr int ZD = SRBD_PAIR_ZD, ZRS = ZD + 1;
-    constexpr int NU = ZO ? 1 : (KIND == SRBD_LINEAR_SPLINE ? 3 * (ST + 1) : 10 * (ST - 1) + 12);
-    float zr[ZO ? ZRS : 1][2][3];
-    float br[ZO ? ZRS : 1][2][3];
-    float pre[2][NU];
-    float dep = x[0];
-    auto zload = [&](const int m) __attribute__((always_inline)) {
-        const int ldn4 = step_int(mc.ldn * 4, dep);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const int j = i * PL + q * HT + m;
-                zr[m % ZRS][i][q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(nrs, voff, j * ldn4, 0));
-                br[m % ZRS][i][q] = CEMT ? 0.0f : bl[j];
-            }
-    };
-    if constexpr (ZO) {
-#pragma unroll
-        for (int m = 0; m < ZD && m < HT; ++m) zload(m);
-    } else {
-#pragma unroll
-        for (int u = 0; u < NU; ++u)
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const float z =
-                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(nrs, voff, (i * PL + u) * mc.ldn * 4, 0));
-                pre[i][u] = param(z, i * PL + u);
-            }
-    }
-    auto step = [&](const int n) __attribute__((always_inline)) {
-        const auto is = step_ptr(in, dep);
-        if constexpr (ZO)
-            if (n + ZD < HT) zload(n + ZD);  // n: a compile-time constant (unrolled)
-        const float c[4] = {is->contact[0][n], is->contact[1][n], is->contact[2][n], is->contact[3][n]};
-        const float cm[2] = {__uint_as_float((__float_as_uint(c[0]) & m0) | (__float_as_uint(c[2]) & m1)),
-                             __uint_as_float((__float_as_uint(c[1]) & m0) | (__float_as_uint(c[3]) & m1))};
-        const float fref = is->fzref[n];
-        const float dt = mc.dts[n];
-        const int idx = ZO ? 0 : chunk_index(n, HT, ST);  // n is a compile-time constant here
-        float Fc[2][3], tc[2][3];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            auto acc = [&](int j) {  // j: parameter of this leg (compile-time)
-                if constexpr (ZO) {
-                    const int q = (j - n) / HT;
-                    const float z = zr[n % ZRS][i][q];
-                    if constexpr (CEMT) return param(z, i * PL + j);
-                    return br[n % ZRS][i][q] + z;
-                } else {
-                    return pre[i][j];
-                }
-            };
-            float f[3];
-            decode_leg(KIND, H, S, idx, mc.sq[n], mc.somq[n], mc.sa[n], mc.sb[n], mc.sc[n], mc.sd[n], n, acc, f[0], f[1],
-                       f[2]);
-            shape_leg(mc, fref, cm[i], f[0], f[1], f[2]);
-#pragma unroll
-            for (int q = 0; q < 3; ++q) Fc[i][q] = f[q] * cm[i];
-            leg_torque(foot[i], x, f, cm[i], tc[i]);
-        }
-        // pair sums, then (leg0 + leg1) + (leg2 + leg3) on both lanes: one swap-add per component
-        float temp[3], temp2[3];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            const float a = Fc[0][q] + Fc[1][q], b = tc[0][q] + tc[1][q];
-            temp[q] = a + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a), 0xB1, 0xF, 0xF, true));
-            temp2[q] = b + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(b), 0xB1, 0xF, 0xF, true));
-        }
-        dep = temp2[2];  // the next step's loads issue from here on (step_ptr)
-        integrate_rb_k(McConst{mc}, x, temp, temp2, dt);
-        float t[12];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-            const float e = x[i] - in->ref[i];
-            t[i] = (e * mc.Q[i]) * e;
-        }
-#pragma unroll
-        for (int q = 0; q < 3; ++q) cost3[q] = cost3[q] + (((t[q] + t[3 + q]) + t[6 + q]) + t[9 + q]);
-    };
-    unroll_seq([&](auto nc) { step(decltype(nc)::value); }, std::make_integer_sequence<int, HT>{});
-    float cost = (cost3[0] + cost3[1]) + cost3[2];
-    cost = cost + in->cost_feet;  // 0, or NaN when a foot term is non-finite (Q_feet = 0)
-    if (isnan(cost) || isinf(cost)) cost = 1000000.0f;  // NMPC:686-687
-    if (valid && h == 0 && costs) costs[k] = cost;
-    block_epilogue<CEMT>(mc, in, SPB, h == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh, 0.0f,
-                         grp, nroll);
 }
 
 template <int KIND>
@@ -564,45 +308,6 @@ void launch_rollout_thread(const ModelConst& mc, const StepInput* in, const floa
             SRBD_LT(SRBD_CUBIC_SPLINE, 0, 0);
     }
 #undef SRBD_LT
-}
-
-// Two lanes per sample (rollout_pair_kernel): `threads` = 2 x samples per block (256).  Shapes without a
-// compile-time form and the opt-in cost terms run the thread form with the same samples per block.
-template <int KIND, int HT, int ST>
-static void launch_pair_t(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
-                          int rec_stride, int threads, hipStream_t s, const RngJob* next, const GroupArgs& grp) {
-    const RngJob job = next ? *next : RngJob{nullptr, 0, 0, 0, 0};
-    const int extra = next ? (rng_grid(mc) < 1024 ? rng_grid(mc) : 1024) : 0;
-    const int spb = threads / 2;
-    const int blocks = (mc.n_local + spb - 1) / spb;
-    const dim3 grid(blocks + extra * 256 / threads);
-    if (mc.method == SRBD_CEM_MPPI)
-        hipLaunchKernelGGL((rollout_pair_kernel<KIND, HT, ST, true>), grid, dim3(threads), 0, s, mc, in, noise, costs,
-                           recs, rec_stride, job, blocks, grp);
-    else
-        hipLaunchKernelGGL((rollout_pair_kernel<KIND, HT, ST, false>), grid, dim3(threads), 0, s, mc, in, noise, costs,
-                           recs, rec_stride, job, blocks, grp);
-}
-
-void launch_rollout_pair(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,
-                         int rec_stride, int threads, hipStream_t s, const RngJob* next, const GroupArgs& grp) {
-    const int H = mc.H, S = mc.S;
-    if (!mc.cost_on) switch (mc.kind) {
-            case SRBD_ZERO_ORDER:
-                if (H == 10) return launch_pair_t<SRBD_ZERO_ORDER, 10, 0>(mc, in, noise, costs, recs, rec_stride, threads, s, next, grp);
-                if (H == 12) return launch_pair_t<SRBD_ZERO_ORDER, 12, 0>(mc, in, noise, costs, recs, rec_stride, threads, s, next, grp);
-                if (H == 16) return launch_pair_t<SRBD_ZERO_ORDER, 16, 0>(mc, in, noise, costs, recs, rec_stride, threads, s, next, grp);
-                break;
-            case SRBD_LINEAR_SPLINE:
-                if (S == 2 && H == 12) return launch_pair_t<SRBD_LINEAR_SPLINE, 12, 2>(mc, in, noise, costs, recs, rec_stride, threads, s, next, grp);
-                if (S == 2 && H == 16) return launch_pair_t<SRBD_LINEAR_SPLINE, 16, 2>(mc, in, noise, costs, recs, rec_stride, threads, s, next, grp);
-                break;
-            default:
-                if (S == 2 && H == 12) return launch_pair_t<SRBD_CUBIC_SPLINE, 12, 2>(mc, in, noise, costs, recs, rec_stride, threads, s, next, grp);
-                if (S == 2 && H == 16) return launch_pair_t<SRBD_CUBIC_SPLINE, 16, 2>(mc, in, noise, costs, recs, rec_stride, threads, s, next, grp);
-                break;
-        }
-    launch_rollout_thread(mc, in, noise, costs, recs, rec_stride, threads / 2, s, next, grp);
 }
 
 void launch_rollout_ga_thread(const ModelConst& mc, const StepInput* in, const float* noise, float* costs,

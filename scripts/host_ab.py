@@ -2,8 +2,9 @@
 """Host-to-host srbd_step times (C-timed, srbd_bench_host_steps) of one workload under environment settings.
 
 Usage: host_ab.py WORKLOAD[:N] STEPS NAME=ENV=VAL[,ENV=VAL] ...   (GPU box; one JSON line per setting)
-Settings are applied when each context is created (knobs read per context, e.g. SRBD_FINAL_MERGE,
-SRBD_GROUP_SIZE), alternating A/B/A/B over three rounds so drift between them cancels.
+Settings are applied when each context is created (the per-context knob SRBD_ROLLOUT=thread|quad), alternating
+A/B/A/B over three rounds so drift between them cancels.  Library variants built with other compile-time code
+(scripts/build_variants.sh) are compared with scripts/vrun.sh instead.
 """
 import json
 import os

@@ -309,14 +309,8 @@ def test_rollout_variants_bitwise_identical(lib, monkeypatch, wkey, method, par,
     """The four-lanes-per-sample kernel performs the thread kernel's float ops in the same order."""
     case = make_case(wkey, N=3000, method=method, par=par, H=H, seed=11)
     out = {}
-    for mode in ("thread", "quad", "pair"):
+    for mode in ("thread", "quad"):
         monkeypatch.setenv("SRBD_ROLLOUT", mode)
         out[mode] = run_gpu(lib, case, noise=False, seed=9, counter=4)
     for k in ("costs", "best", "grf", "pred"):
         np.testing.assert_array_equal(out["thread"][k], out["quad"][k])
-    # two lanes per sample: the same costs bit for bit; its blocks hold 128 samples (64 in the other two
-    # forms at this N), so the weighted sums are summed in another order: the update within float rounding
-    np.testing.assert_array_equal(out["thread"]["costs"], out["pair"]["costs"])
-    assert out["thread"]["best_index"] == out["pair"]["best_index"]
-    for k in ("best", "grf", "pred"):
-        np.testing.assert_allclose(out["pair"][k], out["thread"][k], rtol=1e-5, atol=1e-5)
