@@ -205,12 +205,14 @@ def test_end_to_end_c2_interface_on_jax_stream(lib, part):
 
     case = make_case("c2", N=10000, method="mppi", seed=10)
     o = case["orc"]
-    saved = dict(mirror.mpc_params)
+    saved, robot = dict(mirror.mpc_params), mirror.robot
+    mirror.set_robot(case["w"].robot)  # the case's robot (mass / inertia / grf_max), Go2
     mirror.mpc_params.update(num_parallel_computations=10000, sampling_method="mppi",
                              control_parametrization="zero_order", horizon=12, jax_threefry_partitionable=part)
     try:
         mpc = Sampling_MPC(mirror)
     finally:
+        mirror.set_robot(robot)
         mirror.mpc_params.clear()
         mirror.mpc_params.update(saved)
     try:
