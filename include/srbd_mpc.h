@@ -61,7 +61,7 @@ typedef struct srbd_config {
     int32_t num_splines;     /* S (linear / cubic) */
     int32_t num_elite;       /* CEM elite count; reference: 10 (centroidal_nmpc_jax.py:1075) */
     int32_t device_id;       /* HIP ordinal */
-    int32_t rank;            /* shard index: rows [rank*N/world, (rank+1)*N/world) */
+    int32_t rank;            /* shard index: rows srbd_shard_rows(num_samples, rank, world_size) */
     int32_t world_size;      /* 1 for single GPU */
     int32_t use_graph;       /* 1: replay srbd_step as one hipGraph */
     float mass;              /* config.mass */
@@ -188,14 +188,23 @@ enum { SRBD_RNG_PHILOX = 0, SRBD_RNG_JAX = 1, SRBD_RNG_JAX_LEGACY = 2 };
 int srbd_set_rng(srbd_ctx* ctx, int32_t kind);
 int srbd_get_rng(const srbd_ctx* ctx);
 
-/* Sharded form.  Record size in floats (identical on every rank). */
+/* Sharded form.  The rows of a rank are whole nodes of one level of the fixed reduction tree every merge
+ * folds (64-row leaves, 32 children per node; the exchange level is the highest one that gives every rank a
+ * node), so the merged result is the same bits for every world_size.  A rank's record ("rank buffer") holds
+ * its nodes of that level, ceil(nodes / world_size) record slots; gathered in rank order the buffers are the
+ * level's node list.  Size in floats (identical on every rank). */
 int srbd_record_floats(const srbd_ctx* ctx);
+/* Host-only: srbd_record_floats of a context of this configuration (rank / world_size as given). */
+int srbd_record_floats_host(const srbd_config* cfg);
+/* Host-only: the first global row and row count of `rank` of `world` ranks over num_samples rows
+ * (SRBD_E_INVALID when some rank would get no node). */
+int srbd_shard_rows(int64_t num_samples, int32_t rank, int32_t world, int64_t* row0, int64_t* rows);
 /* Rows of this rank only; writes this rank's partial record to d_record (device pointer).
  * noise_local: NULL or (rows of this shard) x P row-major.  Asynchronous on the context stream. */
 int srbd_step_local(srbd_ctx* ctx, const float* state, const float* ref, const float* contact, int32_t contact_stride,
                     const float* best_params, const float* sigma, const float* noise_local, uint64_t seed,
                     uint64_t counter, void* d_record);
-/* Merge num_records gathered records (device pointer, rank order) and finish the step. */
+/* Merge the gathered rank buffers (device pointer, rank order; num_records == world_size) and finish the step. */
 int srbd_step_finish(srbd_ctx* ctx, const void* d_records, int32_t num_records, float* best_params, float* sigma,
                      srbd_result* out, float* out_costs_local);
 /* Host-only merge of rank records (same math; no device needed). */

@@ -55,7 +55,10 @@ constexpr int MAX_RECORDS = 8192;  // merge_kernel holds 8 record minima per thr
 struct srbd_ctx {
     srbd_config cfg;
     ModelConst mc;
-    int mode = 0, threads = 64, nblocks = 0, wrec_stride = 0, rrec_stride = 0;
+    // rollout blocks, leaf records per block (the reduction tree's leaves, srbd_core.h) and this rank's leaves;
+    // wrec_stride: floats per leaf / level-1 record; rrec_stride: floats of one rank buffer (its exchange-level
+    // node records, t_xmax of them)
+    int mode = 0, threads = 64, nblocks = 0, lpb = 1, nleaf = 0, wrec_stride = 0, rrec_stride = 0;
     hipStream_t stream = nullptr;
     bool own_stream = true;
     StepInput* d_in = nullptr;
@@ -100,8 +103,8 @@ struct srbd_ctx {
     size_t noise_rm_cap = 0;
     float* d_costs = nullptr;
     float* d_wrec = nullptr;
-    // in-launch group reduction of the block records (GroupArgs): gsize blocks per group, ngroups
-    // group records the merge reads; gsize 1: the merge reads the nblocks block records
+    // in-launch level-1 fold of the leaf records (GroupArgs): gsize = TREE_FAN leaves per node, ngroups
+    // level-1 records the merge reads; gsize 1: the merge reads the nleaf leaf records
     int gsize = 1, ngroups = 0;
     float* d_grec = nullptr;
     uint32_t* d_gcnt = nullptr;
@@ -110,7 +113,6 @@ struct srbd_ctx {
     uint32_t* d_gdone = nullptr;
     // host steps pass the step input to the rollout as a kernel argument (ks_ok): no upload kernel
     bool ks = false;
-    float* d_part = nullptr;  // first-level merge partials (rank-record format)
     hipGraphExec_t g_dev2 = nullptr, g_dev1 = nullptr;
     float* d_ga_freq = nullptr;  // injected per-row step frequencies (gait-adaptive parity mode), ldn floats
     bool input_ready = false;
@@ -246,6 +248,11 @@ static int build_model(const srbd_config* cfg, ModelConst* mc, std::string* why)
         *why = "bad rank/world_size";
         return SRBD_E_INVALID;
     }
+    const TreeShape ts = tree_shape(cfg->num_samples, world, cfg->rank);
+    if (!ts.ok) {
+        *why = "too few rows for world_size ranks: every rank needs at least one 64-row leaf";
+        return SRBD_E_INVALID;
+    }
     if (cfg->parametrization == SRBD_CUBIC_SPLINE && 10 * (cfg->num_splines - 1) + 11 >= params_leg(cfg)) {
         *why = "cubic spline needs num_splines >= 1";
         return SRBD_E_INVALID;
@@ -264,9 +271,18 @@ static int build_model(const srbd_config* cfg, ModelConst* mc, std::string* why)
         return SRBD_E_INVALID;
     }
     mc->N = cfg->num_samples;
-    mc->row0 = (int)((long long)cfg->rank * cfg->num_samples / world);
-    mc->n_local = (int)((long long)(cfg->rank + 1) * cfg->num_samples / world) - mc->row0;
+    // rows of this rank: whole nodes of the reduction tree's exchange level (srbd_core.h tree_shape)
+    mc->row0 = (int)ts.row0;
+    mc->n_local = (int)ts.nrows;
     mc->ldn = (mc->n_local + 255) / 256 * 256;
+    mc->t_leaves = ts.leaves;
+    mc->t_depth = ts.depth;
+    mc->t_xlevel = ts.xlevel;
+    mc->t_xnodes = ts.xnodes;
+    mc->t_xmax = ts.xmax;
+    mc->t_world = world;
+    mc->leaf0 = mc->row0 / LEAF_ROWS;
+    mc->nleaf = (mc->n_local + LEAF_ROWS - 1) / LEAF_ROWS;
     mc->inv_m = 1.0f / cfg->mass;
     mc->mg = cfg->mg;
     if (!(cfg->grf_min >= 0.0f && cfg->grf_max >= cfg->grf_min && cfg->mu >= 0.0f)) {
@@ -361,12 +377,14 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     c->ks = ks_ok(mc, c->mode);  // srbd_step, and the xGMI sharded step (xg_step)
     const int spb = rollout_spb(c->mode, c->threads);  // samples per rollout block
     c->nblocks = (mc.n_local + spb - 1) / spb;
+    c->lpb = spb / LEAF_ROWS;
+    c->nleaf = mc.nleaf;
     if (c->nblocks > MAX_RECORDS) {
         delete c;
         return fail(nullptr, SRBD_E_INVALID, "too many samples per rank");
     }
     c->wrec_stride = rec_floats_wave(mc.P, mc.K);
-    c->rrec_stride = rec_floats_rank(mc.P, mc.K);
+    c->rrec_stride = mc.t_xmax * rec_floats_rank(mc.P, mc.K);
     auto cleanup_fail = [&](const char* what, hipError_t e) {
         std::string m = std::string(what) + ": " + hipGetErrorString(e);
         srbd_destroy(c);
@@ -400,10 +418,11 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
         if ((e = hipMalloc((void**)&c->d_noise[b], noise_bytes)) != hipSuccess) return cleanup_fail("hipMalloc", e);
     if ((e = hipMalloc((void**)&c->d_costs, sizeof(float) * mc.ldn)) != hipSuccess)
         return cleanup_fail("hipMalloc", e);
-    if ((e = hipMalloc((void**)&c->d_wrec, sizeof(float) * (size_t)c->nblocks * c->wrec_stride)) != hipSuccess)
+    // every block writes lpb leaf records (the last block's past nleaf are never read)
+    if ((e = hipMalloc((void**)&c->d_wrec, sizeof(float) * (size_t)c->nblocks * c->lpb * c->wrec_stride)) != hipSuccess)
         return cleanup_fail("hipMalloc", e);
-    c->gsize = group_size(c->nblocks, c->wrec_stride, mc.method);
-    c->ngroups = (c->nblocks + c->gsize - 1) / c->gsize;
+    c->gsize = group_size(mc);
+    c->ngroups = (c->nleaf + TREE_FAN - 1) / TREE_FAN;
     if (c->gsize > 1) {
         if ((e = hipMalloc((void**)&c->d_grec, sizeof(float) * (size_t)c->ngroups * c->wrec_stride)) != hipSuccess)
             return cleanup_fail("hipMalloc", e);
@@ -415,11 +434,6 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
             c->final_merge = false;
         if ((e = hipMemsetAsync(c->d_gcnt, 0, sizeof(uint32_t) * (size_t)c->ngroups, c->stream)) != hipSuccess)
             return cleanup_fail("hipMemset", e);
-    }
-    {
-        const int m = merge_partials(c->nblocks, false);  // the larger of the two partial counts
-        if (m > 0 && (e = hipMalloc((void**)&c->d_part, sizeof(float) * (size_t)m * c->rrec_stride)) != hipSuccess)
-            return cleanup_fail("hipMalloc", e);
     }
     for (int b = 0; b < 2; ++b)
         if ((e = hipMemsetAsync(c->d_noise[b], 0, noise_bytes, c->stream)) != hipSuccess)
@@ -455,7 +469,6 @@ extern "C" void srbd_destroy(srbd_ctx* c) {
     (void)hipFree(c->d_grec);
     (void)hipFree(c->d_gcnt);
     (void)hipFree(c->d_gdone);
-    (void)hipFree(c->d_part);
     (void)hipFree(c->d_ga_freq);
     if (c->h_in) (void)hipHostFree(c->h_in);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -556,7 +569,9 @@ static void fill_ksi(const srbd_ctx* c, StepInputK* k) {
 // The records the merge reads: the group records when the rollout launch reduces its blocks in groups.
 static GroupArgs grp_of(const srbd_ctx* c) { return GroupArgs{c->d_grec, c->d_gcnt, c->gsize}; }
 static const float* merge_src(const srbd_ctx* c) { return c->gsize > 1 ? c->d_grec : c->d_wrec; }
-static int merge_nrec(const srbd_ctx* c) { return c->gsize > 1 ? c->ngroups : c->nblocks; }
+static int merge_nrec(const srbd_ctx* c) { return c->gsize > 1 ? c->ngroups : c->nleaf; }
+// tree levels a rank record folds up from the merge's input records (leaves or level-1 nodes) to the exchange level
+static int levels_up(const srbd_ctx* c) { return c->mc.t_xlevel - (c->gsize > 1 ? 1 : 0); }
 
 // Returns the number of merge blocks that publish (wait_published).
 static int enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput* out, int chain = 0,
@@ -582,8 +597,8 @@ static int enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput
     }
     launch_rollout(mc, c->d_in, c->d_noise[buf], costs ? costs : c->d_costs, c->d_wrec, c->wrec_stride, c->mode,
                    c->threads, c->stream, fuse_next ? &next : nullptr, grp);
-    return launch_merge_tree(mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, c->d_noise[buf], c->d_part,
-                             rank_out, out, chain, c->stream, ctr_inc, pub);
+    return launch_merge(mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, 0, c->d_noise[buf], rank_out, out, chain,
+                        c->stream, nullptr, ctr_inc, pub, rank_out ? levels_up(c) : 0);
 }
 
 // Wait for the merge to publish `seq`.  Polls the stream now and then so a device fault or a launch
@@ -870,10 +885,13 @@ extern "C" int srbd_step_finish(srbd_ctx* c, const void* d_records, int32_t nrec
     if (!c || !d_records || nrec < 1 || !best) return SRBD_E_INVALID;
     arm_cancel(c);
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "srbd_step_finish before srbd_step_local");
+    if (nrec != c->mc.t_world) return fail(c, SRBD_E_INVALID, "srbd_step_finish takes world_size rank records");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     const Publish pub{c->d_flag, ++c->seq};
-    const int nflags = launch_merge(c->mc, c->d_in, (const float*)d_records, nrec, c->rrec_stride, 1, nullptr,
-                                    nullptr, c->d_out_host, 0, c->stream, nullptr, 1, pub);
+    // the gathered rank buffers are the exchange level's node list in order (ceil partition, tree_shape)
+    const int nflags = launch_merge(c->mc, c->d_in, (const float*)d_records, c->mc.t_xnodes,
+                                    rec_floats_rank(c->mc.P, c->mc.K), 1, nullptr, nullptr, c->d_out_host, 0,
+                                    c->stream, nullptr, 1, pub);
     HIP_TRY(c, hipGetLastError());
     int rc = wait_published(c, pub.seq, nflags);
     if (rc) return rc;
@@ -913,9 +931,10 @@ extern "C" int srbd_device_step_finish(srbd_ctx* c, const void* d_records, int32
     if (!c || !d_records || nrec < 1) return SRBD_E_INVALID;
     arm_cancel(c);
     if (!c->input_ready) return fail(c, SRBD_E_STATE, "run srbd_step_local once first");
+    if (nrec != c->mc.t_world) return fail(c, SRBD_E_INVALID, "srbd_device_step_finish takes world_size rank records");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
-    launch_merge(c->mc, c->d_in, (const float*)d_records, nrec, c->rrec_stride, 1, nullptr, nullptr, c->d_out, 1,
-                 c->stream, nullptr, 1);
+    launch_merge(c->mc, c->d_in, (const float*)d_records, c->mc.t_xnodes, rec_floats_rank(c->mc.P, c->mc.K), 1,
+                 nullptr, nullptr, c->d_out, 1, c->stream, nullptr, 1);
     HIP_TRY(c, hipGetLastError());
     return SRBD_OK;
 }
@@ -1066,8 +1085,63 @@ static uint64_t next_seed(const srbd_ctx* c, uint64_t seed) {
 }
 
 // ------------------------------------------------------------------ host merge (no device)
+// The same reduction tree as the device (srbd_core.h): 64-row leaves, TREE_FAN children per node folded in
+// order, node key = the children's minimum, child sums rescaled by expf(-1 * (m_child - m_node)).  The host sums
+// a leaf's rows in row order (the device: wave_sum_f32's DPP order), so host and device agree to rounding; the
+// host merge itself is W-invariant, as the device's is.
+namespace {
+struct HostNode {
+    uint64_t key = ~0ull;
+    float s = 0.0f;
+    std::vector<float> v;
+    std::vector<uint64_t> top;  // the K smallest keys under the node, ascending
+};
+
+HostNode host_fold(const HostNode* ch, int n, int P, int K, bool sums) {
+    HostNode o;
+    for (int c = 0; c < n; ++c) o.key = std::min(o.key, ch[c].key);
+    const float m = u2f((uint32_t)(o.key >> 32));
+    o.v.assign(P, 0.0f);
+    if (sums)
+        for (int c = 0; c < n; ++c) {
+            const float sc = expf(-1.0f * (u2f((uint32_t)(ch[c].key >> 32)) - m));
+            o.s = o.s + sc * ch[c].s;
+            for (int j = 0; j < P; ++j) o.v[j] = o.v[j] + sc * ch[c].v[j];
+        }
+    for (int c = 0; c < n; ++c) o.top.insert(o.top.end(), ch[c].top.begin(), ch[c].top.end());
+    std::sort(o.top.begin(), o.top.end());
+    if ((int)o.top.size() > K) o.top.resize(K);
+    return o;
+}
+
+std::vector<HostNode> host_fold_level(const std::vector<HostNode>& lv, int P, int K, bool sums) {
+    std::vector<HostNode> up;
+    for (size_t g = 0; g < lv.size(); g += TREE_FAN)
+        up.push_back(host_fold(lv.data() + g, (int)std::min<size_t>(TREE_FAN, lv.size() - g), P, K, sums));
+    return up;
+}
+}  // namespace
+
 static uint64_t host_rec_key(const float* R, int P, int q) {
     return ((uint64_t)f2u(R[REC_HDR + P + 2 * q + 1]) << 32) | (uint64_t)f2u(R[REC_HDR + P + 2 * q]);
+}
+
+extern "C" int srbd_shard_rows(int64_t num_samples, int32_t rank, int32_t world, int64_t* row0, int64_t* rows) {
+    if (num_samples < 1 || world < 1 || rank < 0 || rank >= world || !row0 || !rows) return SRBD_E_INVALID;
+    const TreeShape t = tree_shape(num_samples, world, rank);
+    if (!t.ok) return fail(nullptr, SRBD_E_INVALID, "too few rows for world_size ranks");
+    *row0 = t.row0;
+    *rows = t.nrows;
+    return SRBD_OK;
+}
+
+extern "C" int srbd_record_floats_host(const srbd_config* cfg) {
+    if (!cfg) return SRBD_E_INVALID;
+    ModelConst mc;
+    std::string why;
+    const int rc = build_model(cfg, &mc, &why);
+    if (rc) return fail(nullptr, rc, why);
+    return mc.t_xmax * rec_floats_rank(mc.P, mc.K);
 }
 
 extern "C" int srbd_make_record_host(const srbd_config* cfg, int32_t rank, int32_t world, const float* costs,
@@ -1079,44 +1153,57 @@ extern "C" int srbd_make_record_host(const srbd_config* cfg, int32_t rank, int32
     std::string why;
     int rc = build_model(&cc, &mc, &why);
     if (rc) return fail(nullptr, rc, why);
-    const int P = mc.P, K = mc.K, n = mc.n_local;
-    std::vector<uint64_t> keys(n);
-    for (int k = 0; k < n; ++k) keys[k] = cost_key(costs[k], (uint32_t)(mc.row0 + k));
-    std::vector<uint64_t> sorted(keys);
-    std::sort(sorted.begin(), sorted.end());
-    const float m = u2f((uint32_t)(sorted[0] >> 32));
-    memset(rec, 0, sizeof(float) * rec_floats_rank(P, K));
-    rec[0] = m;
-    rec[2] = u2f((uint32_t)sorted[0]);
-    if (mc.method != SRBD_RANDOM_SAMPLING) {
-        float s = 0.0f;
-        std::vector<float> v(P, 0.0f);
-        for (int k = 0; k < n; ++k) {
-            const float e = expf(-1.0f * (costs[k] - m));
-            s = s + e;
-            for (int j = 0; j < P; ++j) v[j] = v[j] + e * noise_rows[(size_t)k * P + j];
+    const int P = mc.P, K = mc.K, n = mc.n_local, rf = rec_floats_rank(P, K);
+    const bool sums = mc.method != SRBD_RANDOM_SAMPLING;
+    std::vector<HostNode> lv;
+    for (int l = 0; l < mc.nleaf; ++l) {  // leaves: 64 consecutive rows
+        HostNode o;
+        const int r0 = l * LEAF_ROWS, r1 = std::min(n, r0 + LEAF_ROWS);
+        for (int k = r0; k < r1; ++k) {
+            const uint64_t kk = cost_key(costs[k], (uint32_t)(mc.row0 + k));
+            o.key = std::min(o.key, kk);
+            o.top.push_back(kk);
         }
-        rec[1] = s;
-        for (int j = 0; j < P; ++j) rec[REC_HDR + j] = v[j];
-    } else {
-        rec[1] = 1.0f;
+        std::sort(o.top.begin(), o.top.end());
+        if ((int)o.top.size() > K) o.top.resize(K);
+        o.v.assign(P, 0.0f);
+        if (sums) {
+            const float m = u2f((uint32_t)(o.key >> 32));
+            for (int k = r0; k < r1; ++k) {
+                const float e = expf(-1.0f * (costs[k] - m));
+                o.s = o.s + e;
+                for (int j = 0; j < P; ++j) o.v[j] = o.v[j] + e * noise_rows[(size_t)k * P + j];
+            }
+        }
+        lv.push_back(std::move(o));
     }
-    for (int e = 0; e < K; ++e) {
-        const uint64_t kk = e < n ? sorted[e] : ~0ull;
-        rec[REC_HDR + P + 2 * e] = u2f((uint32_t)kk);
-        rec[REC_HDR + P + 2 * e + 1] = u2f((uint32_t)(kk >> 32));
-        for (int j = 0; j < P; ++j)
-            rec[REC_HDR + P + 2 * K + e * P + j] =
-                kk == ~0ull ? 0.0f : noise_rows[(size_t)((uint32_t)kk - mc.row0) * P + j];
+    for (int L = 0; L < mc.t_xlevel; ++L) lv = host_fold_level(lv, P, K, sums);
+    memset(rec, 0, sizeof(float) * (size_t)mc.t_xmax * rf);
+    for (size_t g = 0; g < lv.size(); ++g) {  // this rank's exchange-level nodes
+        const HostNode& o = lv[g];
+        float* R = rec + g * rf;
+        R[0] = u2f((uint32_t)(o.key >> 32));
+        R[1] = sums ? o.s : 1.0f;
+        R[2] = u2f((uint32_t)o.key);
+        for (int j = 0; j < P; ++j) R[REC_HDR + j] = o.v[j];
+        for (int e = 0; e < K; ++e) {
+            const uint64_t kk = e < (int)o.top.size() ? o.top[e] : ~0ull;
+            R[REC_HDR + P + 2 * e] = u2f((uint32_t)kk);
+            R[REC_HDR + P + 2 * e + 1] = u2f((uint32_t)(kk >> 32));
+            for (int j = 0; j < P; ++j)
+                R[REC_HDR + P + 2 * K + e * P + j] =
+                    kk == ~0ull ? 0.0f : noise_rows[(size_t)((uint32_t)kk - mc.row0) * P + j];
+        }
     }
     return SRBD_OK;
 }
 
 extern "C" int srbd_finish_host(const srbd_config* cfg, const float* recs, int32_t nrec, const float* state,
                                 const float* contact, int32_t stride, float* best, float* sigma, srbd_result* out) {
+    if (!cfg || !recs || nrec < 1) return SRBD_E_INVALID;
     srbd_config cc = *cfg;
     cc.rank = 0;
-    cc.world_size = 1;
+    cc.world_size = nrec;  // one rank buffer per rank
     ModelConst mc;
     std::string why;
     int rc = build_model(&cc, &mc, &why);
@@ -1128,24 +1215,28 @@ extern "C" int srbd_finish_host(const srbd_config* cfg, const float* recs, int32
         delete in;
         return fail(nullptr, rc, "invalid arguments");
     }
-    uint64_t bk = ~0ull;
+    // the gathered buffers are the exchange level's node list: fold it to the root
+    const bool sums = mc.method != SRBD_RANDOM_SAMPLING;
+    std::vector<HostNode> lv(mc.t_xnodes);
     float btag = 0.0f;
-    for (int r = 0; r < nrec; ++r) {
+    uint64_t bk = ~0ull;
+    for (int r = 0; r < mc.t_xnodes; ++r) {
         const float* R = recs + (size_t)r * stridef;
-        const uint64_t kk = ((uint64_t)f2u(R[0]) << 32) | f2u(R[2]);
-        btag = kk < bk ? R[3] : btag;
-        bk = kk < bk ? kk : bk;
+        HostNode& o = lv[r];
+        o.key = ((uint64_t)f2u(R[0]) << 32) | f2u(R[2]);
+        btag = o.key < bk ? R[3] : btag;
+        bk = std::min(bk, o.key);
+        o.s = R[1];
+        o.v.assign(R + REC_HDR, R + REC_HDR + P);
     }
+    while (lv.size() > 1) lv = host_fold_level(lv, P, K, sums);
     const float beta = u2f((uint32_t)(bk >> 32));
     std::vector<float> V(P + 1, 0.0f);
-    if (mc.method != SRBD_RANDOM_SAMPLING) {
-        for (int r = 0; r < nrec; ++r) {
-            const float* R = recs + (size_t)r * stridef;
-            const float sc = expf(-1.0f * (R[0] - beta));
-            for (int j = 0; j < P; ++j) V[j] = V[j] + sc * R[REC_HDR + j];
-            V[P] = V[P] + sc * R[1];
-        }
+    if (sums) {
+        for (int j = 0; j < P; ++j) V[j] = lv[0].v[j];
+        V[P] = lv[0].s;
     }
+    nrec = mc.t_xnodes;
     // global top-K keys with their rows
     std::vector<std::pair<uint64_t, const float*>> cand;
     for (int r = 0; r < nrec; ++r)
@@ -1427,7 +1518,7 @@ static void enqueue_xchg_step(srbd_ctx* c, int buf, StepOutput* out, int chain, 
     launch_rollout(mc, c->d_in, c->d_noise[buf], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
                    c->stream, fuse_next ? &next : nullptr, grp);
     launch_merge_xchg(mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, c->d_noise[buf], c->xa, out, chain,
-                      c->stream, 1, pub);
+                      c->stream, 1, pub, levels_up(c));
 }
 
 // Device-resident exchange chain as replayed graphs (the epoch lives on the device, so a replay is a
@@ -1723,8 +1814,8 @@ extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, 
         }, rollout_us);
     if (!rc)
         rc = timed([&] {
-            launch_merge_tree(mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, c->d_noise[0], c->d_part,
-                              nullptr, c->d_out, 0, c->stream);
+            launch_merge(mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, 0, c->d_noise[0], nullptr, c->d_out,
+                         0, c->stream);
         }, reduce_us);
     // the launch the step actually runs when fusion applies: rollout + the next step's draws
     if (fused_us) *fused_us = 0.0f;
@@ -1794,9 +1885,9 @@ extern "C" int srbd_time_launch(srbd_ctx* c, int32_t which, int32_t iters, float
                 break;
             }
             case SRBD_TL_STEP_MERGE:
-                nflags = launch_merge_tree(mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, c->d_noise[0],
-                                           c->d_part, nullptr, c->d_out_host, 0, c->stream, 0,
-                                           Publish{c->d_flag, ++c->seq, nullptr});
+                nflags = launch_merge(mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, 0, c->d_noise[0],
+                                      nullptr, c->d_out_host, 0, c->stream, nullptr, 0,
+                                      Publish{c->d_flag, ++c->seq, nullptr});
                 break;
             default: launch_empty(c->stream); break;
         }

@@ -28,6 +28,9 @@ constexpr int MAX_TAIL = 48;  // 4 legs x 3 axes x 4 cubic control points
 struct ModelConst {
     int H, P, PL, kind, S, method, K;
     int N, n_local, row0, ldn;
+    // reduction tree (tree_shape): global leaves, depth, the exchange level and its node count, the world size,
+    // this rank's first global leaf and its leaf count
+    int t_leaves, t_depth, t_xlevel, t_xnodes, t_xmax, t_world, leaf0, nleaf;
     float inv_m, mg, grf_min, grf_max, mu, neg_mu;
     float inertia[9], Iinv[9];
     float Q[12];
@@ -117,6 +120,66 @@ SRBD_HD int rec_pad4(int n) { return (n + 3) & ~3; }
 SRBD_HD int rec_floats_wave(int P, int K) { return rec_pad4(REC_HDR + P + 2 * K); }
 SRBD_HD int rec_floats_rank(int P, int K) { return rec_pad4(REC_HDR + P + 2 * K + K * P); }
 SRBD_HD int num_elite(int method, int num_elite_cfg) { return method == SRBD_CEM_MPPI ? num_elite_cfg : 1; }
+
+// ---- The reduction tree of one MPC step (MPPI / CEM weighted sums, random-sampling / CEM keys), fixed by global
+// rows alone -- the same for every rollout form and every rank count W, so 1-GPU and W-GPU steps give the same
+// bits.  A leaf is LEAF_ROWS consecutive global rows; its record holds m = its minimum cost, s = sum of
+// e_i = exp(-(c_i - m)) and v[j] = sum of e_i noise_i[j], each sum in the DPP order of wave_sum_f32 over the 64
+// rows (row i in lane i; rows past N contribute 0), and its K smallest (cost, row) keys.  Above the leaves every
+// node folds up to TREE_FAN consecutive children in order: m = the children's minimum, scale_c = exp(-(m_c - m))
+// (1 for random sampling), s = sum_c scale_c s_c and v[j] = sum_c scale_c v_c[j] summed child by child, keys =
+// the K smallest of the children's.  The root's sums give the update v / s (centroidal_nmpc_jax.py:828-836).
+// Level-d nodes cover LEAF_ROWS * TREE_FAN^d rows.  A W-rank problem is split at whole nodes of its exchange
+// level X: rank r holds nodes [r xmax, (r + 1) xmax) (the last rank fewer), so the ranks' level-X node records
+// gathered in rank order are the level's node list, and every rank folds that list to the root the same way.
+constexpr int LEAF_ROWS = 64;
+constexpr int TREE_FAN = 32;
+SRBD_HD int tree_nodes(int leaves, int d) {  // ceil(leaves / TREE_FAN^d)
+    int n = leaves;
+    for (int i = 0; i < d; ++i) n = (n + TREE_FAN - 1) / TREE_FAN;
+    return n;
+}
+SRBD_HD int tree_depth(int leaves) {  // the root level D: tree_nodes(leaves, D) == 1
+    int d = 0;
+    while (tree_nodes(leaves, d) > 1) ++d;
+    return d;
+}
+SRBD_HD long long tree_node_rows(int d) {  // rows of a level-d node
+    long long r = LEAF_ROWS;
+    for (int i = 0; i < d; ++i) r *= TREE_FAN;
+    return r;
+}
+struct TreeShape {
+    int leaves, depth, xlevel, xnodes, xmax;  // xmax: level-X nodes per rank (the last rank may hold fewer)
+    int node0, nnodes;                        // this rank's level-X nodes
+    long long row0, nrows;                    // this rank's rows
+    bool ok;                                  // every rank holds at least one node
+};
+// N rows over `world` ranks, rank `rank`'s share.  X: the highest level at which every rank gets at least one node
+// (world 1: the root level, one node holding everything).
+SRBD_HD TreeShape tree_shape(long long N, int world, int rank) {
+    TreeShape t;
+    t.leaves = (int)((N + LEAF_ROWS - 1) / LEAF_ROWS);
+    t.depth = tree_depth(t.leaves);
+    int x = t.depth;
+    for (;; --x) {
+        const int n = tree_nodes(t.leaves, x), per = (n + world - 1) / world;
+        if ((long long)(world - 1) * per < n || x == 0) break;
+    }
+    t.xlevel = x;
+    t.xnodes = tree_nodes(t.leaves, x);
+    t.xmax = (t.xnodes + world - 1) / world;
+    t.ok = (long long)(world - 1) * t.xmax < t.xnodes;
+    t.node0 = rank * t.xmax < t.xnodes ? rank * t.xmax : t.xnodes;
+    const int e = (rank + 1) * t.xmax < t.xnodes ? (rank + 1) * t.xmax : t.xnodes;
+    t.nnodes = e - t.node0;
+    const long long nr = tree_node_rows(x);
+    t.row0 = (long long)t.node0 * nr;
+    const long long end = (long long)e * nr;
+    t.nrows = (end < N ? end : N) - t.row0;
+    if (t.nrows < 0) t.nrows = 0;
+    return t;
+}
 
 SRBD_HD uint32_t f2u(float f) {
     union { float f; uint32_t u; } x;

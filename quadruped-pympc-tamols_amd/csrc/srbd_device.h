@@ -309,16 +309,18 @@ __device__ __forceinline__ float ld_rec(const float* p) {
         __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
-// The group's last arriver merges the group's nb block records (blocks b0 .. b0 + nb - 1, in that order)
-// into grp.grecs[g], the same arithmetic as merge_body's rescaled sums: beta_g = min key (first row on
-// ties), scale_i = exp(-(m_i - beta_g)), sum_i scale_i s_i, sum_i scale_i v_i[j] in record order, and
-// the K smallest keys of the group (one wave's K-round DPP minimum over the records' sorted lists).  The
-// records are first copied into LDS with sc1 loads (all in flight together: one memory round trip; the
-// round-2 measurement of column-by-column sc1 loads cost up to 8 us per group at 64 records), then every
-// phase reads LDS.  group_size keeps nb * rec_stride <= GROUP_LDS_FLOATS.
-// All threads of the block call it after block_epilogue's stores.
+// ---- The reduction tree in the rollout launch (srbd_core.h): leaf records and the level-1 fold ----
+// Record words are stored write-through (st_rec) and read back with sc1 loads (ld_rec) by a level-1 node's last
+// arriving block (the hand-off form of MI355X_MICROARCH.md's table row 1, GroupArgs).
+
+// Fold nb (<= TREE_FAN) child records staged in LDS (`st`, rec_stride apart, in order) into one node record `G`
+// (write-through stores): m = the children's minimum (cost, row) key, its record's tag; MPPI / CEM: s = sum_c
+// scale_c s_c and v[j] = sum_c scale_c v_c[j] child by child with scale_c = exp(-(m_c - m)); random sampling:
+// s = 1; the K smallest of the children's keys (one wave's K-round DPP minimum over their sorted lists).  The
+// merge kernel's tree levels (merge_body) and the host restatement (srbd_api.hip host_fold) are the same
+// arithmetic.  All threads of the block call it.
 template <int KM>
-__device__ __forceinline__ void group_topk(const float* st, int rec_stride, int nb, int P, int K, uint64_t* out) {
+__device__ __forceinline__ void fold_topk(const float* st, int rec_stride, int nb, int P, int K, uint64_t* out) {
     const int lane = threadIdx.x & 63;
     uint64_t lk[KM];
     const float* R = st + (size_t)lane * rec_stride + REC_HDR + P;
@@ -328,52 +330,14 @@ __device__ __forceinline__ void group_topk(const float* st, int rec_stride, int 
                                      : KEY_NONE;
     wave_topk(lk, K, out);
 }
-
-// st: GROUP_LDS_FLOATS of LDS for the staged records (a kernel that stages its noise in LDS passes that
-// buffer, dead by now; the others a static array of their own, group_reduce below).
-// Returns true (every thread of the block) when this block was its group's last arriver and wrote the group
-// record (write-through stores).
-__device__ __forceinline__ bool group_reduce_in(const ModelConst& mc, const float* __restrict__ recs, int rec_stride,
-                                                const GroupArgs& grp, int nroll, float* st) {
-    __shared__ int last_sh;
-    __shared__ float sc_sh[GROUP_MAX];
-    __shared__ float gh_sh[2];  // beta_g, tag
+__device__ __forceinline__ void fold_node_lds(const ModelConst& mc, const float* st, int rec_stride, int nb, float* G) {
+    __shared__ float sc_sh[TREE_FAN];
+    __shared__ float gh_sh[2];  // node m, tag
     __shared__ uint64_t gk_sh[MAXK + 1];
     const int tid = threadIdx.x, T = blockDim.x;
-    const int g = (int)blockIdx.x / grp.gsize, b0 = g * grp.gsize;
-    const int nb = min(grp.gsize, nroll - b0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's record stores have completed
-    __syncthreads();
-    if (tid == 0) {
-        const uint32_t old = __hip_atomic_fetch_add(grp.cnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last_sh = old == (uint32_t)(nb - 1);
-    }
-    __syncthreads();
-    if (!last_sh) return false;
-    if (tid == 0) __hip_atomic_store(grp.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-    {  // stage the nb consecutive records (sc1 loads, U per thread in flight)
-        constexpr int U = 16;
-        const int n = nb * rec_stride;
-        const float* src = recs + (size_t)b0 * rec_stride;
-        for (int i0 = 0; i0 < n; i0 += U * T) {
-            float v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int i = i0 + u * T + tid;
-                v[u] = i < n ? ld_rec(src + i) : 0.0f;
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int i = i0 + u * T + tid;
-                if (i < n) st[i] = v[u];
-            }
-        }
-    }
-    __syncthreads();
     const int P = mc.P, K = mc.K;
     const bool rs = mc.method == SRBD_RANDOM_SAMPLING;
-    float* G = grp.grecs + (size_t)g * rec_stride;
-    if (tid < 64) {  // wave 0: headers, beta_g, scales, top-K
+    if (tid < 64) {  // wave 0: headers, the node key, scales, top-K
         const float* R = st + (size_t)tid * rec_stride;
         const bool have = tid < nb;
         const float m = have ? R[0] : 0.0f;
@@ -390,13 +354,13 @@ __device__ __forceinline__ bool group_reduce_in(const ModelConst& mc, const floa
         if (K == 1) {
             if (tid == 0) gk_sh[0] = gk;
         } else if (K <= 10) {
-            group_topk<10>(st, rec_stride, nb, P, K, gk_sh);
+            fold_topk<10>(st, rec_stride, nb, P, K, gk_sh);
         } else {
-            group_topk<MAXK>(st, rec_stride, nb, P, K, gk_sh);
+            fold_topk<MAXK>(st, rec_stride, nb, P, K, gk_sh);
         }
     }
     __syncthreads();
-    if (!rs) {  // column j < P: sum_i scale_i v_i[j]; column P: sum_i scale_i s_i (record order)
+    if (!rs) {  // column j < P: sum_c scale_c v_c[j]; column P: sum_c scale_c s_c (child order)
         for (int j = tid; j <= P; j += T) {
             const int off = j < P ? REC_HDR + j : 1;
             float a = 0.0f;
@@ -415,16 +379,55 @@ __device__ __forceinline__ bool group_reduce_in(const ModelConst& mc, const floa
         st_rec(&G[REC_HDR + P + 2 * tid], __uint_as_float((uint32_t)kk));
         st_rec(&G[REC_HDR + P + 2 * tid + 1], __uint_as_float((uint32_t)(kk >> 32)));
     }
-    return true;
 }
-__device__ __forceinline__ void group_reduce(const ModelConst& mc, const float* __restrict__ recs, int rec_stride,
-                                             const GroupArgs& grp, int nroll) {
-    __shared__ float st[GROUP_LDS_FLOATS];
-    (void)group_reduce_in(mc, recs, rec_stride, grp, nroll, st);
+
+// Level-1 fold in the launch (GroupArgs::gsize > 1): the blocks of a level-1 node (TREE_FAN leaves, aligned to the
+// global leaf index: the rank's first leaf is a multiple of TREE_FAN, tree_shape) count themselves in cnt[g]; the
+// last one stages the node's leaf records (sc1 loads, all in flight together) into `st` (>= TREE_FAN * rec_stride
+// floats of LDS) and folds them into grecs[g].  Returns true (every thread) in the block that wrote the node.
+__device__ __forceinline__ bool level1_fold(const ModelConst& mc, const float* __restrict__ recs, int rec_stride,
+                                            const GroupArgs& grp, int nroll, int lpb, float* st) {
+    __shared__ int last_sh;
+    const int tid = threadIdx.x, T = blockDim.x;
+    const int bpg = TREE_FAN / lpb;  // blocks per level-1 node
+    const int g = (int)blockIdx.x / bpg;
+    const int nblk = min(bpg, nroll - g * bpg);
+    const int nb = min(TREE_FAN, mc.nleaf - g * TREE_FAN);  // the node's leaves
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's record stores have completed
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(grp.cnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_sh = old == (uint32_t)(nblk - 1);
+    }
+    __syncthreads();
+    if (!last_sh) return false;
+    if (tid == 0) __hip_atomic_store(grp.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    {  // stage the node's nb leaf records (sc1 loads, U per thread in flight)
+        constexpr int U = 16;
+        const int n = nb * rec_stride;
+        const float* src = recs + (size_t)g * TREE_FAN * rec_stride;
+        for (int i0 = 0; i0 < n; i0 += U * T) {
+            float v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * T + tid;
+                v[u] = i < n ? ld_rec(src + i) : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * T + tid;
+                if (i < n) st[i] = v[u];
+            }
+        }
+    }
+    __syncthreads();
+    fold_node_lds(mc, st, rec_stride, nb, grp.grecs + (size_t)g * rec_stride);
+    return true;
 }
 
 // Wave sum in a fixed DPP tree (row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15/31); the total
-// lands in lane 63.  All 64 lanes must be active.
+// lands in lane 63.  All 64 lanes must be active.  The leaf order of the reduction tree (srbd_core.h); the host
+// restatement is srbd_api.hip host_wave_sum.
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ float dpp_f32(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, 0xF, false));
@@ -439,182 +442,109 @@ __device__ __forceinline__ float wave_sum_f32(float v) {
     return v;
 }
 
-// The block record's weighted sums: v[j] = sum_k e_k noise_k[j] for the P columns and s = sum_k e_k (column
-// P), over the block's SPB samples (noise `base` = row 0 of the block, SoA [P][ldn]); e in e_sh[0..SPB).
-//  SPB = 64 (four-lane kernel, small thread blocks): thread j sums its column's 64 products in sample order,
-//   its 16 float4 loads in flight at once (one memory round trip, a 128-op dependent chain).
-//  SPB = 128 / 256 (thread kernel): that chain is 2-4x longer with 2-4 round trips (113 of the C5 rollout's
-//   176 us); instead wave w takes columns w, w + NW, ..., lane l reads samples SPL l .. SPL l + SPL - 1 of a
-//   column in one load, forms its SPL products in sample order and the wave adds the 64 partials in a fixed
-//   DPP tree; CB columns' loads are issued together.
-template <int SPL>
-__device__ __forceinline__ void block_wsum_tree(const ModelConst& mc, const StepInput* __restrict__ in,
-                                                const float* __restrict__ base, bool zs, const float* e_sh,
-                                                float* rec) {
-    constexpr int CB = SPL == 4 ? 8 : 12;  // columns per batch of loads (8 / 12 / 16 / 20 at SPL 4 within noise)
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, NW = blockDim.x >> 6;
-    const int P = mc.P;
-    const size_t ldn = (size_t)mc.ldn;
-    float e[SPL];
-#pragma unroll
-    for (int u = 0; u < SPL; ++u) e[u] = e_sh[SPL * lane + u];
-    for (int j0 = w; j0 <= P; j0 += CB * NW) {
-        float z[CB][SPL];
-#pragma unroll
-        for (int b = 0; b < CB; ++b) {
-            const int j = j0 + b * NW;
-            const float* col = base + (size_t)(j < P ? j : 0) * ldn + SPL * lane;
-            if constexpr (SPL == 4) {
-                const float4 v = *reinterpret_cast<const float4*>(col);
-                z[b][0] = v.x, z[b][1] = v.y, z[b][2] = v.z, z[b][3] = v.w;
-            } else {
-                const float2 v = *reinterpret_cast<const float2*>(col);
-                z[b][0] = v.x, z[b][1] = v.y;
-            }
-        }
-#pragma unroll
-        for (int b = 0; b < CB; ++b) {
-            const int j = j0 + b * NW;
-            if (j > P) break;
-            float a;
-            if (j < P) {
-                const float sj = zs ? in->sigma[j] : 1.0f;  // x * 1 == x
-                a = e[0] * (z[b][0] * sj);
-#pragma unroll
-                for (int u = 1; u < SPL; ++u) a = a + e[u] * (z[b][u] * sj);
-            } else {
-                a = e[0];
-#pragma unroll
-                for (int u = 1; u < SPL; ++u) a = a + e[u];
-            }
-            a = wave_sum_f32(a);
-            if (lane == 63) st_rec(&rec[j < P ? REC_HDR + j : 1], a);
-        }
-    }
-}
-__device__ __forceinline__ void block_wsum(const ModelConst& mc, const StepInput* __restrict__ in, int SPB,
-                                           const float* __restrict__ base, bool zs, const float* e_sh, float* rec) {
-    if (SPB == 128) return block_wsum_tree<2>(mc, in, base, zs, e_sh, rec);
-    if (SPB == 256) return block_wsum_tree<4>(mc, in, base, zs, e_sh, rec);
-    const int tid = threadIdx.x, T = blockDim.x, P = mc.P;
-    const size_t ldn = (size_t)mc.ldn;
-    for (int j = tid; j <= P; j += T) {
-        float a = 0.0f;
-        if (j < P) {
-            const float4* row = reinterpret_cast<const float4*>(base + (size_t)j * ldn);
-            const float sj = zs ? in->sigma[j] : 1.0f;  // x * 1 == x
-#pragma unroll 16
-            for (int i = 0; i < SPB / 4; ++i) {
-                const float4 v = row[i];
-                a = a + e_sh[4 * i] * (v.x * sj);
-                a = a + e_sh[4 * i + 1] * (v.y * sj);
-                a = a + e_sh[4 * i + 2] * (v.z * sj);
-                a = a + e_sh[4 * i + 3] * (v.w * sj);
-            }
-            st_rec(&rec[REC_HDR + j], a);
-        } else {
-            for (int i = 0; i < SPB; ++i) a = a + e_sh[i];
-            st_rec(&rec[1], a);
-        }
-    }
-}
-
-// block_wsum with the block's noise staged in LDS, zst[s P + j] (sample-major: consecutive threads read
-// consecutive columns, no bank conflicts), SPB = 64: thread j sums its column's 64 products in sample order
-// exactly as block_wsum's SPB = 64 path does from global memory, so the record is the same bit for bit.
-__device__ __forceinline__ void block_wsum_lds(const ModelConst& mc, const StepInput* __restrict__ in, const float* zst,
-                                               bool zs, const float* e_sh, float* rec) {
-    const int tid = threadIdx.x, T = blockDim.x, P = mc.P;
-    for (int j = tid; j <= P; j += T) {
-        float a = 0.0f;
-        if (j < P) {
-            const float sj = zs ? in->sigma[j] : 1.0f;  // x * 1 == x
-#pragma unroll 16
-            for (int i = 0; i < 64; ++i) a = a + e_sh[i] * (zst[i * P + j] * sj);
-            st_rec(&rec[REC_HDR + j], a);
-        } else {
-#pragma unroll 16
-            for (int i = 0; i < 64; ++i) a = a + e_sh[i];
-            st_rec(&rec[1], a);
-        }
-    }
-}
-
-// Per-block record (see srbd_core.h REC_*): min key, sum_k e_k, sum_k e_k * noise_k[j], top-K keys,
-// e_k = exp(-(c_k - m_b)).  SPB samples per block (multiple of 4); the thread owning sample `sib`
-// passes it (others pass sib = -1) with its `tag` (the gait-adaptive step frequency, else 0), which
-// the owner of the block's best row stores in the record header.  All threads of the block must call
-// this.
-// CEMT: a CEM kernel (K >= 2: the top-K by ranks); the others have K = 1 and carry no top-K code or LDS.
-// ZS: the block's noise is staged in LDS (sample-major, SPB = 64, block_wsum_lds), and the group
-// reduction stages its records in that buffer (>= GROUP_LDS_FLOATS floats) once the sums are formed.
+// The block's leaf records (srbd_core.h): SPB samples = lpb = SPB / 64 leaves (four-lane: 1; thread form: 1, 2
+// or 4), leaf b of block x at record x lpb + b.  The thread owning sample `sib` passes it (others -1) with its
+// `tag` (the gait-adaptive step frequency, else 0), which the owner of the leaf's best row stores in the header.
+//  keys -> LDS; leaf minima (one wave per leaf); CEM: each leaf's K smallest keys by ranks (every sample counts
+//  the leaf's keys below its own; the `lps` lanes of a sample split the count, summed by DPP); e = exp(-(c - m));
+//  the sums: waves_per_leaf = NW / lpb waves take a leaf's columns in turn, lane l the leaf's row l: one product
+//  e_l noise_l[j] per lane and wave_sum_f32 (column P: e_l alone).  The noise comes from the LDS stage `zst`
+//  (ZS: four-lane zero-order, row l at zst[l * zstride]) or from the SoA noise (coalesced).
+// Then the level-1 fold (grp.gsize > 1).  All threads call it; returns level1_fold's verdict (false without one).
 template <bool CEMT, bool ZS = false>
 __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepInput* __restrict__ in, const int SPB,
                                                int sib, bool valid, float cost, const float* __restrict__ noise,
-                                               float* __restrict__ recs, int rec_stride, float* e_sh, uint64_t* red,
-                                               uint64_t* elite_sh, float tag, const GroupArgs& grp, int nroll,
-                                               float* zst = nullptr) {
-    constexpr bool cemt = CEMT;
-    const int tid = threadIdx.x;
-    const int k0 = blockIdx.x * SPB;
-    const uint64_t key = (sib >= 0 && valid) ? cost_key(cost, (uint32_t)(mc.row0 + k0 + sib)) : ~0ull;
-    float* rec = recs + (size_t)blockIdx.x * rec_stride;
+                                               float* __restrict__ recs, int rec_stride, float tag,
+                                               const GroupArgs& grp, int nroll, float* zst = nullptr,
+                                               int zstride = 0) {
+    __shared__ uint64_t ks[256];
+    __shared__ float e_sh[256];
+    __shared__ uint64_t lmin[4];
+    __shared__ uint64_t lel[CEMT ? 4 : 1][CEMT ? MAXK : 1];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int NW = (int)blockDim.x >> 6, lpb = SPB >> 6, wpl = NW / lpb;
     const int P = mc.P, K = mc.K;
-    uint64_t bkey;
-    if (!CEMT || K == 1) {
-        bkey = block_min_u64(key, red);
-        if (tid == 0) elite_sh[0] = bkey;
-    } else if constexpr (CEMT) {
-        // The block's K smallest keys by rank: every sample counts the block's keys below its own (the
-        // `lps` lanes of a sample -- 4 in the four-lane layouts, 2 in the two-lane one, else 1 -- split the
-        // count, summed by DPP),
-        // and a sample of rank < K stores its key at elite_sh[rank] (keys are unique; invalid samples all
-        // carry ~0 and can only fill the tail with ~0).  Two barriers, where K rounds of a block minimum
-        // took 2K (C3 rollout: see DESIGN.md).
-        __shared__ uint64_t ks[256];
-        const int lps = (int)blockDim.x / SPB, part = tid & (lps - 1), s = tid / lps;
-        if (sib >= 0) ks[sib] = key;
-        if (tid < K) elite_sh[tid] = ~0ull;
-        __syncthreads();
-        const uint64_t mine = ks[s];
-        const int span = SPB / lps, i0 = part * span;
-        int cnt = 0;
-        for (int i = 0; i < span; ++i) cnt += ks[i0 + i] < mine ? 1 : 0;
-        if (lps >= 2) cnt += __builtin_amdgcn_mov_dpp(cnt, 0xB1, 0xF, 0xF, true);  // quad lanes (1, 0, 3, 2)
-        if (lps == 4) cnt += __builtin_amdgcn_mov_dpp(cnt, 0x4E, 0xF, 0xF, true);  // quad lanes (2, 3, 0, 1)
-        if (part == 0 && cnt < K) elite_sh[cnt] = mine;
-        __syncthreads();
-        bkey = elite_sh[0];
+    const int k0 = blockIdx.x * SPB;
+    const bool rs = mc.method == SRBD_RANDOM_SAMPLING;
+    const uint64_t key = (sib >= 0 && valid) ? cost_key(cost, (uint32_t)(mc.row0 + k0 + sib)) : KEY_NONE;
+    if (sib >= 0) ks[sib] = key;
+    __syncthreads();
+    if (w < lpb) {
+        const uint64_t m = wave_min_u64(ks[64 * w + lane]);
+        if (lane == 0) lmin[w] = m;
     }
-    const float m = u2f((uint32_t)(bkey >> 32));
-    SRBD_RSTAMP(3);
-    if (mc.method != SRBD_RANDOM_SAMPLING) {
-        if (sib >= 0) e_sh[sib] = valid ? expf(-1.0f * (cost - m)) : 0.0f;
-        __syncthreads();
-        const bool zs = cemt && zs_scaled(mc, in);
-        if constexpr (ZS)
-            block_wsum_lds(mc, in, zst, zs, e_sh, rec);
-        else
-            block_wsum(mc, in, SPB, noise + k0, zs, e_sh, rec);
+    if constexpr (CEMT) {
+        if (K > 1) {
+            for (int i = tid; i < lpb * MAXK; i += (int)blockDim.x) lel[i / MAXK][i % MAXK] = KEY_NONE;
+            __syncthreads();
+            const int lps = (int)blockDim.x / SPB, part = tid & (lps - 1), s = tid / lps, b = s >> 6;
+            const uint64_t mine = ks[s];
+            const int span = 64 / lps, i0 = 64 * b + part * span;
+            int cnt = 0;
+            for (int i = 0; i < span; ++i) cnt += ks[i0 + i] < mine ? 1 : 0;
+            if (lps >= 2) cnt += __builtin_amdgcn_mov_dpp(cnt, 0xB1, 0xF, 0xF, true);  // quad lanes (1, 0, 3, 2)
+            if (lps == 4) cnt += __builtin_amdgcn_mov_dpp(cnt, 0x4E, 0xF, 0xF, true);  // quad lanes (2, 3, 0, 1)
+            if (part == 0 && cnt < K) lel[b][cnt] = mine;
+        }
     }
     __syncthreads();
-    SRBD_RSTAMP(4);
-    if (tid == 0) {
-        st_rec(&rec[0], m);
-        st_rec(&rec[2], u2f((uint32_t)bkey));
-        if (mc.method == SRBD_RANDOM_SAMPLING) st_rec(&rec[1], 1.0f);
+    SRBD_RSTAMP(3);
+    if (!rs) {
+        if (sib >= 0) e_sh[sib] = valid ? expf(-1.0f * (cost - u2f((uint32_t)(lmin[sib >> 6] >> 32)))) : 0.0f;
+        __syncthreads();
+        const int b = w / wpl;
+        const float e = e_sh[64 * b + lane];
+        const bool zs = CEMT && zs_scaled(mc, in);
+        float* rec = recs + (size_t)(blockIdx.x * lpb + b) * rec_stride;
+        const size_t ldn = (size_t)mc.ldn;
+        const float* col0 = noise + k0 + 64 * b + lane;
+        constexpr int CB = 8;  // columns whose loads are in flight together
+        for (int j0 = w % wpl; j0 <= P; j0 += CB * wpl) {
+            float z[CB];
+#pragma unroll
+            for (int u = 0; u < CB; ++u) {
+                const int j = j0 + u * wpl;
+                const int jl = j < P ? j : 0;
+                if constexpr (ZS)
+                    z[u] = zst[lane * zstride + jl];
+                else
+                    z[u] = col0[(size_t)jl * ldn];
+            }
+#pragma unroll
+            for (int u = 0; u < CB; ++u) {
+                const int j = j0 + u * wpl;
+                if (j > P) break;
+                float prod = e;
+                if (j < P) {
+                    const float sj = zs ? in->sigma[j] : 1.0f;  // x * 1 == x
+                    prod = e * (z[u] * sj);
+                }
+                const float tot = wave_sum_f32(prod);
+                if (lane == 63) st_rec(&rec[j < P ? REC_HDR + j : 1], tot);
+            }
+        }
     }
-    if (sib >= 0 && key == bkey) st_rec(&rec[3], tag);  // keys are unique: exactly one writer
-    if (tid < K) {
-        const uint64_t kk = elite_sh[tid];
-        st_rec(&rec[REC_HDR + P + 2 * tid], u2f((uint32_t)kk));
-        st_rec(&rec[REC_HDR + P + 2 * tid + 1], u2f((uint32_t)(kk >> 32)));
+    SRBD_RSTAMP(4);
+    if (tid < lpb) {  // headers of leaf tid
+        float* rec = recs + (size_t)(blockIdx.x * lpb + tid) * rec_stride;
+        const uint64_t m = lmin[tid];
+        st_rec(&rec[0], u2f((uint32_t)(m >> 32)));
+        st_rec(&rec[2], u2f((uint32_t)m));
+        if (rs) st_rec(&rec[1], 1.0f);
+    }
+    if (sib >= 0 && key == lmin[sib >> 6]) st_rec(&recs[(size_t)(blockIdx.x * lpb + (sib >> 6)) * rec_stride + 3], tag);
+    for (int i = tid; i < lpb * K; i += (int)blockDim.x) {  // keys
+        const int b = i / K, q = i % K;
+        uint64_t kk = lmin[b];
+        if constexpr (CEMT) kk = K > 1 ? lel[b][q] : kk;
+        float* rec = recs + (size_t)(blockIdx.x * lpb + b) * rec_stride;
+        st_rec(&rec[REC_HDR + P + 2 * q], u2f((uint32_t)kk));
+        st_rec(&rec[REC_HDR + P + 2 * q + 1], u2f((uint32_t)(kk >> 32)));
     }
     if (grp.gsize > 1) {
-        if constexpr (ZS)
-            return group_reduce_in(mc, recs, rec_stride, grp, nroll, zst);
-        else
-            group_reduce(mc, recs, rec_stride, grp, nroll);
+        if (zst) return level1_fold(mc, recs, rec_stride, grp, nroll, lpb, zst);
+        __shared__ float st[GROUP_LDS_FLOATS];
+        return level1_fold(mc, recs, rec_stride, grp, nroll, lpb, st);
     }
     return false;
 }

@@ -200,9 +200,6 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
         SRBD_RSTAMP(5);
         return;
     }
-    __shared__ float e_sh[128];
-    __shared__ uint64_t red[8];
-    __shared__ uint64_t elite_sh[MAXK];
 
     constexpr bool CT = HT > 0 && (KIND == SRBD_ZERO_ORDER || ST > 0);
     const int SPB = (int)blockDim.x >> 2;  // samples per block: 64 or 128
@@ -218,7 +215,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     // 38.5 KB of LDS per block keeps four blocks per CU (H = 16 would need 51 KB: three).
     constexpr bool ZST = CT && KIND == SRBD_ZERO_ORDER && !EXT && HT <= 12;
     constexpr int PCT = ZST ? 12 * HT : 1;
-    __shared__ float zst[ZST ? (64 * PCT > GROUP_LDS_FLOATS ? 64 * PCT : GROUP_LDS_FLOATS) : 1];
+    constexpr int ZSTR = PCT + 1;  // sample stride of the stage: odd, so the epilogue's row-per-lane reads hit 64 banks
+    __shared__ float zst[ZST ? (64 * ZSTR > GROUP_LDS_FLOATS ? 64 * ZSTR : GROUP_LDS_FLOATS) : 1];
     __shared__ float bls[ZST ? PCT : 1];
     __shared__ float sls[ZST && CEMT ? PCT : 1];
     const int tid = threadIdx.x;
@@ -501,14 +499,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
 #pragma unroll
         for (int q = 0; q < 3; ++q)
 #pragma unroll
-            for (int i = 0; i < NPRE; ++i) zst[sib * PCT + lq * PL + q * HT + i] = pre[q][i];
+            for (int i = 0; i < NPRE; ++i) zst[sib * ZSTR + lq * PL + q * HT + i] = pre[q][i];
     }
 #ifdef SRBD_DIAG_NOEPI  // diagnostic build: no block epilogue (timing only)
     if (tid == 0) recs[blockIdx.x] = cost;
     return;
 #endif
     const bool glast = block_epilogue<CEMT, ZST>(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride,
-                                                 e_sh, red, elite_sh, 0.0f, grp, nroll, zst);
+                                                 0.0f, grp, nroll, ZST ? zst : nullptr, ZSTR);
     if constexpr (FM && ZST && !CEMT)
         if (glast) final_merge<256>(mc, in, noise, rec_stride, grp, zst);
     SRBD_RSTAMP(5);
@@ -530,9 +528,6 @@ __global__ void __launch_bounds__(512) rollout_ga_quad_kernel(const ModelConst m
                   ((int)gridDim.x - nroll) * (int)blockDim.x);
         return;
     }
-    __shared__ float e_sh[128];
-    __shared__ uint64_t red[8];
-    __shared__ uint64_t elite_sh[MAXK];
     const int H = HT > 0 ? HT : mc.H, S = mc.S, PL = mc.PL;  // HT: horizon fixed at compile time
     const int tid = threadIdx.x;
     const int q4 = tid & 3;
@@ -634,8 +629,7 @@ __global__ void __launch_bounds__(512) rollout_ga_quad_kernel(const ModelConst m
     cost = cost + (df * 100.0f) * df;  // GA:500
     if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
     if (valid && q4 == 0 && costs) costs[k] = cost;
-    block_epilogue<false>(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh,
-                          f, grp, nroll);
+    block_epilogue<false>(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride, f, grp, nroll);
 }
 
 // ------------------------------------------------------------------ merge
@@ -644,7 +638,6 @@ __device__ __forceinline__ uint64_t rec_key(const float* R, int P, int q) {
 }
 
 constexpr int MERGE_THREADS = 1024;
-constexpr int MERGE_PREF = 24;  // record values of the weighted sums loaded per thread before beta is known
 constexpr int MERGE_RPT = 8;    // record headers per thread (nrec <= MERGE_RPT * MERGE_THREADS)
 // The LDS-staged merge runs two waves per SIMD: its phases are short dependent chains that every
 // wave repeats (index math, the beta reduction), so 16 waves pay ~2x the issue of 8, while fewer
@@ -779,7 +772,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
                                            StepOutput* __restrict__ out, int chain, int ctr_inc,
                                            uint64_t* __restrict__ dbg, uint32_t* __restrict__ flag, uint32_t seq,
                                            int split_cs, int fence_sys, MergeShared<NT>& sh, float* smem,
-                                           bool prestaged = false) {
+                                           bool prestaged = false, int levels_up = 0) {
     constexpr int NW = NT / 64;
     uint64_t* red = sh.red;
     uint64_t* elite = sh.elite;
@@ -817,16 +810,6 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         else
             *reinterpret_cast<float*>(dst) = v;
     };
-    // first level of a two-level merge: block b reduces its slice into rank_out[b] (a merge inside another
-    // launch -- final_merge -- has gridDim > 1 but no rank_out)
-    if (!split && rank_out && gridDim.x > 1) {
-        // 32-bit: blockIdx.x * nrec < 64 * MAX_RECORDS (a 64-bit division is a ~100-instruction sequence)
-        const int b0 = (int)(blockIdx.x * (uint32_t)nrec / gridDim.x),
-                  b1 = (int)((blockIdx.x + 1) * (uint32_t)nrec / gridDim.x);
-        recs += (size_t)b0 * rec_stride;
-        nrec = b1 - b0;
-        rank_out += (size_t)blockIdx.x * rec_floats_rank(P, K);
-    }
     // this block's columns: local index i -> parameter column jc(i)
     const int j0 = split && !tailblk ? ((int)blockIdx.x - 1) * split_cs : 0;
     const int ncol = !split ? P : (tailblk ? mc.ntail : min(split_cs, P - j0));
@@ -835,13 +818,16 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     auto owns = [&](int jj) { return !split || tailblk || !is_tail_col(mc, jj); };
     const bool do_tail = out && (!split || tailblk);
     const int cols = ncol + 1;
-    int G = (STAGE ? MERGE_STAGE_THREADS : T) / cols;
-    G = G < 1 ? 1 : (G > nrec ? nrec : G);
     const int nrec_pad = (nrec + 3) & ~3;
+    // the tree levels above the input records: n1 nodes at most (merge_smem_bytes)
+    const int n1 = (nrec + TREE_FAN - 1) / TREE_FAN, lvf = (n1 * cols + 3) & ~3;
     float* stage = smem;
     float* scale = STAGE ? smem + (size_t)nrec * rec_stride : smem;
-    float* part = scale + nrec_pad;
-    float* erow = part + ((G * cols + 3) & ~3);
+    float* lvA = scale + nrec_pad;
+    float* lvB = lvA + lvf;
+    uint64_t* nkA = reinterpret_cast<uint64_t*>(lvB + lvf);  // 8-byte aligned: lvf and nrec_pad are multiples of 4
+    uint64_t* nkB = nkA + n1;
+    float* erow = reinterpret_cast<float*>(nkB + n1);
 
     // ---- L: loads.  The StepInput fields the output phases need are fetched first, so their latency
     // hides under the record loads instead of stalling the tail.
@@ -919,7 +905,6 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     }
     // ---- 1. beta.  Staged: only the waves holding a record scan and reduce (nrec <= RPT * T, but a
     // step's few hundred records sit in the first waves), and the block minimum is over those waves.
-    float mr[STAGE ? 1 : MERGE_RPT];  // staged: re-read from LDS when scaling
     uint64_t mine = KEY_NONE;
     float mtag = 0.0f;
     const int nhw = STAGE ? (nrec + 63) >> 6 : NW;  // waves that hold a record (staged: <= RPT * NW)
@@ -927,11 +912,9 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
 #pragma unroll
         for (int i = 0; i < (STAGE ? MERGE_RPT : MERGE_RPT); ++i) {
             const int r = tid + i * T;
-            if (!STAGE) mr[i] = 0.0f;
             if (r < nrec) {
                 const float* R = recs + (size_t)r * rec_stride;
                 const float m_r = R[0];
-                if (!STAGE) mr[i] = m_r;
                 const uint64_t kk = ((uint64_t)f2u(m_r) << 32) | (uint64_t)f2u(R[2]);
                 const float tg = R[3];
                 mtag = kk < mine ? tg : mtag;
@@ -942,18 +925,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         if (lane == 0 && wv < NW) red[wv] = wmin;
     }
     MERGE_MARK(0);
-    const int j = (int)((uint32_t)tid % (uint32_t)cols), g = (int)((uint32_t)tid / (uint32_t)cols);
-    const bool summer = !rs && tid < G * cols;
-    const int r0 = summer ? (int)((uint32_t)(g * nrec) / (uint32_t)G) : 0,
-              r1 = summer ? (int)((uint32_t)((g + 1) * nrec) / (uint32_t)G) : 0;
-    const int off = j < ncol ? REC_HDR + jc(j) : 1;
-    constexpr int NPV = STAGE ? 1 : MERGE_PREF;  // staged: the sums read LDS directly
-    float pv[NPV];
-    if constexpr (!STAGE) {
-#pragma unroll
-        for (int i = 0; i < MERGE_PREF; ++i) pv[i] = (r0 + i < r1) ? recs[(size_t)(r0 + i) * rec_stride + off] : 0.0f;
-        tail_prep();
-    }
+    if constexpr (!STAGE) tail_prep();
     MERGE_MARK(1);
     __syncthreads();
     MERGE_MARK(2);
@@ -963,62 +935,117 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     if (mine == bkey && mine != KEY_NONE) tag_sh = mtag;  // keys are unique: one writer
     MERGE_STAMP(1);
 
-    // ---- 2./3. softmax-weighted sums
+    // ---- 2./3. the reduction tree's sums (srbd_core.h): the input records folded level by level, TREE_FAN
+    // consecutive children per node in order (the fold of fold_node_lds, srbd_device.h), to the root -- or, for a
+    // rank record (rank_out), `levels_up` levels, up to this rank's nodes of the exchange level.  Every block of a
+    // column split folds its own columns; all recompute the node keys the same way.
+    auto off_of = [&](int jj) { return jj < ncol ? REC_HDR + jc(jj) : 1; };
+    int nlev = nrec;            // nodes of the current level
+    bool lev_recs = true;       // the current level is the input records
+    const float* lvp = nullptr;  // values of the current level (lev_recs: the records)
+    const uint64_t* nkp = nullptr;
     if (!rs) {
-#pragma unroll
-        for (int i = 0; i < MERGE_RPT; ++i) {
-            const int r = tid + i * T;
-            if (r < nrec) scale[r] = expf(-1.0f * ((STAGE ? recs[(size_t)r * rec_stride] : mr[i]) - beta));
-        }
-        MERGE_MARK(3);
-        __syncthreads();
-        MERGE_MARK(4);
-        if constexpr (STAGE) {  // (group, column) items; more columns than threads loop (G = 1)
-            for (int q = tid; !rs && q < G * cols; q += T) {
-                const int jq = (int)((uint32_t)q % (uint32_t)cols), gq = (int)((uint32_t)q / (uint32_t)cols);
-                const int q0 = (int)((uint32_t)(gq * nrec) / (uint32_t)G), q1 = (int)((uint32_t)((gq + 1) * nrec) / (uint32_t)G);
-                const int oq = jq < ncol ? REC_HDR + jc(jq) : 1;
-                // batches of 8 LDS reads in flight, then the fixed-order sum
-                float a = 0.0f;
-                int r = q0;
-                for (; r + 8 <= q1; r += 8) {
-                    float sv[8], xv[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        sv[u] = scale[r + u];
-                        xv[u] = recs[(size_t)(r + u) * rec_stride + oq];
-                    }
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) a = a + sv[u] * xv[u];
+        float* lv_out = lvA;
+        uint64_t* nk_out = nkA;
+        for (int L = 0; rank_out ? L < levels_up : nlev > 1; ++L) {
+            const int n2 = (nlev + TREE_FAN - 1) / TREE_FAN;
+            for (int g2 = tid; g2 < n2; g2 += T) {  // node keys: the children's minimum
+                uint64_t k = KEY_NONE;
+                const int c1 = min(TREE_FAN * g2 + TREE_FAN, nlev);
+                for (int c = TREE_FAN * g2; c < c1; ++c) {
+                    const uint64_t kc = lev_recs ? ((uint64_t)f2u(recs[(size_t)c * rec_stride]) << 32) |
+                                                       (uint64_t)f2u(recs[(size_t)c * rec_stride + 2])
+                                                 : nkp[c];
+                    k = umin64(k, kc);
                 }
-                for (; r < q1; ++r) a = a + scale[r] * recs[(size_t)r * rec_stride + oq];
-                part[gq * cols + jq] = a;
+                nk_out[g2] = k;
             }
-            MERGE_MARK(5);
-        } else if (summer) {
-            float a = 0.0f;
-#pragma unroll
-            for (int i = 0; i < MERGE_PREF; ++i)
-                if (r0 + i < r1) a = a + scale[r0 + i] * pv[i];
-            for (int rb0 = r0 + MERGE_PREF; rb0 < r1; rb0 += MERGE_PREF) {
-#pragma unroll
-                for (int i = 0; i < MERGE_PREF; ++i)
-                    pv[i] = (rb0 + i < r1) ? recs[(size_t)(rb0 + i) * rec_stride + off] : 0.0f;
-#pragma unroll
-                for (int i = 0; i < MERGE_PREF; ++i)
-                    if (rb0 + i < r1) a = a + scale[rb0 + i] * pv[i];
+            __syncthreads();
+            for (int c = tid; c < nlev; c += T) {  // child scales
+                const float mc_ = lev_recs ? recs[(size_t)c * rec_stride] : u2f((uint32_t)(nkp[c] >> 32));
+                scale[c] = expf(-1.0f * (mc_ - u2f((uint32_t)(nk_out[c / TREE_FAN] >> 32))));
             }
-            part[g * cols + j] = a;
+            __syncthreads();
+            for (int q = tid; q < n2 * cols; q += T) {  // (node, column) sums, child by child
+                const int g2 = (int)((uint32_t)q / (uint32_t)cols), jq = (int)((uint32_t)q % (uint32_t)cols);
+                const int c0 = TREE_FAN * g2, c1 = min(c0 + TREE_FAN, nlev);
+                float a = 0.0f;
+                if (lev_recs) {
+                    const int oq = off_of(jq);
+                    for (int c = c0; c < c1; ++c) a = a + scale[c] * recs[(size_t)c * rec_stride + oq];
+                } else {
+                    for (int c = c0; c < c1; ++c) a = a + scale[c] * lvp[(size_t)c * cols + jq];
+                }
+                lv_out[(size_t)g2 * cols + jq] = a;
+            }
+            __syncthreads();
+            lvp = lv_out;
+            nkp = nk_out;
+            lev_recs = false;
+            nlev = n2;
+            lv_out = lv_out == lvA ? lvB : lvA;
+            nk_out = nk_out == nkA ? nkB : nkA;
         }
-        __syncthreads();
-        MERGE_MARK(6);
-        for (int jj = tid; jj < cols; jj += T) {
-            float a = 0.0f;
-            for (int gg = 0; gg < G; ++gg) a = a + part[gg * cols + jj];
-            Vs[jj] = a;
-        }
+        MERGE_MARK(5);
+        if (!rank_out)  // the root
+            for (int jj = tid; jj < cols; jj += T) Vs[jj] = lev_recs ? recs[off_of(jj)] : lvp[jj];
     }
     MERGE_STAMP(2);
+
+    if (rank_out) {  // ---- a rank record: this rank's nodes of the exchange level (unsplit: column i == i)
+        const int rstride = rec_floats_rank(P, K);
+        int span = 1;
+        for (int L = 0; L < levels_up; ++L) span *= TREE_FAN;
+        const bool zs = zs_scaled(mc, in);
+        const int nout = (nrec + span - 1) / span;  // == nlev after the folds (random sampling folds no sums)
+        for (int g = 0; g < nout; ++g) {
+            const int r0 = g * span, r1 = min(r0 + span, nrec);
+            float* R = rank_out + (size_t)g * rstride;
+            // the node's key (its records' minimum) and the tag of the record holding it
+            uint64_t km = KEY_NONE;
+            for (int r = r0 + tid; r < r1; r += T)
+                km = umin64(km, ((uint64_t)f2u(recs[(size_t)r * rec_stride]) << 32) | f2u(recs[(size_t)r * rec_stride + 2]));
+            km = wave_min_u64(km);
+            __syncthreads();
+            if (lane == 0) red[wv] = km;
+            __syncthreads();
+            uint64_t nk = red[0];
+            for (int i = 1; i < NW; ++i) nk = umin64(nk, red[i]);
+            for (int r = r0 + tid; r < r1; r += T)
+                if ((((uint64_t)f2u(recs[(size_t)r * rec_stride]) << 32) | f2u(recs[(size_t)r * rec_stride + 2])) == nk)
+                    tag_sh = recs[(size_t)r * rec_stride + 3];
+            if (K == 1) {
+                if (tid == 0) elite[0] = nk;
+            } else {
+                block_topk_rank<NT>(recs + (size_t)r0 * rec_stride, r1 - r0, rec_stride, P, K, elite, tk);
+            }
+            __syncthreads();
+            for (int jj = tid; jj < P; jj += T)
+                R[REC_HDR + jj] = rs ? 0.0f : (lev_recs ? recs[(size_t)g * rec_stride + REC_HDR + jj] : lvp[(size_t)g * cols + jj]);
+            for (int e = tid; e < K; e += T) {
+                R[REC_HDR + P + 2 * e] = u2f((uint32_t)elite[e]);
+                R[REC_HDR + P + 2 * e + 1] = u2f((uint32_t)(elite[e] >> 32));
+            }
+            const bool rows = rs || cem;  // the rows the root needs: random sampling's best, CEM's elite
+            for (int t = tid; t < K * P; t += T) {
+                const int e = t / P, jj = t % P;
+                float v = 0.0f;
+                if (rows && elite[e] != KEY_NONE) {
+                    v = noise[(size_t)jj * mc.ldn + ((int)(uint32_t)elite[e] - mc.row0)];
+                    if (zs) v = v * in->sigma[jj];
+                }
+                R[REC_HDR + P + 2 * K + t] = v;
+            }
+            if (tid == 0) {
+                R[0] = u2f((uint32_t)(nk >> 32));
+                R[1] = rs ? 1.0f : (lev_recs ? recs[(size_t)g * rec_stride + 1] : lvp[(size_t)g * cols + P]);
+                R[2] = u2f((uint32_t)nk);
+                R[3] = tag_sh;
+            }
+            __syncthreads();
+        }
+        return;
+    }
 
     // ---- 4. top-K keys (ascending; keys are unique).  The tail block of a CEM split never reads
     // elite rows (sigma belongs to the slices), so it skips them.
@@ -1064,20 +1091,6 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     __syncthreads();
 
     // ---- 6. outputs
-    if (rank_out) {  // unsplit: column i == parameter i
-        for (int jj = tid; jj < P; jj += T) rank_out[REC_HDR + jj] = rs ? 0.0f : Vs[jj];
-        for (int e = tid; e < K; e += T) {
-            rank_out[REC_HDR + P + 2 * e] = u2f((uint32_t)elite[e]);
-            rank_out[REC_HDR + P + 2 * e + 1] = u2f((uint32_t)(elite[e] >> 32));
-        }
-        for (int t = tid; t < K * P; t += T) rank_out[REC_HDR + P + 2 * K + t] = need_rows ? erow[t] : 0.0f;
-        if (tid == 0) {
-            rank_out[0] = beta;
-            rank_out[1] = rs ? 1.0f : Vs[P];
-            rank_out[2] = u2f((uint32_t)bkey);
-            rank_out[3] = tag_sh;
-        }
-    }
     if (out) {
         for (int i = tid; i < ncol; i += T) {
             const int jj = jc(i);
@@ -1246,7 +1259,7 @@ __global__ void __launch_bounds__(NT) merge_kernel(const ModelConst mc, StepInpu
                                                               int ctr_inc, uint64_t* __restrict__ dbg,
                                                               uint32_t* __restrict__ flag, uint32_t seq,
                                                               int split_cs, int fence_sys,
-                                                              const uint32_t* __restrict__ gate) {
+                                                              const uint32_t* __restrict__ gate, int levels_up) {
     if (gate && (*gate & ARM_CANCEL)) {  // armed chain that did not fire (Publish::gate)
         if (threadIdx.x == 0 && flag)
             __hip_atomic_store(flag + (split_cs > 0 ? blockIdx.x : 0), seq | ARM_CANCEL, __ATOMIC_RELAXED,
@@ -1256,7 +1269,7 @@ __global__ void __launch_bounds__(NT) merge_kernel(const ModelConst mc, StepInpu
     __shared__ MergeShared<NT> sh;
     extern __shared__ __attribute__((aligned(16))) float dsm[];
     merge_body<NT, STAGE>(mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag,
-                          seq, split_cs, fence_sys, sh, dsm);
+                          seq, split_cs, fence_sys, sh, dsm, false, levels_up);
 }
 
 // In-launch final merge (zero-order four-lane rollout, host steps; launch_rollout with GroupArgs::out): a
@@ -1303,12 +1316,8 @@ __device__ void final_merge(const ModelConst& mc, const StepInput* in, const flo
 }
 
 size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride) {
-    const int cols = mc.P + 1;
-    int G = MERGE_STAGE_THREADS / cols;
-    G = G < 1 ? 1 : (G > ngroups ? ngroups : G);
-    const size_t fl = (size_t)ngroups * rec_stride + (size_t)((ngroups + 3) & ~3) + (size_t)((G * cols + 3) & ~3) +
-                      (size_t)mc.K * mc.P;
-    return (sizeof(MergeShared<256>) + 15) / 16 * 16 + sizeof(float) * fl;
+    return (sizeof(MergeShared<256>) + 15) / 16 * 16 + sizeof(float) * (size_t)ngroups * rec_stride +
+           merge_smem_bytes(ngroups, mc.P, mc.K);
 }
 
 // The zero-order four-lane kernel with the LDS noise stage (ZST: H 10 / 12, no cost terms), MPPI / random
@@ -1324,7 +1333,8 @@ bool final_merge_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride)
     // (the gait-adaptive rollout and the cost terms, which can be switched on later, are checked per launch)
     if (mode != ROLLOUT_QUAD || mc.kind != SRBD_ZERO_ORDER) return false;
     if ((mc.H != 10 && mc.H != 12) || mc.method == SRBD_CEM_MPPI || ngroups < 1) return false;
-    const size_t zst = sizeof(float) * (size_t)(64 * 12 * mc.H > GROUP_LDS_FLOATS ? 64 * 12 * mc.H : GROUP_LDS_FLOATS);
+    const size_t zst =
+        sizeof(float) * (size_t)(64 * (12 * mc.H + 1) > GROUP_LDS_FLOATS ? 64 * (12 * mc.H + 1) : GROUP_LDS_FLOATS);
     return final_merge_lds(mc, ngroups, rec_stride) <= zst;
 }
 
@@ -1348,15 +1358,15 @@ __global__ void __launch_bounds__(NT) merge_xchg_kernel(const ModelConst mc, Ste
                                                                    int rec_stride, const float* __restrict__ noise,
                                                                    XchgArgs x, StepOutput* __restrict__ out,
                                                                    int chain, int ctr_inc, uint32_t* __restrict__ flag,
-                                                                   uint32_t seq) {
+                                                                   uint32_t seq, int levels_up) {
     const int tid = threadIdx.x, T = blockDim.x;
-    const int stride = rec_floats_rank(mc.P, mc.K);
+    const int stride = x.stride;  // one rank's buffer: its exchange-level node records (t_xmax of them)
     const uint32_t epoch = *x.epoch + 1;
     float* mine = x.stage + (size_t)x.rank * stride;
     __shared__ MergeShared<NT> sh;  // both passes (they run one after the other)
     extern __shared__ __attribute__((aligned(16))) float dsm[];
     merge_body<NT, STAGE1>(mc, in, recs, nrec, rec_stride, 0, noise, mine, nullptr, 0, 0, nullptr, nullptr, 0, 0, 1, sh,
-                           dsm);
+                           dsm, false, levels_up);
     __syncthreads();
     // slot parity: epoch & 1.  A peer can run at most one exchange ahead of this rank (it cannot pass
     // its next wait before this rank has published that epoch, i.e. finished copying this one), so
@@ -1407,8 +1417,9 @@ __global__ void __launch_bounds__(NT) merge_xchg_kernel(const ModelConst mc, Ste
                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     }
     __syncthreads();
-    merge_body<NT, false>(mc, in, x.stage, x.world, stride, 1, noise, nullptr, out, chain, ctr_inc, nullptr, flag, seq, 0, 1,
-                          sh, dsm);
+    // pass 2: the ranks' buffers side by side are the exchange level's node list (tree_shape)
+    merge_body<NT, false>(mc, in, x.stage, mc.t_xnodes, rec_floats_rank(mc.P, mc.K), 1, noise, nullptr, out, chain,
+                          ctr_inc, nullptr, flag, seq, 0, 1, sh, dsm);
 }
 
 __global__ void advance_kernel(const ModelConst mc, StepInput* __restrict__ in, const StepOutput* __restrict__ out) {
@@ -1552,15 +1563,11 @@ void launch_rollout(const ModelConst& mc, const StepInput* in, const float* nois
 #undef SRBD_LR
 }
 
-int group_size(int nblocks, int rec_stride, int method) {
-    // measured (round 3, r3e): the group hand-off adds ~2-3 us to the rollout launch and saves 1.7 us of merge
-    // at C2 (157 blocks), 4.8 at N = 65 536 (1024 blocks), 6 at C5 (2048); CEM's group top-K adds ~8 us at C3
-    const bool use = method != SRBD_CEM_MPPI && nblocks >= GROUP_MIN_BLOCKS;
-    int g = use ? (nblocks + GROUP_TARGET - 1) / GROUP_TARGET : 1;
-    const int cap = GROUP_LDS_FLOATS / rec_stride;  // the last arriver's LDS copy of its group's records
-    g = g > cap ? cap : g;
-    g = g > GROUP_MAX ? GROUP_MAX : g;
-    return g < 1 ? 1 : g;
+int group_size(const ModelConst& mc) {
+    // the level-1 fold runs in the launch when the merge would read more than GROUP_MIN_LEAVES leaf records, and
+    // the rank's rows start at a level-1 node (world 1, or an exchange level >= 1)
+    const bool use = mc.nleaf > GROUP_MIN_LEAVES && (mc.t_world == 1 || mc.t_xlevel >= 1);
+    return use ? TREE_FAN : 1;
 }
 
 int rng_grid(const ModelConst& mc) {
@@ -1582,8 +1589,10 @@ void launch_transpose(const float* src, int n, int P, int ldn, float* dst, hipSt
 }
 
 size_t merge_smem_bytes(int nrec, int P, int K) {
-    const int nrec_pad = (nrec + 3) & ~3;
-    return sizeof(float) * ((size_t)nrec_pad + MERGE_THREADS + 4 + (size_t)K * P);  // part: <= T + cols
+    // scale[nrec_pad] | two tree-level value buffers of n1 x (P + 1) | two node-key arrays of n1 | erow[K P]
+    const int nrec_pad = (nrec + 3) & ~3, n1 = (nrec + TREE_FAN - 1) / TREE_FAN;
+    const size_t lvf = ((size_t)n1 * (P + 1) + 3) & ~(size_t)3;
+    return sizeof(float) * ((size_t)nrec_pad + 2 * lvf + 4 * (size_t)n1 + (size_t)K * P);
 }
 
 int merge_split_cols(const ModelConst& mc) {
@@ -1627,23 +1636,23 @@ static void launch_merge_kernel(bool stage, dim3 grid, size_t smem, hipStream_t 
                                 StepInput* in, const float* recs, int nrec, int rec_stride, int rows_in_rec,
                                 const float* noise, float* rank_out, StepOutput* out, int chain, int ctr_inc,
                                 uint64_t* dbg, uint32_t* flag, uint32_t seq, int split_cs,
-                                const uint32_t* gate = nullptr) {
+                                const uint32_t* gate, int levels_up) {
     if (stage) {
         hipLaunchKernelGGL((merge_kernel<MERGE_STAGE_THREADS, true>), grid, dim3(MERGE_STAGE_THREADS), smem, s, mc, in,
                            recs, nrec, rec_stride,
                            rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag, seq, split_cs,
-                           merge_fence_sys(), gate);
+                           merge_fence_sys(), gate, levels_up);
     } else {
         hipLaunchKernelGGL((merge_kernel<MERGE_THREADS, false>), grid, dim3(MERGE_THREADS), smem, s, mc, in, recs, nrec,
                            rec_stride,
                            rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag, seq, split_cs,
-                           merge_fence_sys(), gate);
+                           merge_fence_sys(), gate, levels_up);
     }
 }
 
 int launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                  int rows_in_rec, const float* noise, float* rank_out, StepOutput* out, int chain, hipStream_t s,
-                 uint64_t* dbg, int ctr_inc, Publish pub) {
+                 uint64_t* dbg, int ctr_inc, Publish pub, int levels_up) {
     // step outputs only (no rank record): column-split over merge_blocks() blocks when the column work
     // is large (many records, or CEM's per-column elite statistics); a few hundred MPPI records merge
     // faster in one block (C2: 157 records, 24.9 vs 25.5 us/step)
@@ -1654,7 +1663,7 @@ int launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nre
     const bool stage = !cs && merge_stage_fits(nrec, rec_stride, mc.P, mc.K, &smem);
     if (cs) smem = merge_smem_bytes(nrec, mc.P, mc.K);
     launch_merge_kernel(stage, dim3(nb), smem, s, mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out,
-                        chain, chain ? ctr_inc : 0, dbg, pub.flag, pub.seq, cs, pub.gate);
+                        chain, chain ? ctr_inc : 0, dbg, pub.flag, pub.seq, cs, pub.gate, levels_up);
     return nb;
 }
 
@@ -1696,7 +1705,7 @@ void launch_xchg_probe(const XchgArgs& x, int* ok, hipStream_t s) {
 
 void launch_merge_xchg(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                        const float* noise, const XchgArgs& x, StepOutput* out, int chain, hipStream_t s, int ctr_inc,
-                       Publish pub) {
+                       Publish pub, int levels_up) {
     // the kernel holds both passes' static LDS (two merge_body instantiations), so the staged records
     // get XCHG_LDS_STATIC less dynamic LDS than merge_kernel's
     size_t smem = 0;
@@ -1705,36 +1714,18 @@ void launch_merge_xchg(const ModelConst& mc, StepInput* in, const float* recs, i
         stage = false;
         smem = merge_smem_bytes(nrec, mc.P, mc.K);
     }
-    const size_t smem2 = merge_smem_bytes(x.world, mc.P, mc.K);
+    const size_t smem2 = merge_smem_bytes(mc.t_xnodes, mc.P, mc.K);
     smem = smem > smem2 ? smem : smem2;
     if (stage)
         hipLaunchKernelGGL((merge_xchg_kernel<MERGE_STAGE_THREADS, true>), dim3(1), dim3(MERGE_STAGE_THREADS), smem, s,
-                           mc, in, recs, nrec, rec_stride, noise, x, out, chain, chain ? ctr_inc : 0, pub.flag, pub.seq);
+                           mc, in, recs, nrec, rec_stride, noise, x, out, chain, chain ? ctr_inc : 0, pub.flag, pub.seq,
+                           levels_up);
     else
         hipLaunchKernelGGL((merge_xchg_kernel<MERGE_THREADS, false>), dim3(1), dim3(MERGE_THREADS), smem, s, mc, in,
-                           recs, nrec, rec_stride, noise, x, out, chain, chain ? ctr_inc : 0, pub.flag, pub.seq);
+                           recs, nrec, rec_stride, noise, x, out, chain, chain ? ctr_inc : 0, pub.flag, pub.seq,
+                           levels_up);
 }
 
-
-int merge_partials(int nrec, bool to_outputs) {
-    if (nrec <= (to_outputs ? MERGE_DIRECT_MAX : MERGE_DIRECT_MAX_RECORD)) return 0;
-    int m = (nrec + MERGE_PER_BLOCK - 1) / MERGE_PER_BLOCK;
-    return m > MERGE_MAX_PARTIALS ? MERGE_MAX_PARTIALS : m;
-}
-
-int launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
-                      const float* noise, float* partials, float* rank_out, StepOutput* out, int chain,
-                      hipStream_t s, int ctr_inc, Publish pub) {
-    const int m = merge_partials(nrec, out && !rank_out);
-    if (m == 0) return launch_merge(mc, in, recs, nrec, rec_stride, 0, noise, rank_out, out, chain, s, nullptr, ctr_inc, pub);
-    const int per = (nrec + m - 1) / m;
-    size_t smem = 0;
-    const bool stage = merge_stage_fits(per, rec_stride, mc.P, mc.K, &smem);
-    launch_merge_kernel(stage, dim3(m), smem, s, mc, in, recs, nrec, rec_stride, 0, noise, partials, nullptr, 0, 0,
-                        nullptr, nullptr, 0u, 0, pub.gate);
-    return launch_merge(mc, in, partials, m, rec_floats_rank(mc.P, mc.K), 1, noise, rank_out, out, chain, s, nullptr,
-                        ctr_inc, pub);
-}
 
 // Two byte ranges [0, n0) and [off1, off1 + n1) (16-byte words) of src -> dst, one block.
 __global__ void __launch_bounds__(256) copy16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int n0,

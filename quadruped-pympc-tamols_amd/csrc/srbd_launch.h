@@ -18,24 +18,15 @@ struct RngJob {
 };
 int rng_grid(const ModelConst& mc);
 
-// In-launch second reduction level of the rollout's block records.  Consecutive rollout blocks form
-// groups of `gsize`; every block publishes its record write-through and counts itself in cnt[group];
-// the group's last arriver merges the group's records (in block order) into grecs[group], a record of
-// the same format, so the merge kernel reads ceil(nblocks / gsize) records instead of nblocks.
-// gsize <= 1: no grouping (the merge reads the block records).
-constexpr int GROUP_MAX = 64;      // records one group merges (one wave's lanes hold their keys)
-constexpr int GROUP_TARGET = 32;   // groups per launch the sizing aims at (group_size)
-constexpr int GROUP_LDS_FLOATS = 6144;  // the last arriver stages its group's records in LDS (24 KB)
-constexpr int GROUP_MIN_BLOCKS = 512;   // grouping pays from here on (MPPI / random sampling)
-// Memory-model note: the hand-off (record stores write-through, `s_waitcnt vmcnt(0)`, a block barrier, one
-// relaxed agent-scope fetch_add; the last arriver reads the records with sc1 loads) relies on gfx950's codegen
-// for agent-scope relaxed atomics (sc1 stores / loads that go past the per-CU caches and the per-XCD L2s, which
-// are not coherent with each other, and complete device-wide before vmcnt drops: a group's blocks sit on all
-// eight XCDs), the pattern of MI355X_MICROARCH.md's hand-off table, not on HIP release / acquire ordering.
+// In-launch level-1 fold of the reduction tree (srbd_core.h): the leaf records of TREE_FAN consecutive leaves (a
+// level-1 node) are folded by the node's last arriving block into grecs[node], a record of the same format, so
+// the merge reads ceil(nleaf / TREE_FAN) records instead of nleaf.  gsize == TREE_FAN when on, 1 when off.
+constexpr int GROUP_LDS_FLOATS = 6144;  // the last arriver stages its node's records in LDS (24 KB)
+constexpr int GROUP_MIN_LEAVES = 256;   // the merge reads the leaf records up to this many (C2: 157)
 struct GroupArgs {
-    float* grecs;   // ngroups x rec_stride
-    uint32_t* cnt;  // ngroups arrival counters, zero between launches (each group's last arriver resets its own)
-    int gsize;      // blocks per group
+    float* grecs;   // ngroups x rec_stride (level-1 node records)
+    uint32_t* cnt;  // ngroups arrival counters, zero between launches (each node's last arriver resets its own)
+    int gsize;      // TREE_FAN (the fold runs) or 1
     const uint32_t* gate;  // armed chain (Publish::gate): every block exits at once when the chain did not fire
     // Final merge in the rollout launch (zero-order four-lane kernel, host steps): the last group arriver to
     // finish counts itself in *gdone; the block that completes the count merges the ngroups group records
@@ -55,9 +46,8 @@ bool ks_ok(const ModelConst& mc, int mode);
 size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride);
 bool final_merge_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride);
 int merge_fence_sys();
-// blocks per group for a launch of `nblocks` rollout blocks of `rec_stride`-float records (1: no grouping:
-// CEM, or fewer than GROUP_MIN_BLOCKS blocks); SRBD_GROUP_SIZE overrides (1 disables grouping)
-int group_size(int nblocks, int rec_stride, int method);
+// TREE_FAN when the rollout launch folds level 1 of the tree, else 1 (group_size)
+int group_size(const ModelConst& mc);
 
 // rollout forms: one thread per sample (block = `threads` samples) or four lanes per sample (block = 256
 // threads = 64 samples)
@@ -100,23 +90,13 @@ constexpr int MERGE_SPLIT_MIN_RECS = 256;
 int merge_split_cols(const ModelConst& mc);
 void merge_prepare();  // once per context: the LDS-staged merge's dynamic LDS limit
 int merge_blocks(const ModelConst& mc);
+// The tree's levels above the `nrec` input records (leaves or level-1 nodes, in global order): to the root and the
+// step outputs, or (rank_out) `levels_up` levels up to this rank's exchange-level nodes, one rank record each.
 int launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                   int rows_in_rec, const float* noise, float* rank_out, StepOutput* out, int chain, hipStream_t s,
-                  uint64_t* dbg = nullptr, int ctr_inc = 1, Publish pub = {nullptr, 0, nullptr});
-// Two-level merge when there are many block records: merge_partials(nrec) first-level blocks each
-// reduce a slice of the records (spreading the record reads over CUs) into rank-format partials,
-// then the partials are merged.
-// Defaults (measured, scripts/kernel_sweep.py); SRBD_MERGE_DIRECT_MAX / SRBD_MERGE_PER_BLOCK override.
-// Up to 1024 records the column-split merge reads them directly (N = 65 536 quad: CEM cubic H16 90.6 ->
-// 79.0 us/step, MPPI 53.7 -> 52.7); at 4096 the tree is faster (130.8 vs 158.5 us).
-constexpr int MERGE_DIRECT_MAX = 1024;
-constexpr int MERGE_DIRECT_MAX_RECORD = 256;  // merging into a rank record: one block, no split
-constexpr int MERGE_PER_BLOCK = 32;
-constexpr int MERGE_MAX_PARTIALS = 64;
-// to_outputs: the merge produces step outputs (column-split final level), else a rank record.
-int merge_partials(int nrec, bool to_outputs);
+                  uint64_t* dbg = nullptr, int ctr_inc = 1, Publish pub = {nullptr, 0, nullptr}, int levels_up = 0);
 // xGMI exchange of rank records (merge_xchg_kernel).  mailbox: this rank's 2 x W slots of one rank
-// record each (half epoch & 1, slot r of a half written by rank r); flags: W epochs (word r written
+// buffer each (its exchange-level node records; half epoch & 1, slot r of a half written by rank r); flags: W epochs (word r written
 // by rank r; waits accept >= epoch); peer_*: every rank's mailbox / flags as
 // this GPU addresses them (IPC-mapped; entry `rank` is the local one).  epoch: this rank's exchange
 // counter in device memory, advanced by every exchange kernel (so the chain can be a replayed graph).
@@ -135,10 +115,7 @@ struct XchgArgs {
 void launch_xchg_probe(const XchgArgs& x, int* ok, hipStream_t s);
 void launch_merge_xchg(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
                        const float* noise, const XchgArgs& x, StepOutput* out, int chain, hipStream_t s, int ctr_inc,
-                       Publish pub);
-int launch_merge_tree(const ModelConst& mc, StepInput* in, const float* recs, int nrec, int rec_stride,
-                       const float* noise, float* partials, float* rank_out, StepOutput* out, int chain,
-                       hipStream_t s, int ctr_inc = 1, Publish pub = {nullptr, 0, nullptr});
+                       Publish pub, int levels_up);
 void launch_advance(const ModelConst& mc, StepInput* in, const StepOutput* out, hipStream_t s);
 void launch_empty(hipStream_t s);  // measurement: the event floor
 // src -> dst bytes [0, bytes0) and [off1, off1 + bytes1); all multiples of 16

@@ -40,9 +40,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
                   ((int)gridDim.x - nroll) * (int)blockDim.x);
         return;
     }
-    __shared__ float e_sh[256];
-    __shared__ uint64_t red[4];
-    __shared__ uint64_t elite_sh[MAXK];
 
     constexpr bool CT = HT > 0 && (KIND == SRBD_ZERO_ORDER || ST > 0);  // compile-time shape
     const int H = CT ? HT : mc.H;
@@ -155,7 +152,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
     if (tid == 0) recs[blockIdx.x] = cost;
     return;
 #endif
-    block_epilogue<CEMT>(mc, in, T, tid, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh, 0.0f, grp, nroll);
+    block_epilogue<CEMT>(mc, in, T, tid, valid, cost, noise, recs, rec_stride, 0.0f, grp, nroll);
 }
 
 template <int KIND>
@@ -169,9 +166,6 @@ __global__ void __launch_bounds__(256) rollout_ga_kernel(const ModelConst mc, co
                   ((int)gridDim.x - nroll) * (int)blockDim.x);
         return;
     }
-    __shared__ float e_sh[256];
-    __shared__ uint64_t red[4];
-    __shared__ uint64_t elite_sh[MAXK];
     const int H = mc.H, S = mc.S, PL = mc.PL;
     const int tid = threadIdx.x, T = blockDim.x;
     const int k = blockIdx.x * T + tid;  // rows >= n_local are padding (readable zeros)
@@ -256,7 +250,7 @@ __global__ void __launch_bounds__(256) rollout_ga_kernel(const ModelConst mc, co
     cost = cost + (df * 100.0f) * df;  // GA:500
     if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
     if (valid && costs) costs[k] = cost;
-    block_epilogue<false>(mc, in, T, tid, valid, cost, noise, recs, rec_stride, e_sh, red, elite_sh, f, grp, nroll);
+    block_epilogue<false>(mc, in, T, tid, valid, cost, noise, recs, rec_stride, f, grp, nroll);
 }
 
 // ------------------------------------------------------------------ launchers (srbd_launch.h)

@@ -80,6 +80,8 @@ SIGNATURES = {
     "srbd_armed_refired": (_I, [_P, C.POINTER(C.c_int64)]),
     "srbd_debug_arm_delay": (_I, [_P, C.c_uint32]),
     "srbd_record_floats": (_I, [_P]),
+    "srbd_record_floats_host": (_I, [C.POINTER(SrbdConfig)]),
+    "srbd_shard_rows": (_I, [C.c_int64, _I, _I, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "srbd_step_local": (_I, [_P, _FP, _FP, _FP, _I, _FP, _FP, _FP, C.c_uint64, C.c_uint64, _P]),
     "srbd_step_finish": (_I, [_P, _P, _I, _FP, _FP, C.POINTER(SrbdResult), _FP]),
     "srbd_finish_host": (_I, [C.POINTER(SrbdConfig), _FP, _I, _FP, _FP, _I, _FP, _FP, C.POINTER(SrbdResult)]),
@@ -305,16 +307,34 @@ def num_params(cfg: SrbdConfig) -> int:
 REC_HDR = 4  # srbd_core.h: [m, s, best row bits, pad]
 
 
-def record_floats_host(cfg: SrbdConfig) -> int:
-    """Floats per rank record (== srbd_record_floats of a context of this configuration)."""
+def node_record_floats(cfg: SrbdConfig) -> int:
+    """Floats per node record of the reduction tree (srbd_core.h rec_floats_rank)."""
     K = cfg.num_elite if cfg.method == CEM_MPPI else 1
     P = num_params(cfg)
     return (REC_HDR + P + 2 * K + K * P + 3) // 4 * 4  # padded to 16-byte words (srbd_core.h rec_pad4)
 
 
+def record_floats_host(cfg: SrbdConfig) -> int:
+    """Floats per rank buffer (== srbd_record_floats of a context of this configuration)."""
+    n = lib.srbd_record_floats_host(C.byref(cfg))
+    if n < 0:
+        raise ValueError(f"srbd_record_floats_host failed ({n}): {last_error(None)}")
+    return n
+
+
+def shard_rows(n_total: int, rank: int, world: int) -> tuple[int, int]:
+    """(first row, row count) of `rank` of `world`: whole nodes of the reduction tree (srbd_shard_rows)."""
+    a, n = C.c_int64(), C.c_int64()
+    rc = lib.srbd_shard_rows(int(n_total), int(rank), int(world), C.byref(a), C.byref(n))
+    if rc != OK:
+        raise ValueError(f"srbd_shard_rows({n_total}, {rank}, {world}) failed ({rc}): {last_error(None)}")
+    return a.value, n.value
+
+
 def make_record_host(cfg: SrbdConfig, rank: int, world: int, costs: np.ndarray, noise_rows: np.ndarray) -> np.ndarray:
-    """srbd_make_record_host: one rank's partial record from its saturated costs and noise rows."""
-    rec = np.zeros(record_floats_host(cfg), np.float32)
+    """srbd_make_record_host: one rank's buffer (its exchange-level node records) from its saturated costs and
+    noise rows (the rows of shard_rows(N, rank, world))."""
+    rec = np.zeros(record_floats_host(_with_shard(cfg, rank, world)), np.float32)
     costs = np.ascontiguousarray(costs, np.float32)
     noise_rows = np.ascontiguousarray(noise_rows, np.float32)
     check(lib.srbd_make_record_host(C.byref(cfg), int(rank), int(world), fptr(costs), fptr(noise_rows), fptr(rec)),
@@ -322,10 +342,22 @@ def make_record_host(cfg: SrbdConfig, rank: int, world: int, costs: np.ndarray, 
     return rec
 
 
-def finish_host(cfg: SrbdConfig, records: np.ndarray, state, contact, best, sigma=None):
-    """srbd_finish_host: merge gathered rank records (rank order) on the host."""
+def _with_shard(cfg: SrbdConfig, rank: int, world: int) -> SrbdConfig:
+    c = SrbdConfig.from_buffer_copy(cfg)
+    c.rank, c.world_size = int(rank), int(world)
+    return c
+
+
+def finish_host(cfg: SrbdConfig, records: np.ndarray, state, contact, best, sigma=None, world=None):
+    """srbd_finish_host: merge gathered rank buffers (rank order) on the host.  world: the number of buffers
+    (default: the world size whose buffers make up `records`)."""
     records = np.ascontiguousarray(records, np.float32)
-    nrec = records.size // record_floats_host(cfg)
+    if world is None:
+        world = next((w for w in range(1, records.size + 1)
+                      if w * record_floats_host(_with_shard(cfg, 0, w)) == records.size), None)
+        if world is None:
+            raise ValueError("records are not a whole number of rank buffers")
+    nrec = int(world)
     state = np.ascontiguousarray(state, np.float32).reshape(24)
     contact = np.ascontiguousarray(contact, np.float32)
     best = np.array(best, np.float32).reshape(-1).copy()
@@ -348,9 +380,7 @@ class Context:
         self.cfg = cfg
         self.P = num_params(cfg)
         self.N = cfg.num_samples
-        ws = max(1, cfg.world_size)
-        self.row0 = cfg.rank * self.N // ws
-        self.n_local = (cfg.rank + 1) * self.N // ws - self.row0
+        self.row0, self.n_local = shard_rows(self.N, cfg.rank, max(1, cfg.world_size))
         h = _P()
         rc = lib.srbd_create(C.byref(cfg), C.byref(h))
         if rc != OK:

@@ -47,9 +47,8 @@ class RecordExchange:
 
 
 def shard_rows(n_total: int, rank: int, world: int) -> tuple[int, int]:
-    """(first row, row count) of `rank` (matches the library's build_model)."""
-    a = rank * n_total // world
-    return a, (rank + 1) * n_total // world - a
+    """(first row, row count) of `rank`: whole nodes of the reduction tree (srbd_shard_rows)."""
+    return _lib.shard_rows(n_total, rank, world)
 
 
 def torch_rccl_path() -> str:

@@ -128,18 +128,21 @@ def oracle_case(method, N, seed, key="c2", par="zero_order", H=12):
     return o, cfg, s, c, best, sigma, noise, costs
 
 
+def _host_merge(cfg, world, costs, noise, s, c, best, sigma=None):
+    recs = []
+    for rank in range(world):
+        a, n = _lib.shard_rows(cfg.num_samples, rank, world)
+        recs.append(_lib.make_record_host(cfg, rank, world, costs[a:a + n], noise[a:a + n]))
+    return _lib.finish_host(cfg, np.concatenate(recs), s, c, best, sigma)
+
+
 @pytest.mark.parametrize("method", ["mppi", "cem_mppi", "random_sampling"])
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 def test_host_records_merge_matches_oracle(method, world):
     N = 997
     o, cfg, s, c, best, sigma, noise, costs = oracle_case(method, N, seed=world)
     ref = o.reduce(s, c, best, noise, costs)
-    recs = []
-    for rank in range(world):
-        a, b = rank * N // world, (rank + 1) * N // world
-        recs.append(_lib.make_record_host(cfg, rank, world, costs[a:b], noise[a:b]))
-    nb, ns, res = _lib.finish_host(cfg, np.concatenate(recs), s, c, best,
-                                   sigma if method == "cem_mppi" else None)
+    nb, ns, res = _host_merge(cfg, world, costs, noise, s, c, best, sigma if method == "cem_mppi" else None)
     assert res.best_index == ref["best_index"]
     assert f32(res.best_cost) == ref["best_cost"]
     np.testing.assert_allclose(nb, ref["best"], rtol=1e-5, atol=1e-5)
@@ -151,14 +154,28 @@ def test_host_records_merge_matches_oracle(method, world):
 
 def test_host_merge_ties_pick_first_row():
     """nanargmin semantics across shards: equal costs -> lowest global row wins."""
-    N, world = 60, 3
+    N, world = 300, 3
     o, cfg, s, c, best, sigma, noise, costs = oracle_case("mppi", N, seed=7)
     costs = np.full(N, 5.0, f32)
-    costs[[13, 41, 59]] = 1.0
-    recs = [_lib.make_record_host(cfg, r, world, costs[r * 20:(r + 1) * 20], noise[r * 20:(r + 1) * 20])
-            for r in range(world)]
-    _, _, res = _lib.finish_host(cfg, np.concatenate(recs), s, c, best)
+    costs[[13, 141, 299]] = 1.0  # one per shard
+    _, _, res = _host_merge(cfg, world, costs, noise, s, c, best)
     assert res.best_index == 13
+
+
+@pytest.mark.parametrize("method", ["mppi", "cem_mppi", "random_sampling"])
+def test_host_merge_is_world_invariant(method):
+    """The fixed reduction tree: every world size merges to the same bits (up to 8 ranks; N spans 3 levels)."""
+    N = 70001
+    o, cfg, s, c, best, sigma, noise, costs = oracle_case(method, N, seed=11)
+    sg = sigma if method == "cem_mppi" else None
+    b1, s1, r1 = _host_merge(cfg, 1, costs, noise, s, c, best, sg)
+    for world in (2, 3, 5, 8):
+        bw, sw, rw = _host_merge(cfg, world, costs, noise, s, c, best, sg)
+        np.testing.assert_array_equal(bw, b1)
+        if sg is not None:
+            np.testing.assert_array_equal(sw, s1)
+        np.testing.assert_array_equal(np.array(rw.grf), np.array(r1.grf))
+        assert rw.best_index == r1.best_index and rw.best_cost == r1.best_cost
 
 
 def test_host_merge_saturated_costs():

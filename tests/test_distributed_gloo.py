@@ -83,10 +83,15 @@ def test_sharded_merge_gloo(tmp_path, world, method, N):
 def test_shard_rows_cover_problem():
     from quadruped_pympc_amd.sharded import shard_rows
 
-    for N in (1, 7, 10000, 65537):
+    for N in (1, 7, 300, 10000, 65537, 524288):
         for W in (1, 2, 3, 8):
+            if W > (N + 63) // 64:  # fewer 64-row leaves than ranks: no whole-node shard for every rank
+                with pytest.raises(ValueError):
+                    shard_rows(N, W - 1, W)
+                continue
             spans = [shard_rows(N, r, W) for r in range(W)]
             assert spans[0][0] == 0
             assert sum(n for _, n in spans) == N
             for (a, n), (b, _) in zip(spans, spans[1:]):
                 assert a + n == b
+                assert a % 64 == 0 and n > 0  # whole leaves (tree nodes)

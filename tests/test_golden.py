@@ -93,8 +93,9 @@ def test_host_merge_reproduces_fixture(path):
                            parametrization=str(g["parametrization"]), mass=float(g["mass"]), inertia=g["inertia"],
                            dts=g["dts"])
     world = 2
-    recs = [_lib.make_record_host(cfg, r, world, g["costs"][r * N // world:(r + 1) * N // world],
-                                  g["noise"][r * N // world:(r + 1) * N // world]) for r in range(world)]
+    spans = [_lib.shard_rows(N, r, world) for r in range(world)]
+    recs = [_lib.make_record_host(cfg, r, world, g["costs"][a:a + n], g["noise"][a:a + n])
+            for r, (a, n) in enumerate(spans)]
     sigma = g["sigma_in"] if g["sigma_in"].size else None
     best, ns, res = _lib.finish_host(cfg, np.concatenate(recs), g["state"], g["contact"], g["best_in"], sigma)
     assert res.best_index == int(g["best_index"])

@@ -47,10 +47,10 @@ def test_sharded_driver_world1_matches_step(transport):
             b1, s1, r1 = mpc.step(case["state"], case["ref"], case["contact"], case["best"], sigma=case["sigma"],
                                   noise_local=case["noise"])
             assert r1.best_index == r0.best_index
-            np.testing.assert_allclose(b1, b0, rtol=1e-5, atol=1e-5)
-            np.testing.assert_allclose(np.array(r1.grf), np.array(r0.grf), rtol=1e-5, atol=1e-3)
+            np.testing.assert_array_equal(b1, b0)
+            np.testing.assert_array_equal(np.array(r1.grf), np.array(r0.grf))
             if method == "cem_mppi":
-                np.testing.assert_allclose(s1, s0, rtol=1e-5, atol=1e-6)
+                np.testing.assert_array_equal(s1, s0)
             # device-resident chain on the torch stream
             b2, _, _ = mpc.step(case["state"], case["ref"], case["contact"], b1, sigma=s1, seed=42, counter=5)
             assert mpc.device_steps(4) > 0
@@ -60,7 +60,7 @@ def test_sharded_driver_world1_matches_step(transport):
             b3, s3, r3 = mpc.step(case["state"], case["ref"], case["contact"], case["best"], sigma=case["sigma"],
                                   noise_local=case["noise"])
             assert r3.best_index == r0.best_index
-            np.testing.assert_allclose(b3, b0, rtol=1e-5, atol=1e-5)
+            np.testing.assert_array_equal(b3, b0)
             mpc.close()
     finally:
         dist.destroy_process_group()
