@@ -63,6 +63,9 @@ def parse_args(argv=None):
     ap.add_argument("--rng", default="philox", choices=["philox", "jax", "jax_legacy"],
                     help="device noise stream of the timed steps (srbd_set_rng): this library's Philox, or the "
                          "reference's jax.random stream (threefry, partitionable / legacy counter layout)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the sharded step (srbd_step_sharded, xGMI exchange) even on one GPU (world 1)")
+    ap.add_argument("--num-samples", type=int, default=0, help="override the workload's num_samples")
     ap.add_argument("--extras", type=int, default=200,
                     help="steps of the supplementary interface / TAMOLS latency probes (0: skip)")
     return ap.parse_args(argv)
@@ -430,15 +433,16 @@ def bench_single(_lib, w, args):
                 transport=None, py_lat=py, armed=armed, other=other, arm_stats=(served, cancelled))
 
 
-def bench_multi(_lib, w, args, rank, world, local_rank, scaling):
+def bench_multi(_lib, w, args, rank, world, local_rank, scaling, steps=None, device_steps=None):
+    """One sharded workload on this rank's GPU (the process group is up); steps / device_steps override args."""
     import numpy as np
     import torch
     import torch.distributed as dist
 
     from quadruped_pympc_amd.sharded import ShardedSamplingMPC
 
-    torch.cuda.set_device(local_rank)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    steps = args.steps if steps is None else steps
+    device_steps = args.device_steps if device_steps is None else device_steps
     n_total = w.num_samples if scaling == "strong" else w.num_samples * world
     mpc = ShardedSamplingMPC(make_cfg(_lib, w, n_total, rank, world, local_rank), rank, world, local_rank,
                              transport=args.transport, rng=args.rng)
@@ -458,7 +462,7 @@ def bench_multi(_lib, w, args, rank, world, local_rank, scaling):
     best = run_steps(step, ins, best, k, max(1, args.warmup))
     k += max(1, args.warmup)
     lat = []
-    if args.steps < args.latency_steps:
+    if steps < args.latency_steps:
         dist.barrier()
         best = run_steps(step, ins, best, k, args.latency_steps, lat)
         k += args.latency_steps
@@ -470,10 +474,10 @@ def bench_multi(_lib, w, args, rank, world, local_rank, scaling):
     timed = []
     t0 = time.perf_counter()
     if c_timed:  # rollout -> xGMI record exchange -> merge, srbd_step_sharded from C
-        t_us, best, state["sigma"] = mpc.ctx.bench_host_steps(*arrs, best, state["sigma"], keys.at(k), k, args.steps)
+        t_us, best, state["sigma"] = mpc.ctx.bench_host_steps(*arrs, best, state["sigma"], keys.at(k), k, steps)
         timed = list(t_us * 1e-6)
     else:
-        best = run_steps(step, ins, best, k, args.steps, timed)
+        best = run_steps(step, ins, best, k, steps, timed)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     dist.barrier()
@@ -483,25 +487,37 @@ def bench_multi(_lib, w, args, rank, world, local_rank, scaling):
     if not lat:
         lat = timed
     dev = None
-    if args.device_steps > 0:
+    if device_steps > 0:
         mpc.device_steps(max(1, args.warmup))
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        mpc.device_steps(args.device_steps)
+        mpc.device_steps(device_steps)
         torch.cuda.synchronize()
         dwall = time.perf_counter() - t0
         t = torch.tensor([dwall], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dwall = float(t.item())
-        dev = {"value": round(n_total * args.device_steps / dwall, 1),
-               "ms_per_step": round(1e3 * dwall / args.device_steps, 5), "steps": args.device_steps}
+        dev = {"value": round(n_total * device_steps / dwall, 1),
+               "ms_per_step": round(1e3 * dwall / device_steps, 5), "steps": device_steps}
     n_local = mpc.ctx.n_local
     kern = mpc.ctx.time_kernels(100)
     transport = mpc.transport
     mpc.close()
-    dist.destroy_process_group()
-    return dict(n_total=n_total, n_local=n_local, wall=wall, lat=lat, kern=kern, dev=dev, transport=transport)
+    return dict(n_total=n_total, n_local=n_local, wall=wall, lat=lat, kern=kern, dev=dev, transport=transport,
+                steps=steps)
+
+
+def multi_line(w, out, scaling):
+    """The per-workload summary of a sharded run (the supplementary C5 lines at N > 1)."""
+    import numpy as np
+
+    lat = np.array(out["lat"]) * 1e3
+    return {"value": round(out["n_total"] * out["steps"] / out["wall"], 1), "unit": "rollouts/s",
+            "scaling": scaling, "num_samples": out["n_total"], "rows_per_gpu": out["n_local"],
+            "ms_per_step": round(1e3 * out["wall"] / out["steps"], 5), "steps": out["steps"],
+            "p50_step_ms": round(float(np.percentile(lat, 50)), 4), "transport": out["transport"],
+            "kernels_us": {k: round(v, 3) for k, v in out["kern"].items()}}
 
 
 def main(argv=None):
@@ -521,13 +537,37 @@ def main(argv=None):
     from quadruped_pympc_amd.synthetic import CONFIGS
 
     w = CONFIGS[args.config]
+    if args.num_samples > 0:
+        import dataclasses
+
+        w = dataclasses.replace(w, num_samples=args.num_samples, name=f"{w.name}_n{args.num_samples}")
     scaling = args.scaling or ("strong" if args.config == "c5" else "weak")
-    if world > 1:
+    extra = {}
+    if world > 1 or args.sharded:
+        if "WORLD_SIZE" not in os.environ:  # --sharded on one GPU without a launcher: a group of one
+            with socket.socket() as s_:
+                s_.bind(("127.0.0.1", 0))
+                os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s_.getsockname()[1]), RANK="0",
+                                  WORLD_SIZE="1", LOCAL_RANK="0")
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         out = bench_multi(_lib, w, args, rank, world, local_rank, scaling)
+        if world > 1 and args.targets > 0 and args.config == "c2":
+            # BASELINE configs[4] beside the headline: C5's 524 288 rows split over the N GPUs (strong; the
+            # one-GPU line's c5_1gpu is its denominator) and 524 288 rows per GPU (weak)
+            c5 = CONFIGS["c5"]
+            for sc in ("strong", "weak"):
+                o = bench_multi(_lib, c5, args, rank, world, local_rank, sc, steps=args.targets, device_steps=0)
+                extra[f"c5_{sc}"] = multi_line(c5, o, sc)
+        dist.destroy_process_group()
     else:
         out = bench_single(_lib, w, args)
     if rank != 0:
         return
+    single = world == 1 and not args.sharded
     lat = np.array(out["lat"]) * 1e3
     line = {
         "metric": METRIC,
@@ -551,27 +591,28 @@ def main(argv=None):
                    "horizon": w.horizon, "method": w.method, "parametrization": w.parametrization,
                    "robot": w.robot, "gait": w.gait,
                    "parallelism": (f"rows sharded over {world} GPUs ({scaling} scaling), record exchange: "
-                                   f"{out['transport']}") if world > 1 else "single GPU"},
+                                   f"{out['transport']}") if not single else "single GPU"},
         "step": (("armed " if out.get("armed") else "")
                  + "host-to-host srbd_step, timed around each call in C (srbd_bench_host_steps; state/ref/contact/"
-                 "params in, GRFs/pred/params out; noise device-resident)") if world == 1 else
+                 "params in, GRFs/pred/params out; noise device-resident)") if single else
                 (f"host-to-host srbd_step_sharded ({out['transport']} record exchange), "
                  + ("timed in C (srbd_bench_host_steps)" if out["transport"] in ("xgmi", "rccl")
                     else "through the Python binding") + ", max over ranks"),
         "device_chain": out["dev"],
         **({("unarmed_step" if out["armed"] else "armed_step"): out["other"],
-            "armed_served_cancelled": list(out["arm_stats"])} if world == 1 else {}),
+            "armed_served_cancelled": list(out["arm_stats"])} if single else {}),
         "python_step": ({"p50_ms": round(float(np.percentile(np.array(out["py_lat"]) * 1e3, 50)), 4),
                          "steps": len(out["py_lat"]), "path": "Context.step (ctypes) -> srbd_step"}
                         if out.get("py_lat") else None),
         "kernels_us": {k: round(v, 3) for k, v in out["kern"].items()},
         "roofline": roofline(w, out["n_local"], out["kern"], pmc_traffic(w.name)),
+        **extra,
     }
-    if world == 1 and not args.no_cpu_baseline:
+    if single and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
     else:
         line["cpu_baseline"] = None
-    if world == 1 and args.targets > 0 and args.config == "c2":  # the north-star shape, C3 and C5 beside the headline
+    if single and args.targets > 0 and args.config == "c2":  # the north-star shape, C3 and C5 beside the headline
         line["north_star_65536"] = supplementary(_lib, "ns", args.targets, args.rng)
         line["c3"] = supplementary(_lib, "c3", args.targets, args.rng)
         # C5's 524 288 rows on one GPU: the denominator of the driver's C5 strong-scaling ratio
@@ -579,7 +620,7 @@ def main(argv=None):
         # the headline shape on the other noise stream (Philox <-> the reference's jax.random stream)
         other = "jax" if args.rng == "philox" else "philox"
         line["c2_rng_" + other] = supplementary(_lib, "c2", args.targets, other)
-    if world == 1 and args.extras and args.config in ("c2", "c4"):  # the callers either side of the path
+    if single and args.extras and args.config in ("c2", "c4"):  # the callers either side of the path
         line["interface_step"] = interface_latency(w, args.extras)
         line["interface_step_armed"] = interface_latency(w, args.extras, armed=True)
         line["tamols_c4"] = tamols_latency(args.extras)

@@ -86,6 +86,7 @@ struct srbd_ctx {
     float* xg_base = nullptr;
     std::vector<void*> xg_opened;
     XchgArgs xa{};
+    XchgArgs* d_xa = nullptr;  // device copy (the rollout launch's in-launch exchange, GroupArgs::xa)
     int xg_world = 0;
     int* xg_err = nullptr;
     float* xg_stage = nullptr;
@@ -1347,7 +1348,9 @@ static void comm_release(srbd_ctx* c) {
     (void)hipFree(c->xg_base);
     (void)hipFree(c->xg_err);
     (void)hipFree(c->xg_stage);
+    (void)hipFree(c->d_xa);
     c->xg_stage = nullptr;
+    c->d_xa = nullptr;
     xg_drop_graphs(c);
     c->xg_base = nullptr;
     c->xg_err = nullptr;
@@ -1405,6 +1408,7 @@ extern "C" int srbd_xgmi_export(srbd_ctx* c, uint8_t* handle_out) {
         HIP_TRY(c, hipMalloc((void**)&c->xg_err, 2 * sizeof(int)));
         HIP_TRY(c, hipMemset(c->xg_err, 0, 2 * sizeof(int)));
         HIP_TRY(c, hipMalloc((void**)&c->xg_stage, sizeof(float) * (size_t)world * c->rrec_stride));
+        HIP_TRY(c, hipMalloc((void**)&c->d_xa, sizeof(XchgArgs)));
     }
     hipIpcMemHandle_t h;
     HIP_TRY(c, hipIpcGetMemHandle(&h, c->xg_base));
@@ -1435,6 +1439,7 @@ static int xg_table(srbd_ctx* c, int world, float* const* bases) {
     c->xa.rank = c->cfg.rank;
     c->xa.world = world;
     c->xa.stride = c->rrec_stride;
+    HIP_TRY(c, hipMemcpy(c->d_xa, &c->xa, sizeof(XchgArgs), hipMemcpyHostToDevice));
     c->xg_world = world;
     return SRBD_OK;
 }
@@ -1515,6 +1520,20 @@ static void enqueue_xchg_step(srbd_ctx* c, int buf, StepOutput* out, int chain, 
     const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1};
     GroupArgs grp = grp_of(c);
     grp.ksi = ksi;  // the step input as the rollout's kernel argument (its block 0 writes the device copy)
+    if (c->final_merge && !mc.ga && !mc.cost_on && out && !chain && pub.flag) {
+        // host step: the rollout launch's final merger folds this rank's buffer, exchanges and merges (one launch)
+        grp.out = out;
+        grp.flag = pub.flag;
+        grp.seq = pub.seq;
+        grp.gdone = c->d_gdone;
+        grp.ngroups = c->ngroups;
+        grp.fence_sys = merge_fence_sys();
+        grp.xa = c->d_xa;
+        grp.levels_up = levels_up(c);
+        launch_rollout(mc, c->d_in, c->d_noise[buf], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
+                       c->stream, fuse_next ? &next : nullptr, grp);
+        return;
+    }
     launch_rollout(mc, c->d_in, c->d_noise[buf], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
                    c->stream, fuse_next ? &next : nullptr, grp);
     launch_merge_xchg(mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, c->d_noise[buf], c->xa, out, chain,

@@ -1272,72 +1272,6 @@ __global__ void __launch_bounds__(NT) merge_kernel(const ModelConst mc, StepInpu
                           seq, split_cs, fence_sys, sh, dsm, false, levels_up);
 }
 
-// In-launch final merge (zero-order four-lane rollout, host steps; launch_rollout with GroupArgs::out): a
-// group's last arriver, its group record stored write-through, counts itself in *gdone; the block that
-// completes the count (every group record is then in memory) copies the ngroups records into LDS with sc1
-// loads and runs the single-block merge on them -- merge_body<NT, STAGE> with the record groups of the
-// 512-thread kernel, so the outputs are merge_kernel's bit for bit -- writing the step outputs and
-// publishing `seq` (and resets the count for the next launch).  The merge's LDS is carved from the rollout's
-// noise stage, dead by then (final_merge_lds).  Saves the merge launch and its record staging: N = 65 536
-// (see DESIGN.md).
-template <int NT>
-__device__ void final_merge(const ModelConst& mc, const StepInput* in, const float* noise, int rec_stride,
-                            const GroupArgs& grp, float* lds) {
-    __shared__ int fin;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's group record stores have completed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t old = __hip_atomic_fetch_add(grp.gdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        fin = old == (uint32_t)(grp.ngroups - 1);
-    }
-    __syncthreads();
-    if (!fin) return;
-    if (threadIdx.x == 0) __hip_atomic_store(grp.gdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    MergeShared<NT>& sh = *reinterpret_cast<MergeShared<NT>*>(lds);
-    float* smem = lds + (sizeof(MergeShared<NT>) + 15) / 16 * 4;  // 16-byte aligned
-    const int n = grp.ngroups * rec_stride;
-    constexpr int U = 16;  // sc1 loads in flight per thread (other CUs wrote the records)
-    for (int i0 = 0; i0 < n; i0 += U * NT) {
-        float v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = i0 + u * NT + (int)threadIdx.x;
-            v[u] = i < n ? ld_rec(grp.grecs + i) : 0.0f;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = i0 + u * NT + (int)threadIdx.x;
-            if (i < n) smem[i] = v[u];
-        }
-    }
-    __syncthreads();
-    merge_body<NT, true>(mc, const_cast<StepInput*>(in), smem, grp.ngroups, rec_stride, 0, noise, nullptr, grp.out, 0,
-                         0, nullptr, grp.flag, grp.seq, 0, grp.fence_sys, sh, smem, true);
-}
-
-size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride) {
-    return (sizeof(MergeShared<256>) + 15) / 16 * 16 + sizeof(float) * (size_t)ngroups * rec_stride +
-           merge_smem_bytes(ngroups, mc.P, mc.K);
-}
-
-// The zero-order four-lane kernel with the LDS noise stage (ZST: H 10 / 12, no cost terms), MPPI / random
-// sampling, grouped records, and the merge's LDS inside the stage (64 x 12 H floats).
-// The step input as a kernel argument (StepInputK): the zero-order four-lane kernel with the LDS noise stage,
-// MPPI / random sampling (no sigma in the argument), P <= KSI_MAXP; SRBD_KS=0 disables (read per context).
-bool ks_ok(const ModelConst& mc, int mode) {
-    if ((mode != ROLLOUT_QUAD && mode != ROLLOUT_THREAD) || mc.kind != SRBD_ZERO_ORDER) return false;
-    return (mc.H == 10 || mc.H == 12) && mc.method != SRBD_CEM_MPPI && mc.P <= KSI_MAXP;
-}
-
-bool final_merge_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride) {
-    // (the gait-adaptive rollout and the cost terms, which can be switched on later, are checked per launch)
-    if (mode != ROLLOUT_QUAD || mc.kind != SRBD_ZERO_ORDER) return false;
-    if ((mc.H != 10 && mc.H != 12) || mc.method == SRBD_CEM_MPPI || ngroups < 1) return false;
-    const size_t zst =
-        sizeof(float) * (size_t)(64 * (12 * mc.H + 1) > GROUP_LDS_FLOATS ? 64 * (12 * mc.H + 1) : GROUP_LDS_FLOATS);
-    return final_merge_lds(mc, ngroups, rec_stride) <= zst;
-}
-
 // Sharded step without a collective launch (xGMI exchange).
 //  1. pass 1 merges this rank's block records into its rank record (a cached stage slot);
 //  2. the record goes to slot `rank` of every peer's mailbox as system-scope (sc0 sc1, write-through)
@@ -1352,21 +1286,21 @@ bool final_merge_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride)
 // step; this form measures within noise of no release at all (scripts/sharded_probe.py).
 // NT / STAGE1: pass 1 as the single-rank merge runs it -- the LDS-staged 512-thread body when this
 // rank's block records fit (C2: 157), else the 1024-thread direct body; pass 2 (W records) direct.
+// xchg_body: the whole sequence for one block (merge_xchg_kernel; the rollout launch's final merger, final_merge,
+// with prestaged level-1 records).
 template <int NT, bool STAGE1>
-__global__ void __launch_bounds__(NT) merge_xchg_kernel(const ModelConst mc, StepInput* __restrict__ in,
-                                                                   const float* __restrict__ recs, int nrec,
-                                                                   int rec_stride, const float* __restrict__ noise,
-                                                                   XchgArgs x, StepOutput* __restrict__ out,
-                                                                   int chain, int ctr_inc, uint32_t* __restrict__ flag,
-                                                                   uint32_t seq, int levels_up) {
-    const int tid = threadIdx.x, T = blockDim.x;
+__device__ __forceinline__ void xchg_body(const ModelConst& mc, StepInput* __restrict__ in,
+                                          const float* __restrict__ recs, int nrec, int rec_stride,
+                                          const float* __restrict__ noise, const XchgArgs& x,
+                                          StepOutput* __restrict__ out, int chain, int ctr_inc,
+                                          uint32_t* __restrict__ flag, uint32_t seq, int levels_up, int fence_sys,
+                                          MergeShared<NT>& sh, float* dsm, bool prestaged) {
+    const int tid = threadIdx.x, T = NT;
     const int stride = x.stride;  // one rank's buffer: its exchange-level node records (t_xmax of them)
     const uint32_t epoch = *x.epoch + 1;
     float* mine = x.stage + (size_t)x.rank * stride;
-    __shared__ MergeShared<NT> sh;  // both passes (they run one after the other)
-    extern __shared__ __attribute__((aligned(16))) float dsm[];
     merge_body<NT, STAGE1>(mc, in, recs, nrec, rec_stride, 0, noise, mine, nullptr, 0, 0, nullptr, nullptr, 0, 0, 1, sh,
-                           dsm, false, levels_up);
+                           dsm, prestaged, levels_up);
     __syncthreads();
     // slot parity: epoch & 1.  A peer can run at most one exchange ahead of this rank (it cannot pass
     // its next wait before this rank has published that epoch, i.e. finished copying this one), so
@@ -1419,7 +1353,90 @@ __global__ void __launch_bounds__(NT) merge_xchg_kernel(const ModelConst mc, Ste
     __syncthreads();
     // pass 2: the ranks' buffers side by side are the exchange level's node list (tree_shape)
     merge_body<NT, false>(mc, in, x.stage, mc.t_xnodes, rec_floats_rank(mc.P, mc.K), 1, noise, nullptr, out, chain,
-                          ctr_inc, nullptr, flag, seq, 0, 1, sh, dsm);
+                          ctr_inc, nullptr, flag, seq, 0, fence_sys, sh, dsm);
+}
+template <int NT, bool STAGE1>
+__global__ void __launch_bounds__(NT) merge_xchg_kernel(const ModelConst mc, StepInput* __restrict__ in,
+                                                        const float* __restrict__ recs, int nrec, int rec_stride,
+                                                        const float* __restrict__ noise, XchgArgs x,
+                                                        StepOutput* __restrict__ out, int chain, int ctr_inc,
+                                                        uint32_t* __restrict__ flag, uint32_t seq, int levels_up) {
+    __shared__ MergeShared<NT> sh;  // both passes (they run one after the other)
+    extern __shared__ __attribute__((aligned(16))) float dsm[];
+    xchg_body<NT, STAGE1>(mc, in, recs, nrec, rec_stride, noise, x, out, chain, ctr_inc, flag, seq, levels_up, 1, sh,
+                          dsm, false);
+}
+
+
+
+// In-launch final merge (zero-order four-lane rollout, host steps; launch_rollout with GroupArgs::out): a
+// group's last arriver, its group record stored write-through, counts itself in *gdone; the block that
+// completes the count (every group record is then in memory) copies the ngroups records into LDS with sc1
+// loads and runs the single-block merge on them -- merge_body<NT, STAGE> with the record groups of the
+// 512-thread kernel, so the outputs are merge_kernel's bit for bit -- writing the step outputs and
+// publishing `seq` (and resets the count for the next launch).  The merge's LDS is carved from the rollout's
+// noise stage, dead by then (final_merge_lds).  Saves the merge launch and its record staging: N = 65 536
+// (see DESIGN.md).
+template <int NT>
+__device__ void final_merge(const ModelConst& mc, const StepInput* in, const float* noise, int rec_stride,
+                            const GroupArgs& grp, float* lds) {
+    __shared__ int fin;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's group record stores have completed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(grp.gdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fin = old == (uint32_t)(grp.ngroups - 1);
+    }
+    __syncthreads();
+    if (!fin) return;
+    if (threadIdx.x == 0) __hip_atomic_store(grp.gdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    MergeShared<NT>& sh = *reinterpret_cast<MergeShared<NT>*>(lds);
+    float* smem = lds + (sizeof(MergeShared<NT>) + 15) / 16 * 4;  // 16-byte aligned
+    const int n = grp.ngroups * rec_stride;
+    constexpr int U = 16;  // sc1 loads in flight per thread (other CUs wrote the records)
+    for (int i0 = 0; i0 < n; i0 += U * NT) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * NT + (int)threadIdx.x;
+            v[u] = i < n ? ld_rec(grp.grecs + i) : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * NT + (int)threadIdx.x;
+            if (i < n) smem[i] = v[u];
+        }
+    }
+    __syncthreads();
+    if (grp.xa)  // sharded: this rank's buffer, the exchange, the gathered buffers' merge
+        xchg_body<NT, true>(mc, const_cast<StepInput*>(in), smem, grp.ngroups, rec_stride, noise, *grp.xa, grp.out, 0,
+                            0, grp.flag, grp.seq, grp.levels_up, grp.fence_sys, sh, smem, true);
+    else
+        merge_body<NT, true>(mc, const_cast<StepInput*>(in), smem, grp.ngroups, rec_stride, 0, noise, nullptr,
+                             grp.out, 0, 0, nullptr, grp.flag, grp.seq, 0, grp.fence_sys, sh, smem, true);
+}
+
+size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride) {
+    return (sizeof(MergeShared<256>) + 15) / 16 * 16 + sizeof(float) * (size_t)ngroups * rec_stride +
+           merge_smem_bytes(ngroups, mc.P, mc.K);
+}
+
+// The zero-order four-lane kernel with the LDS noise stage (ZST: H 10 / 12, no cost terms), MPPI / random
+// sampling, grouped records, and the merge's LDS inside the stage (64 x 12 H floats).
+// The step input as a kernel argument (StepInputK): the zero-order four-lane kernel with the LDS noise stage,
+// MPPI / random sampling (no sigma in the argument), P <= KSI_MAXP; SRBD_KS=0 disables (read per context).
+bool ks_ok(const ModelConst& mc, int mode) {
+    if ((mode != ROLLOUT_QUAD && mode != ROLLOUT_THREAD) || mc.kind != SRBD_ZERO_ORDER) return false;
+    return (mc.H == 10 || mc.H == 12) && mc.method != SRBD_CEM_MPPI && mc.P <= KSI_MAXP;
+}
+
+bool final_merge_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride) {
+    // (the gait-adaptive rollout and the cost terms, which can be switched on later, are checked per launch)
+    if (mode != ROLLOUT_QUAD || mc.kind != SRBD_ZERO_ORDER) return false;
+    if ((mc.H != 10 && mc.H != 12) || mc.method == SRBD_CEM_MPPI || ngroups < 1) return false;
+    const size_t zst =
+        sizeof(float) * (size_t)(64 * (12 * mc.H + 1) > GROUP_LDS_FLOATS ? 64 * (12 * mc.H + 1) : GROUP_LDS_FLOATS);
+    return final_merge_lds(mc, ngroups, rec_stride) <= zst;
 }
 
 __global__ void advance_kernel(const ModelConst mc, StepInput* __restrict__ in, const StepOutput* __restrict__ out) {

@@ -21,6 +21,7 @@ int rng_grid(const ModelConst& mc);
 // In-launch level-1 fold of the reduction tree (srbd_core.h): the leaf records of TREE_FAN consecutive leaves (a
 // level-1 node) are folded by the node's last arriving block into grecs[node], a record of the same format, so
 // the merge reads ceil(nleaf / TREE_FAN) records instead of nleaf.  gsize == TREE_FAN when on, 1 when off.
+struct XchgArgs;
 constexpr int GROUP_LDS_FLOATS = 6144;  // the last arriver stages its node's records in LDS (24 KB)
 constexpr int GROUP_MIN_LEAVES = 256;   // the merge reads the leaf records up to this many (C2: 157)
 struct GroupArgs {
@@ -40,6 +41,11 @@ struct GroupArgs {
     // host steps: the step input by value (host memory, read by the launcher): the rollout takes it as a
     // kernel argument and writes the device StepInput itself (ks_ok), no upload kernel
     const void* ksi = nullptr;  // a StepInputK
+    // sharded host steps over xGMI: the final merger folds the rank's buffer (`levels_up` levels above the
+    // level-1 records), exchanges it with the peers and merges the gathered buffers, as merge_xchg_kernel does
+    // (device copy of the context's XchgArgs)
+    const XchgArgs* xa = nullptr;
+    int levels_up = 0;
 };
 bool ks_ok(const ModelConst& mc, int mode);
 // LDS the in-launch final merge needs (merge_body<256> of ngroups records) and whether the launch can do it

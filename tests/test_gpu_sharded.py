@@ -3,8 +3,9 @@
 World size 1 (the box has one GPU; RCCL refuses two ranks on one device), both transports: the
 library's own RCCL communicator (ncclAllGather issued from C++ on the context stream) and
 torch.distributed.all_gather_into_tensor on a torch stream shared with the library.  The
-result must match the unsharded srbd_step on the same noise to reduction-order tolerance, and
-the device-resident chain must run.  Multi-rank merging is covered on CPU with gloo
+result must equal the unsharded srbd_step on the same noise bit for bit (the fixed reduction tree), also on
+device draws, and the device-resident chain must run.  At N = 65 536 (grouped zero-order MPPI) the xGMI host
+step folds, exchanges and merges inside the rollout launch (final merger, GroupArgs::xa).  Multi-rank merging is covered on CPU with gloo
 (tests/test_distributed_gloo.py) and on this GPU with several contexts
 (test_gpu_parity.py::test_sharded_records_on_one_gpu).
 """
@@ -35,11 +36,14 @@ def test_sharded_driver_world1_matches_step(transport):
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
     try:
-        for method in ("mppi", "cem_mppi", "random_sampling"):
-            case = make_case("c2", N=3000, method=method, seed=17)
+        for wkey, N, method in (("c2", 3000, "mppi"), ("c2", 3000, "cem_mppi"), ("c2", 3000, "random_sampling"),
+                                ("c2", 65536, "mppi"), ("c5", 65536, "mppi")):
+            case = make_case(wkey, N=N, method=method, seed=17)
             ref = _lib.Context(product_cfg(case))
             b0, s0, r0, _ = ref.step(case["state"], case["ref"], case["contact"], case["best"], sigma=case["sigma"],
                                      noise=case["noise"])
+            bd, _, rd, _ = ref.step(case["state"], case["ref"], case["contact"], case["best"], sigma=case["sigma"],
+                                    seed=42, counter=5)
             ref.close()
             mpc = ShardedSamplingMPC(product_cfg(case), 0, 1, 0, transport=transport)
             if transport == "auto":
@@ -51,11 +55,14 @@ def test_sharded_driver_world1_matches_step(transport):
             np.testing.assert_array_equal(np.array(r1.grf), np.array(r0.grf))
             if method == "cem_mppi":
                 np.testing.assert_array_equal(s1, s0)
+            # device draws: the same bits as the unsharded step keyed alike
+            b2, _, r2 = mpc.step(case["state"], case["ref"], case["contact"], case["best"], sigma=case["sigma"],
+                                 seed=42, counter=5)
+            assert r2.best_index == rd.best_index
+            np.testing.assert_array_equal(b2, bd)
             # device-resident chain on the torch stream
-            b2, _, _ = mpc.step(case["state"], case["ref"], case["contact"], b1, sigma=s1, seed=42, counter=5)
             assert mpc.device_steps(4) > 0
             torch.cuda.synchronize()
-            assert np.all(np.isfinite(b2))
             # after a device chain, a host step still reproduces the unsharded step
             b3, s3, r3 = mpc.step(case["state"], case["ref"], case["contact"], case["best"], sigma=case["sigma"],
                                   noise_local=case["noise"])
