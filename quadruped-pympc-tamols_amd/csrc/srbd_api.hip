@@ -1086,10 +1086,10 @@ static uint64_t next_seed(const srbd_ctx* c, uint64_t seed) {
 }
 
 // ------------------------------------------------------------------ host merge (no device)
-// The same reduction tree as the device (srbd_core.h): 64-row leaves, TREE_FAN children per node folded in
-// order, node key = the children's minimum, child sums rescaled by expf(-1 * (m_child - m_node)).  The host sums
-// a leaf's rows in row order (the device: wave_sum_f32's DPP order), so host and device agree to rounding; the
-// host merge itself is W-invariant, as the device's is.
+// The same reduction tree as the device (srbd_core.h): 64-row leaves summed in the balanced pairwise tree,
+// TREE_FAN children per node folded in order, node key = the children's minimum, child sums rescaled by
+// expf(-1 * (m_child - m_node)).  Host and device differ only by their expf; the host merge is W-invariant, as
+// the device's is.
 namespace {
 struct HostNode {
     uint64_t key = ~0ull;
@@ -1113,6 +1113,13 @@ HostNode host_fold(const HostNode* ch, int n, int P, int K, bool sums) {
     std::sort(o.top.begin(), o.top.end());
     if ((int)o.top.size() > K) o.top.resize(K);
     return o;
+}
+
+// The leaf sum: the balanced pairwise tree over 64 values in row order (wave_sum_f32's lane-63 chain)
+float pairwise64(float* v) {
+    for (int n = 32; n >= 1; n >>= 1)
+        for (int i = 0; i < n; ++i) v[i] = v[2 * i] + v[2 * i + 1];
+    return v[0];
 }
 
 std::vector<HostNode> host_fold_level(const std::vector<HostNode>& lv, int P, int K, bool sums) {
@@ -1168,12 +1175,15 @@ extern "C" int srbd_make_record_host(const srbd_config* cfg, int32_t rank, int32
         std::sort(o.top.begin(), o.top.end());
         if ((int)o.top.size() > K) o.top.resize(K);
         o.v.assign(P, 0.0f);
-        if (sums) {
+        if (sums) {  // rows past the shard's end are empty leaf slots: e = 0
             const float m = u2f((uint32_t)(o.key >> 32));
-            for (int k = r0; k < r1; ++k) {
-                const float e = expf(-1.0f * (costs[k] - m));
-                o.s = o.s + e;
-                for (int j = 0; j < P; ++j) o.v[j] = o.v[j] + e * noise_rows[(size_t)k * P + j];
+            float e[LEAF_ROWS], t[LEAF_ROWS];
+            for (int k = 0; k < LEAF_ROWS; ++k) e[k] = r0 + k < r1 ? expf(-1.0f * (costs[r0 + k] - m)) : 0.0f;
+            for (int k = 0; k < LEAF_ROWS; ++k) t[k] = e[k];
+            o.s = pairwise64(t);
+            for (int j = 0; j < P; ++j) {
+                for (int k = 0; k < LEAF_ROWS; ++k) t[k] = r0 + k < r1 ? e[k] * noise_rows[(size_t)(r0 + k) * P + j] : 0.0f;
+                o.v[j] = pairwise64(t);
             }
         }
         lv.push_back(std::move(o));

@@ -426,8 +426,9 @@ __device__ __forceinline__ bool level1_fold(const ModelConst& mc, const float* _
 }
 
 // Wave sum in a fixed DPP tree (row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15/31); the total
-// lands in lane 63.  All 64 lanes must be active.  The leaf order of the reduction tree (srbd_core.h); the host
-// restatement is srbd_api.hip host_wave_sum.
+// lands in lane 63.  All 64 lanes must be active.  Lane 63's chain is the balanced pairwise tree over the lanes in
+// order ((v0 + v1) + (v2 + v3)) + ... (no term ever adds the zero of an invalid source), the leaf sum of the
+// reduction tree (srbd_core.h); block_epilogue's LDS path and the host (srbd_api.hip pairwise64) form the same tree.
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ float dpp_f32(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, 0xF, false));
@@ -499,6 +500,28 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
         const size_t ldn = (size_t)mc.ldn;
         const float* col0 = noise + k0 + 64 * b + lane;
         constexpr int CB = 8;  // columns whose loads are in flight together
+        if constexpr (ZS) {
+            // one leaf (64 samples) staged in LDS: thread j sums column j over the 64 rows itself, in the balanced
+            // pairwise tree wave_sum_f32 forms across lanes (adjacent pairs, then pairs of pairs: the same bits),
+            // instead of one six-step DPP reduction per column per wave
+            for (int j = tid; j <= P; j += (int)blockDim.x) {
+                const float sj = (j < P && zs) ? in->sigma[j] : 1.0f;
+                const int jl = j < P ? j : 0;
+                float lv[32];
+#pragma unroll
+                for (int i = 0; i < 32; ++i) {
+                    const float e0 = e_sh[2 * i], e1 = e_sh[2 * i + 1];
+                    const float p0 = j < P ? e0 * (zst[(2 * i) * zstride + jl] * sj) : e0;
+                    const float p1 = j < P ? e1 * (zst[(2 * i + 1) * zstride + jl] * sj) : e1;
+                    lv[i] = p0 + p1;
+                }
+#pragma unroll
+                for (int n = 16; n >= 1; n >>= 1)
+#pragma unroll
+                    for (int i = 0; i < n; ++i) lv[i] = lv[2 * i] + lv[2 * i + 1];
+                st_rec(&rec[j < P ? REC_HDR + j : 1], lv[0]);
+            }
+        } else
         for (int j0 = w % wpl; j0 <= P; j0 += CB * wpl) {
             float z[CB];
 #pragma unroll

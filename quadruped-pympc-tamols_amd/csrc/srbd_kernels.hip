@@ -156,16 +156,17 @@ __device__ __forceinline__ float quad_cross(float vl, float fl) {
 }
 
 // The in-launch final merge of the group records (GroupArgs::out), defined after merge_body.
-template <int NT>
+template <int NT, bool XG>
 __device__ void final_merge(const ModelConst& mc, const StepInput* in, const float* noise, int rec_stride,
                             const GroupArgs& grp, float* lds);
 
-// FM: the instantiation with the in-launch final merge (launched when GroupArgs::out is set); the others carry
-// none of its code (C2's launch, which never merges in-launch, measured 0.25 us slower with it).
+// FM: 1 the instantiation with the in-launch final merge (launched when GroupArgs::out is set), 2 with the sharded
+// step's exchange too (GroupArgs::xa); the others carry none of its code (C2's launch, which never merges
+// in-launch, measured 0.25 us slower with it; the exchange costs the plain final merge 23 VGPRs and a spill).
 // KS: the host step's input arrives by value (StepInputK, GroupArgs::ksi); block 0 writes it to the device
 // StepInput `in_dev` for the merge and later readers, so the step needs no upload kernel (one dependent launch
 // and a PCIe read fewer).
-template <int KIND, int HT, int ST, bool CEMT, bool EXT, bool FM = false, bool KS = false>
+template <int KIND, int HT, int ST, bool CEMT, bool EXT, int FM = 0, bool KS = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) rollout_quad_kernel(
                                                            const std::conditional_t<KS, StepInputK, KsNone> ksi,
                                                            const ModelConst mc, const StepInput* __restrict__ in_dev,
@@ -508,7 +509,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     const bool glast = block_epilogue<CEMT, ZST>(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride,
                                                  0.0f, grp, nroll, ZST ? zst : nullptr, ZSTR);
     if constexpr (FM && ZST && !CEMT)
-        if (glast) final_merge<256>(mc, in, noise, rec_stride, grp, zst);
+        if (glast) final_merge<256, FM == 2>(mc, in, noise, rec_stride, grp, zst);
     SRBD_RSTAMP(5);
 }
 
@@ -1286,22 +1287,14 @@ __global__ void __launch_bounds__(NT) merge_kernel(const ModelConst mc, StepInpu
 // step; this form measures within noise of no release at all (scripts/sharded_probe.py).
 // NT / STAGE1: pass 1 as the single-rank merge runs it -- the LDS-staged 512-thread body when this
 // rank's block records fit (C2: 157), else the 1024-thread direct body; pass 2 (W records) direct.
-// xchg_body: the whole sequence for one block (merge_xchg_kernel; the rollout launch's final merger, final_merge,
-// with prestaged level-1 records).
-template <int NT, bool STAGE1>
-__device__ __forceinline__ void xchg_body(const ModelConst& mc, StepInput* __restrict__ in,
-                                          const float* __restrict__ recs, int nrec, int rec_stride,
-                                          const float* __restrict__ noise, const XchgArgs& x,
-                                          StepOutput* __restrict__ out, int chain, int ctr_inc,
-                                          uint32_t* __restrict__ flag, uint32_t seq, int levels_up, int fence_sys,
-                                          MergeShared<NT>& sh, float* dsm, bool prestaged) {
+// xchg_exchange: steps 2-3 for one block, after pass 1 has written this rank's buffer `mine` (= x.stage slot rank):
+// returns false after publishing the failure when a peer timed out, true with the gathered buffers in x.stage.
+template <int NT>
+__device__ __forceinline__ bool xchg_exchange(const XchgArgs& x, const float* mine, StepOutput* out, uint32_t* flag,
+                                              uint32_t seq) {
     const int tid = threadIdx.x, T = NT;
     const int stride = x.stride;  // one rank's buffer: its exchange-level node records (t_xmax of them)
     const uint32_t epoch = *x.epoch + 1;
-    float* mine = x.stage + (size_t)x.rank * stride;
-    merge_body<NT, STAGE1>(mc, in, recs, nrec, rec_stride, 0, noise, mine, nullptr, 0, 0, nullptr, nullptr, 0, 0, 1, sh,
-                           dsm, prestaged, levels_up);
-    __syncthreads();
     // slot parity: epoch & 1.  A peer can run at most one exchange ahead of this rank (it cannot pass
     // its next wait before this rank has published that epoch, i.e. finished copying this one), so
     // its epoch+1 record lands in the other half and never overwrites a slot still being copied.
@@ -1342,7 +1335,7 @@ __device__ __forceinline__ void xchg_body(const ModelConst& mc, StepInput* __res
             __threadfence_system();
             if (flag) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        return;
+        return false;
     }
     for (int i = tid; i < (x.world - 1) * stride; i += T) {
         const int q = i / stride, k = i - q * stride;
@@ -1351,9 +1344,7 @@ __device__ __forceinline__ void xchg_body(const ModelConst& mc, StepInput* __res
                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
     }
     __syncthreads();
-    // pass 2: the ranks' buffers side by side are the exchange level's node list (tree_shape)
-    merge_body<NT, false>(mc, in, x.stage, mc.t_xnodes, rec_floats_rank(mc.P, mc.K), 1, noise, nullptr, out, chain,
-                          ctr_inc, nullptr, flag, seq, 0, fence_sys, sh, dsm);
+    return true;
 }
 template <int NT, bool STAGE1>
 __global__ void __launch_bounds__(NT) merge_xchg_kernel(const ModelConst mc, StepInput* __restrict__ in,
@@ -1363,8 +1354,14 @@ __global__ void __launch_bounds__(NT) merge_xchg_kernel(const ModelConst mc, Ste
                                                         uint32_t* __restrict__ flag, uint32_t seq, int levels_up) {
     __shared__ MergeShared<NT> sh;  // both passes (they run one after the other)
     extern __shared__ __attribute__((aligned(16))) float dsm[];
-    xchg_body<NT, STAGE1>(mc, in, recs, nrec, rec_stride, noise, x, out, chain, ctr_inc, flag, seq, levels_up, 1, sh,
-                          dsm, false);
+    float* mine = x.stage + (size_t)x.rank * x.stride;
+    merge_body<NT, STAGE1>(mc, in, recs, nrec, rec_stride, 0, noise, mine, nullptr, 0, 0, nullptr, nullptr, 0, 0, 1, sh,
+                           dsm, false, levels_up);
+    __syncthreads();
+    if (!xchg_exchange<NT>(x, mine, out, flag, seq)) return;
+    // pass 2: the ranks' buffers side by side are the exchange level's node list (tree_shape)
+    merge_body<NT, false>(mc, in, x.stage, mc.t_xnodes, rec_floats_rank(mc.P, mc.K), 1, noise, nullptr, out, chain,
+                          ctr_inc, nullptr, flag, seq, 0, 1, sh, dsm);
 }
 
 
@@ -1377,7 +1374,7 @@ __global__ void __launch_bounds__(NT) merge_xchg_kernel(const ModelConst mc, Ste
 // publishing `seq` (and resets the count for the next launch).  The merge's LDS is carved from the rollout's
 // noise stage, dead by then (final_merge_lds).  Saves the merge launch and its record staging: N = 65 536
 // (see DESIGN.md).
-template <int NT>
+template <int NT, bool XG>
 __device__ void final_merge(const ModelConst& mc, const StepInput* in, const float* noise, int rec_stride,
                             const GroupArgs& grp, float* lds) {
     __shared__ int fin;
@@ -1408,17 +1405,31 @@ __device__ void final_merge(const ModelConst& mc, const StepInput* in, const flo
         }
     }
     __syncthreads();
-    if (grp.xa)  // sharded: this rank's buffer, the exchange, the gathered buffers' merge
-        xchg_body<NT, true>(mc, const_cast<StepInput*>(in), smem, grp.ngroups, rec_stride, noise, *grp.xa, grp.out, 0,
-                            0, grp.flag, grp.seq, grp.levels_up, grp.fence_sys, sh, smem, true);
-    else
-        merge_body<NT, true>(mc, const_cast<StepInput*>(in), smem, grp.ngroups, rec_stride, 0, noise, nullptr,
-                             grp.out, 0, 0, nullptr, grp.flag, grp.seq, 0, grp.fence_sys, sh, smem, true);
+    // sharded (grp.xa): pass 0 folds this rank's buffer, the exchange gathers the ranks' buffers (the exchange
+    // level's node list), pass 1 merges them into the outputs.  One merge_body call site for both passes.
+    int nrec = grp.ngroups, stride = rec_stride;
+    for (int pass = 0;; ++pass) {
+        const bool rank_pass = XG && pass == 0;
+        float* mine = rank_pass ? grp.xa->stage + (size_t)grp.xa->rank * grp.xa->stride : nullptr;
+        merge_body<NT, true>(mc, const_cast<StepInput*>(in), smem, nrec, stride, 0, noise, mine,
+                             rank_pass ? nullptr : grp.out, 0, 0, nullptr, rank_pass ? nullptr : grp.flag, grp.seq, 0,
+                             grp.fence_sys, sh, smem, true, rank_pass ? grp.levels_up : 0);
+        if (!rank_pass) return;
+        __syncthreads();
+        if (!xchg_exchange<NT>(*grp.xa, mine, grp.out, grp.flag, grp.seq)) return;
+        nrec = mc.t_xnodes;
+        stride = rec_floats_rank(mc.P, mc.K);
+        for (int i = threadIdx.x; i < nrec * stride; i += NT) smem[i] = grp.xa->stage[i];
+        __syncthreads();
+    }
 }
 
 size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride) {
-    return (sizeof(MergeShared<256>) + 15) / 16 * 16 + sizeof(float) * (size_t)ngroups * rec_stride +
-           merge_smem_bytes(ngroups, mc.P, mc.K);
+    const size_t a = sizeof(float) * (size_t)ngroups * rec_stride + merge_smem_bytes(ngroups, mc.P, mc.K);
+    // a sharded step's second pass: the gathered node records
+    const size_t b =
+        sizeof(float) * (size_t)mc.t_xnodes * rec_floats_rank(mc.P, mc.K) + merge_smem_bytes(mc.t_xnodes, mc.P, mc.K);
+    return (sizeof(MergeShared<256>) + 15) / 16 * 16 + (a > b ? a : b);
 }
 
 // The zero-order four-lane kernel with the LDS noise stage (ZST: H 10 / 12, no cost terms), MPPI / random
@@ -1473,18 +1484,25 @@ static void launch_rollout_t(const ModelConst& mc, const StepInput* in, const fl
         const dim3 grid(blocks + extra * 256 / threads);
         if constexpr (KIND == SRBD_ZERO_ORDER && (HT == 10 || HT == 12) && !EXT) {
             if (!cem && grp.ksi) {  // ks_ok: the step input as a kernel argument
-                if (grp.out)
-                    hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, true, true>), grid, dim3(threads),
+                if (grp.out && grp.xa)
+                    hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, 2, true>), grid, dim3(threads),
+                                       0, s, *static_cast<const StepInputK*>(grp.ksi), mc, in, noise, costs, recs, rec_stride, job, blocks, grp);
+                else if (grp.out)
+                    hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, 1, true>), grid, dim3(threads),
                                        0, s, *static_cast<const StepInputK*>(grp.ksi), mc, in, noise, costs, recs, rec_stride, job, blocks, grp);
                 else
-                    hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, false, true>), grid,
+                    hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, 0, true>), grid,
                                        dim3(threads), 0, s, *static_cast<const StepInputK*>(grp.ksi), mc, in, noise, costs, recs, rec_stride, job, blocks,
                                        grp);
                 return;
             }
             if (grp.out && !cem) {  // final_merge_ok: the in-launch final merge
-                hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, true>), grid, dim3(threads), 0, s, KsNone{},
-                                   mc, in, noise, costs, recs, rec_stride, job, blocks, grp);
+                if (grp.xa)
+                    hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, 2>), grid, dim3(threads), 0, s,
+                                       KsNone{}, mc, in, noise, costs, recs, rec_stride, job, blocks, grp);
+                else
+                    hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, 1>), grid, dim3(threads), 0, s,
+                                       KsNone{}, mc, in, noise, costs, recs, rec_stride, job, blocks, grp);
                 return;
             }
         }
