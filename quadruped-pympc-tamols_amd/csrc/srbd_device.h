@@ -364,7 +364,14 @@ __device__ __forceinline__ void fold_node_lds(const ModelConst& mc, const float*
         for (int j = tid; j <= P; j += T) {
             const int off = j < P ? REC_HDR + j : 1;
             float a = 0.0f;
-            for (int i = 0; i < nb; ++i) a = a + sc_sh[i] * st[(size_t)i * rec_stride + off];
+            for (int cb = 0; cb < nb; cb += 8) {  // 8 children's LDS loads in flight, then their adds in order
+                float x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = cb + u < nb ? st[(size_t)(cb + u) * rec_stride + off] : 0.0f;
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (cb + u < nb) a = a + sc_sh[cb + u] * x[u];
+            }
             st_rec(&G[off], a);
         }
     }
@@ -433,14 +440,144 @@ template <int CTRL, int ROWMASK>
 __device__ __forceinline__ float dpp_f32(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWMASK, 0xF, false));
 }
-__device__ __forceinline__ float wave_sum_f32(float v) {
+// The first LEVELS levels of that tree: 4 -> lane 16 r + 15 holds the pairwise sum of 16-lane row r, 5 -> lanes 31
+// and 63 hold those of lanes 0..31 and 32..63, 6 -> lane 63 the wave's.
+template <int LEVELS>
+__device__ __forceinline__ float lane_tree_f32(float v) {
     v = v + dpp_f32<0x111, 0xF>(v);
     v = v + dpp_f32<0x112, 0xF>(v);
     v = v + dpp_f32<0x114, 0xF>(v);
     v = v + dpp_f32<0x118, 0xF>(v);
-    v = v + dpp_f32<0x142, 0xA>(v);
-    v = v + dpp_f32<0x143, 0xC>(v);
+    if constexpr (LEVELS >= 5) v = v + dpp_f32<0x142, 0xA>(v);
+    if constexpr (LEVELS >= 6) v = v + dpp_f32<0x143, 0xC>(v);
     return v;
+}
+__device__ __forceinline__ float wave_sum_f32(float v) { return lane_tree_f32<6>(v); }
+
+// Leaf sums of the weighted noise, thread form with SPB = 64 SPL samples per block (SPL = 2 / 4): wave w takes
+// columns w, w + NW, ...; lane l holds samples SPL l .. SPL l + SPL - 1 of a column (one coalesced load), pairs
+// them in registers (the tree's first log2 SPL levels) and the DPP rows finish each leaf (64 / SPL lanes): leaf b's
+// sum lands in lane (b + 1) 64 / SPL - 1.  Column P: the e alone.  CB columns' loads are in flight together.
+template <int SPL>
+__device__ __forceinline__ void leaf_wsum_lanes(const ModelConst& mc, const StepInput* __restrict__ in,
+                                                const float* __restrict__ base, bool zs, const float* e_sh,
+                                                float* __restrict__ recs, int rec_stride, int rec0) {
+    constexpr int CB = SPL == 4 ? 8 : 12;
+    constexpr int LPL = 64 / SPL;  // lanes per leaf
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, NW = blockDim.x >> 6;
+    const int P = mc.P;
+    const size_t ldn = (size_t)mc.ldn;
+    float e[SPL];
+#pragma unroll
+    for (int u = 0; u < SPL; ++u) e[u] = e_sh[SPL * lane + u];
+    float* rec = recs + (size_t)(rec0 + lane / LPL) * rec_stride;
+    const bool writer = (lane % LPL) == LPL - 1;
+    for (int j0 = w; j0 <= P; j0 += CB * NW) {
+        float z[CB][SPL];
+#pragma unroll
+        for (int b = 0; b < CB; ++b) {
+            const int j = j0 + b * NW;
+            const float* col = base + (size_t)(j < P ? j : 0) * ldn + SPL * lane;
+            if constexpr (SPL == 4) {
+                const float4 v = *reinterpret_cast<const float4*>(col);
+                z[b][0] = v.x, z[b][1] = v.y, z[b][2] = v.z, z[b][3] = v.w;
+            } else {
+                const float2 v = *reinterpret_cast<const float2*>(col);
+                z[b][0] = v.x, z[b][1] = v.y;
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < CB; ++b) {
+            const int j = j0 + b * NW;
+            if (j > P) break;
+            float p[SPL];
+            if (j < P) {
+                const float sj = zs ? in->sigma[j] : 1.0f;  // x * 1 == x
+#pragma unroll
+                for (int u = 0; u < SPL; ++u) p[u] = e[u] * (z[b][u] * sj);
+            } else {
+#pragma unroll
+                for (int u = 0; u < SPL; ++u) p[u] = e[u];
+            }
+            float a;
+            if constexpr (SPL == 4)
+                a = (p[0] + p[1]) + (p[2] + p[3]);
+            else
+                a = p[0] + p[1];
+            a = lane_tree_f32<SPL == 4 ? 4 : 5>(a);
+            if (writer) st_rec(&rec[j < P ? REC_HDR + j : 1], a);
+        }
+    }
+}
+
+// Leaf sums, one 64-sample leaf per block (four-lane form, thread form at 64 samples per block): thread j forms
+// column j's 64 products from the LDS stage (ZS: row s at zst[s zstride]) or the SoA noise (16 float4 loads in
+// flight) and adds them in the pairwise tree in registers; the last wave adds the e alone (column P) by DPP.
+template <bool ZS>
+__device__ __forceinline__ void leaf_wsum_cols(const ModelConst& mc, const StepInput* __restrict__ in,
+                                               const float* __restrict__ base, const float* zst, int zstride, bool zs,
+                                               const float* e_sh, float* __restrict__ rec) {
+    const int tid = threadIdx.x, T = blockDim.x, P = mc.P;
+    const size_t ldn = (size_t)mc.ldn;
+    if ((tid >> 6) == (T >> 6) - 1) {
+        const float t = wave_sum_f32(e_sh[tid & 63]);
+        if ((tid & 63) == 63) st_rec(&rec[1], t);
+    }
+    if constexpr (!ZS) {  // from global memory: the column's 16 float4 loads in flight together, the tree in place
+        for (int j = tid; j < P; j += T) {
+            const float sj = zs ? in->sigma[j] : 1.0f;  // x * 1 == x
+            const float4* row = reinterpret_cast<const float4*>(base + (size_t)j * ldn);
+            float x[64];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float4 v = row[i];
+                x[4 * i] = v.x, x[4 * i + 1] = v.y, x[4 * i + 2] = v.z, x[4 * i + 3] = v.w;
+            }
+#pragma unroll
+            for (int i = 0; i < 32; ++i) x[i] = e_sh[2 * i] * (x[2 * i] * sj) + e_sh[2 * i + 1] * (x[2 * i + 1] * sj);
+#pragma unroll
+            for (int n = 16; n >= 1; n >>= 1)
+#pragma unroll
+                for (int i = 0; i < n; ++i) x[i] = x[2 * i] + x[2 * i + 1];
+            st_rec(&rec[REC_HDR + j], x[0]);
+        }
+        return;
+    }
+    for (int j = tid; j < P; j += T) {
+        const float sj = zs ? in->sigma[j] : 1.0f;  // x * 1 == x
+        float first = 0.0f, tot = 0.0f;
+#pragma nounroll
+        for (int h = 0; h < 2; ++h) {  // the tree's two 32-row halves one after the other (registers), then the root
+            float lv[16];
+            if constexpr (ZS) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int r = 32 * h + 2 * i;
+                    lv[i] = e_sh[r] * (zst[r * zstride + j] * sj) + e_sh[r + 1] * (zst[(r + 1) * zstride + j] * sj);
+                }
+            } else {
+                const float4* row = reinterpret_cast<const float4*>(base + (size_t)j * ldn) + 8 * h;
+                float4 v[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] = row[i];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int r = 32 * h + 4 * i;
+                    lv[2 * i] = e_sh[r] * (v[i].x * sj) + e_sh[r + 1] * (v[i].y * sj);
+                    lv[2 * i + 1] = e_sh[r + 2] * (v[i].z * sj) + e_sh[r + 3] * (v[i].w * sj);
+                }
+            }
+#pragma unroll
+            for (int n = 8; n >= 1; n >>= 1)
+#pragma unroll
+                for (int i = 0; i < n; ++i) lv[i] = lv[2 * i] + lv[2 * i + 1];
+            if (h == 0)
+                first = lv[0];
+            else
+                tot = first + lv[0];
+        }
+        st_rec(&rec[REC_HDR + j], tot);
+    }
 }
 
 // The block's leaf records (srbd_core.h): SPB samples = lpb = SPB / 64 leaves (four-lane: 1; thread form: 1, 2
@@ -448,9 +585,9 @@ __device__ __forceinline__ float wave_sum_f32(float v) {
 // `tag` (the gait-adaptive step frequency, else 0), which the owner of the leaf's best row stores in the header.
 //  keys -> LDS; leaf minima (one wave per leaf); CEM: each leaf's K smallest keys by ranks (every sample counts
 //  the leaf's keys below its own; the `lps` lanes of a sample split the count, summed by DPP); e = exp(-(c - m));
-//  the sums: waves_per_leaf = NW / lpb waves take a leaf's columns in turn, lane l the leaf's row l: one product
-//  e_l noise_l[j] per lane and wave_sum_f32 (column P: e_l alone).  The noise comes from the LDS stage `zst`
-//  (ZS: four-lane zero-order, row l at zst[l * zstride]) or from the SoA noise (coalesced).
+//  the sums v[j] = sum_l e_l noise_l[j] and s = sum_l e_l of each leaf in the pairwise tree over its 64 rows
+//  (leaf_wsum_cols at one leaf per block, from the LDS stage `zst` (ZS: four-lane zero-order) or the SoA noise;
+//  leaf_wsum_lanes at 2 / 4 leaves per block).
 // Then the level-1 fold (grp.gsize > 1).  All threads call it; returns level1_fold's verdict (false without one).
 template <bool CEMT, bool ZS = false>
 __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepInput* __restrict__ in, const int SPB,
@@ -458,12 +595,14 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
                                                float* __restrict__ recs, int rec_stride, float tag,
                                                const GroupArgs& grp, int nroll, float* zst = nullptr,
                                                int zstride = 0) {
-    __shared__ uint64_t ks[256];
-    __shared__ float e_sh[256];
+    // ZS (four-lane, 64 samples per block): sized for one leaf, so the block's LDS (the noise stage) stays within a
+    // quarter of the CU's 160 KB (four blocks per CU)
+    __shared__ uint64_t ks[ZS ? 64 : 256];
+    __shared__ float e_sh[ZS ? 64 : 256];
     __shared__ uint64_t lmin[4];
     __shared__ uint64_t lel[CEMT ? 4 : 1][CEMT ? MAXK : 1];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int NW = (int)blockDim.x >> 6, lpb = SPB >> 6, wpl = NW / lpb;
+    const int NW = (int)blockDim.x >> 6, lpb = SPB >> 6;
     const int P = mc.P, K = mc.K;
     const int k0 = blockIdx.x * SPB;
     const bool rs = mc.method == SRBD_RANDOM_SAMPLING;
@@ -493,58 +632,14 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
     if (!rs) {
         if (sib >= 0) e_sh[sib] = valid ? expf(-1.0f * (cost - u2f((uint32_t)(lmin[sib >> 6] >> 32)))) : 0.0f;
         __syncthreads();
-        const int b = w / wpl;
-        const float e = e_sh[64 * b + lane];
         const bool zs = CEMT && zs_scaled(mc, in);
-        float* rec = recs + (size_t)(blockIdx.x * lpb + b) * rec_stride;
-        const size_t ldn = (size_t)mc.ldn;
-        const float* col0 = noise + k0 + 64 * b + lane;
-        constexpr int CB = 8;  // columns whose loads are in flight together
-        if constexpr (ZS) {
-            // one leaf (64 samples) staged in LDS: thread j sums column j over the 64 rows itself, in the balanced
-            // pairwise tree wave_sum_f32 forms across lanes (adjacent pairs, then pairs of pairs: the same bits),
-            // instead of one six-step DPP reduction per column per wave
-            for (int j = tid; j <= P; j += (int)blockDim.x) {
-                const float sj = (j < P && zs) ? in->sigma[j] : 1.0f;
-                const int jl = j < P ? j : 0;
-                float lv[32];
-#pragma unroll
-                for (int i = 0; i < 32; ++i) {
-                    const float e0 = e_sh[2 * i], e1 = e_sh[2 * i + 1];
-                    const float p0 = j < P ? e0 * (zst[(2 * i) * zstride + jl] * sj) : e0;
-                    const float p1 = j < P ? e1 * (zst[(2 * i + 1) * zstride + jl] * sj) : e1;
-                    lv[i] = p0 + p1;
-                }
-#pragma unroll
-                for (int n = 16; n >= 1; n >>= 1)
-#pragma unroll
-                    for (int i = 0; i < n; ++i) lv[i] = lv[2 * i] + lv[2 * i + 1];
-                st_rec(&rec[j < P ? REC_HDR + j : 1], lv[0]);
-            }
-        } else
-        for (int j0 = w % wpl; j0 <= P; j0 += CB * wpl) {
-            float z[CB];
-#pragma unroll
-            for (int u = 0; u < CB; ++u) {
-                const int j = j0 + u * wpl;
-                const int jl = j < P ? j : 0;
-                if constexpr (ZS)
-                    z[u] = zst[lane * zstride + jl];
-                else
-                    z[u] = col0[(size_t)jl * ldn];
-            }
-#pragma unroll
-            for (int u = 0; u < CB; ++u) {
-                const int j = j0 + u * wpl;
-                if (j > P) break;
-                float prod = e;
-                if (j < P) {
-                    const float sj = zs ? in->sigma[j] : 1.0f;  // x * 1 == x
-                    prod = e * (z[u] * sj);
-                }
-                const float tot = wave_sum_f32(prod);
-                if (lane == 63) st_rec(&rec[j < P ? REC_HDR + j : 1], tot);
-            }
+        if (SPB == 64)
+            leaf_wsum_cols<ZS>(mc, in, noise + k0, zst, zstride, zs, e_sh, recs + (size_t)blockIdx.x * rec_stride);
+        else if constexpr (!ZS) {
+            if (SPB == 128)
+                leaf_wsum_lanes<2>(mc, in, noise + k0, zs, e_sh, recs, rec_stride, blockIdx.x * lpb);
+            else
+                leaf_wsum_lanes<4>(mc, in, noise + k0, zs, e_sh, recs, rec_stride, blockIdx.x * lpb);
         }
     }
     SRBD_RSTAMP(4);
@@ -565,9 +660,12 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
         st_rec(&rec[REC_HDR + P + 2 * q + 1], u2f((uint32_t)(kk >> 32)));
     }
     if (grp.gsize > 1) {
-        if (zst) return level1_fold(mc, recs, rec_stride, grp, nroll, lpb, zst);
-        __shared__ float st[GROUP_LDS_FLOATS];
-        return level1_fold(mc, recs, rec_stride, grp, nroll, lpb, st);
+        if constexpr (ZS) {
+            return level1_fold(mc, recs, rec_stride, grp, nroll, lpb, zst);
+        } else {
+            __shared__ float st[GROUP_LDS_FLOATS];
+            return level1_fold(mc, recs, rec_stride, grp, nroll, lpb, st);
+        }
     }
     return false;
 }

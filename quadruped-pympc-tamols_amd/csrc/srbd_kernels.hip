@@ -950,32 +950,35 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         uint64_t* nk_out = nkA;
         for (int L = 0; rank_out ? L < levels_up : nlev > 1; ++L) {
             const int n2 = (nlev + TREE_FAN - 1) / TREE_FAN;
-            for (int g2 = tid; g2 < n2; g2 += T) {  // node keys: the children's minimum
-                uint64_t k = KEY_NONE;
-                const int c1 = min(TREE_FAN * g2 + TREE_FAN, nlev);
-                for (int c = TREE_FAN * g2; c < c1; ++c) {
-                    const uint64_t kc = lev_recs ? ((uint64_t)f2u(recs[(size_t)c * rec_stride]) << 32) |
-                                                       (uint64_t)f2u(recs[(size_t)c * rec_stride + 2])
-                                                 : nkp[c];
-                    k = umin64(k, kc);
-                }
-                nk_out[g2] = k;
-            }
-            __syncthreads();
-            for (int c = tid; c < nlev; c += T) {  // child scales
-                const float mc_ = lev_recs ? recs[(size_t)c * rec_stride] : u2f((uint32_t)(nkp[c] >> 32));
-                scale[c] = expf(-1.0f * (mc_ - u2f((uint32_t)(nk_out[c / TREE_FAN] >> 32))));
+            for (int g2 = wv; g2 < n2; g2 += NW) {  // one wave per node, lane = child: the key (minimum), the scales
+                const int c = TREE_FAN * g2 + lane;
+                const bool have = lane < TREE_FAN && c < nlev;
+                const uint64_t kc = !have ? KEY_NONE
+                                          : lev_recs ? ((uint64_t)f2u(recs[(size_t)c * rec_stride]) << 32) |
+                                                           (uint64_t)f2u(recs[(size_t)c * rec_stride + 2])
+                                                     : nkp[c];
+                const uint64_t k = wave_min_u64(kc);
+                if (lane == 0) nk_out[g2] = k;
+                if (have) scale[c] = expf(-1.0f * (u2f((uint32_t)(kc >> 32)) - u2f((uint32_t)(k >> 32))));
             }
             __syncthreads();
             for (int q = tid; q < n2 * cols; q += T) {  // (node, column) sums, child by child
                 const int g2 = (int)((uint32_t)q / (uint32_t)cols), jq = (int)((uint32_t)q % (uint32_t)cols);
-                const int c0 = TREE_FAN * g2, c1 = min(c0 + TREE_FAN, nlev);
+                const int c0 = TREE_FAN * g2, nc = min(TREE_FAN, nlev - c0);
+                const float* src = lev_recs ? recs + (size_t)c0 * rec_stride + off_of(jq) : lvp + (size_t)c0 * cols + jq;
+                const int sstride = lev_recs ? rec_stride : cols;
                 float a = 0.0f;
-                if (lev_recs) {
-                    const int oq = off_of(jq);
-                    for (int c = c0; c < c1; ++c) a = a + scale[c] * recs[(size_t)c * rec_stride + oq];
-                } else {
-                    for (int c = c0; c < c1; ++c) a = a + scale[c] * lvp[(size_t)c * cols + jq];
+                for (int cb = 0; cb < nc; cb += 8) {  // 8 children's loads in flight, then their adds in order
+                    float x[8], sc[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const bool ok = cb + u < nc;
+                        x[u] = ok ? src[(size_t)(cb + u) * sstride] : 0.0f;
+                        sc[u] = ok ? scale[c0 + cb + u] : 0.0f;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (cb + u < nc) a = a + sc[u] * x[u];
                 }
                 lv_out[(size_t)g2 * cols + jq] = a;
             }
