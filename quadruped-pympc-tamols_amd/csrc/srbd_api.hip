@@ -2256,3 +2256,24 @@ extern "C" int srbd_tamols_phases_raw(srbd_tamols_ctx* t, uint64_t* out) {
     TAM_TRY(t, hipMemcpy(out, t->d_dbg, sizeof(uint64_t) * 4 * TAMOLS_BPL * 8, hipMemcpyDeviceToHost));
     return SRBD_OK;
 }
+
+#ifdef SRBD_ROLLOUT_STAMPS
+// Probe build only: one merge launch of the context's last rollout records with the phase stamps on (merge_body's
+// MERGE_STAMP / MERGE_MARK: 32 words per block for blocks 0 and 1, s_memrealtime ticks of 10 ns).
+extern "C" int srbd_probe_merge_phases(srbd_ctx* c, uint64_t* host64) {
+    if (!c || !host64) return SRBD_E_INVALID;
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    uint64_t* d = nullptr;
+    HIP_TRY(c, hipMalloc((void**)&d, sizeof(uint64_t) * 64));
+    hipError_t e = hipMemsetAsync(d, 0, sizeof(uint64_t) * 64, c->stream);
+    if (e == hipSuccess) {
+        launch_merge(c->mc, c->d_in, merge_src(c), merge_nrec(c), c->wrec_stride, 0, c->d_noise[c->cur], nullptr,
+                     c->d_out, 0, c->stream, d);
+        e = hipMemcpyAsync(host64, d, sizeof(uint64_t) * 64, hipMemcpyDeviceToHost, c->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d);
+    HIP_TRY(c, e);
+    return SRBD_OK;
+}
+#endif

@@ -77,6 +77,19 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// Minimum of each 32-lane half (the reduction tree's level-0 nodes of 32 children): lanes 0..31 -> *lo, 32..63 -> *hi.
+__device__ __forceinline__ void half_wave_min_u64(uint64_t v, uint64_t* lo, uint64_t* hi) {
+    v = umin64(v, dpp_u64<0x111, 0xF>(v));
+    v = umin64(v, dpp_u64<0x112, 0xF>(v));
+    v = umin64(v, dpp_u64<0x114, 0xF>(v));
+    v = umin64(v, dpp_u64<0x118, 0xF>(v));
+    v = umin64(v, dpp_u64<0x142, 0xA>(v));
+    *lo = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 31) << 32) |
+          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 31);
+    *hi = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32) |
+          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+}
+
 // Block-wide min; every thread gets the result.  `red` holds blockDim/64 words.
 __device__ __forceinline__ uint64_t block_min_u64(uint64_t v, uint64_t* red) {
     v = wave_min_u64(v);
@@ -364,14 +377,15 @@ __device__ __forceinline__ void fold_node_lds(const ModelConst& mc, const float*
         for (int j = tid; j <= P; j += T) {
             const int off = j < P ? REC_HDR + j : 1;
             float a = 0.0f;
-            for (int cb = 0; cb < nb; cb += 8) {  // 8 children's LDS loads in flight, then their adds in order
+            int cb = 0;
+            for (; cb + 8 <= nb; cb += 8) {  // 8 children's LDS loads in flight, then their adds in order
                 float x[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) x[u] = cb + u < nb ? st[(size_t)(cb + u) * rec_stride + off] : 0.0f;
+                for (int u = 0; u < 8; ++u) x[u] = st[(size_t)(cb + u) * rec_stride + off];
 #pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (cb + u < nb) a = a + sc_sh[cb + u] * x[u];
+                for (int u = 0; u < 8; ++u) a = a + sc_sh[cb + u] * x[u];
             }
+            for (; cb < nb; ++cb) a = a + sc_sh[cb] * st[(size_t)cb * rec_stride + off];
             st_rec(&G[off], a);
         }
     }
@@ -457,11 +471,12 @@ __device__ __forceinline__ float wave_sum_f32(float v) { return lane_tree_f32<6>
 // Leaf sums of the weighted noise, thread form with SPB = 64 SPL samples per block (SPL = 2 / 4): wave w takes
 // columns w, w + NW, ...; lane l holds samples SPL l .. SPL l + SPL - 1 of a column (one coalesced load), pairs
 // them in registers (the tree's first log2 SPL levels) and the DPP rows finish each leaf (64 / SPL lanes): leaf b's
-// sum lands in lane (b + 1) 64 / SPL - 1.  Column P: the e alone.  CB columns' loads are in flight together.
+// sum lands in lane (b + 1) 64 / SPL - 1, which writes it into the block's records in LDS (rbuf; block_epilogue
+// stores them whole).  Column P: the e alone.  CB columns' loads are in flight together.
 template <int SPL>
 __device__ __forceinline__ void leaf_wsum_lanes(const ModelConst& mc, const StepInput* __restrict__ in,
                                                 const float* __restrict__ base, bool zs, const float* e_sh,
-                                                float* __restrict__ recs, int rec_stride, int rec0) {
+                                                float* rbuf, int rec_stride) {
     constexpr int CB = SPL == 4 ? 8 : 12;
     constexpr int LPL = 64 / SPL;  // lanes per leaf
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, NW = blockDim.x >> 6;
@@ -470,7 +485,7 @@ __device__ __forceinline__ void leaf_wsum_lanes(const ModelConst& mc, const Step
     float e[SPL];
 #pragma unroll
     for (int u = 0; u < SPL; ++u) e[u] = e_sh[SPL * lane + u];
-    float* rec = recs + (size_t)(rec0 + lane / LPL) * rec_stride;
+    float* rec = rbuf + (lane / LPL) * rec_stride;
     const bool writer = (lane % LPL) == LPL - 1;
     for (int j0 = w; j0 <= P; j0 += CB * NW) {
         float z[CB][SPL];
@@ -505,7 +520,7 @@ __device__ __forceinline__ void leaf_wsum_lanes(const ModelConst& mc, const Step
             else
                 a = p[0] + p[1];
             a = lane_tree_f32<SPL == 4 ? 4 : 5>(a);
-            if (writer) st_rec(&rec[j < P ? REC_HDR + j : 1], a);
+            if (writer) rec[j < P ? REC_HDR + j : 1] = a;
         }
     }
 }
@@ -601,6 +616,9 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
     __shared__ float e_sh[ZS ? 64 : 256];
     __shared__ uint64_t lmin[4];
     __shared__ uint64_t lel[CEMT ? 4 : 1][CEMT ? MAXK : 1];
+    // thread form with 2 / 4 leaves per block: the records are assembled in LDS and stored whole (consecutive
+    // lanes, consecutive words) instead of word by word from the lanes that finish each sum
+    __shared__ float rbuf[ZS ? 1 : 4 * ((REC_HDR + MAXP + 2 * MAXK + 3) & ~3)];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int NW = (int)blockDim.x >> 6, lpb = SPB >> 6;
     const int P = mc.P, K = mc.K;
@@ -637,27 +655,37 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
             leaf_wsum_cols<ZS>(mc, in, noise + k0, zst, zstride, zs, e_sh, recs + (size_t)blockIdx.x * rec_stride);
         else if constexpr (!ZS) {
             if (SPB == 128)
-                leaf_wsum_lanes<2>(mc, in, noise + k0, zs, e_sh, recs, rec_stride, blockIdx.x * lpb);
+                leaf_wsum_lanes<2>(mc, in, noise + k0, zs, e_sh, rbuf, rec_stride);
             else
-                leaf_wsum_lanes<4>(mc, in, noise + k0, zs, e_sh, recs, rec_stride, blockIdx.x * lpb);
+                leaf_wsum_lanes<4>(mc, in, noise + k0, zs, e_sh, rbuf, rec_stride);
         }
     }
     SRBD_RSTAMP(4);
+    const bool via_lds = !ZS && SPB > 64;
+    float* const grec = recs + (size_t)blockIdx.x * lpb * rec_stride;  // the block's lpb records, consecutive
+    auto put = [&](int b, int off, float v) {
+        if (via_lds)
+            rbuf[b * rec_stride + off] = v;
+        else
+            st_rec(&grec[(size_t)b * rec_stride + off], v);
+    };
     if (tid < lpb) {  // headers of leaf tid
-        float* rec = recs + (size_t)(blockIdx.x * lpb + tid) * rec_stride;
         const uint64_t m = lmin[tid];
-        st_rec(&rec[0], u2f((uint32_t)(m >> 32)));
-        st_rec(&rec[2], u2f((uint32_t)m));
-        if (rs) st_rec(&rec[1], 1.0f);
+        put(tid, 0, u2f((uint32_t)(m >> 32)));
+        put(tid, 2, u2f((uint32_t)m));
+        if (rs) put(tid, 1, 1.0f);
     }
-    if (sib >= 0 && key == lmin[sib >> 6]) st_rec(&recs[(size_t)(blockIdx.x * lpb + (sib >> 6)) * rec_stride + 3], tag);
+    if (sib >= 0 && key == lmin[sib >> 6]) put(sib >> 6, 3, tag);
     for (int i = tid; i < lpb * K; i += (int)blockDim.x) {  // keys
         const int b = i / K, q = i % K;
         uint64_t kk = lmin[b];
         if constexpr (CEMT) kk = K > 1 ? lel[b][q] : kk;
-        float* rec = recs + (size_t)(blockIdx.x * lpb + b) * rec_stride;
-        st_rec(&rec[REC_HDR + P + 2 * q], u2f((uint32_t)kk));
-        st_rec(&rec[REC_HDR + P + 2 * q + 1], u2f((uint32_t)(kk >> 32)));
+        put(b, REC_HDR + P + 2 * q, u2f((uint32_t)kk));
+        put(b, REC_HDR + P + 2 * q + 1, u2f((uint32_t)(kk >> 32)));
+    }
+    if (via_lds) {
+        __syncthreads();
+        for (int i = tid; i < lpb * rec_stride; i += (int)blockDim.x) st_rec(&grec[i], rbuf[i]);
     }
     if (grp.gsize > 1) {
         if constexpr (ZS) {

@@ -909,17 +909,31 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     uint64_t mine = KEY_NONE;
     float mtag = 0.0f;
     const int nhw = STAGE ? (nrec + 63) >> 6 : NW;  // waves that hold a record (staged: <= RPT * NW)
+    // the tree's first level rides along (srbd_core.h: 32 consecutive records per node, so a node is a 32-lane half
+    // of a wave here): its node keys (nkA) and each record's scale exp(-(m_r - m_node)), formed in this pass
     if (!STAGE || wv < nhw) {
 #pragma unroll
-        for (int i = 0; i < (STAGE ? MERGE_RPT : MERGE_RPT); ++i) {
+        for (int i = 0; i < MERGE_RPT; ++i) {
+            if (i * T >= nrec) break;
             const int r = tid + i * T;
+            uint64_t kk = KEY_NONE;
+            float m_r = 0.0f;
             if (r < nrec) {
                 const float* R = recs + (size_t)r * rec_stride;
-                const float m_r = R[0];
-                const uint64_t kk = ((uint64_t)f2u(m_r) << 32) | (uint64_t)f2u(R[2]);
+                m_r = R[0];
+                kk = ((uint64_t)f2u(m_r) << 32) | (uint64_t)f2u(R[2]);
                 const float tg = R[3];
                 mtag = kk < mine ? tg : mtag;
                 mine = umin64(mine, kk);
+            }
+            if (!rs) {
+                uint64_t nlo, nhi;
+                half_wave_min_u64(kk, &nlo, &nhi);
+                const uint64_t nk = lane < 32 ? nlo : nhi;
+                if (r < nrec) {
+                    if ((r & (TREE_FAN - 1)) == 0) nkA[r / TREE_FAN] = nk;
+                    scale[r] = expf(-1.0f * (m_r - u2f((uint32_t)(nk >> 32))));
+                }
             }
         }
         const uint64_t wmin = wave_min_u64(mine);
@@ -950,7 +964,8 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         uint64_t* nk_out = nkA;
         for (int L = 0; rank_out ? L < levels_up : nlev > 1; ++L) {
             const int n2 = (nlev + TREE_FAN - 1) / TREE_FAN;
-            for (int g2 = wv; g2 < n2; g2 += NW) {  // one wave per node, lane = child: the key (minimum), the scales
+            // level 0's keys and scales came with the beta pass; above it, one wave per node, lane = child
+            for (int g2 = wv; L > 0 && g2 < n2; g2 += NW) {
                 const int c = TREE_FAN * g2 + lane;
                 const bool have = lane < TREE_FAN && c < nlev;
                 const uint64_t kc = !have ? KEY_NONE
@@ -961,28 +976,31 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
                 if (lane == 0) nk_out[g2] = k;
                 if (have) scale[c] = expf(-1.0f * (u2f((uint32_t)(kc >> 32)) - u2f((uint32_t)(k >> 32))));
             }
-            __syncthreads();
+            if (L > 0) __syncthreads();
+            if (L == 1) MERGE_MARK(6);
             for (int q = tid; q < n2 * cols; q += T) {  // (node, column) sums, child by child
                 const int g2 = (int)((uint32_t)q / (uint32_t)cols), jq = (int)((uint32_t)q % (uint32_t)cols);
                 const int c0 = TREE_FAN * g2, nc = min(TREE_FAN, nlev - c0);
                 const float* src = lev_recs ? recs + (size_t)c0 * rec_stride + off_of(jq) : lvp + (size_t)c0 * cols + jq;
                 const int sstride = lev_recs ? rec_stride : cols;
                 float a = 0.0f;
-                for (int cb = 0; cb < nc; cb += 8) {  // 8 children's loads in flight, then their adds in order
+                int cb = 0;
+                for (; cb + 8 <= nc; cb += 8) {  // 8 children's loads in flight, then their adds in order
                     float x[8], sc[8];
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
-                        const bool ok = cb + u < nc;
-                        x[u] = ok ? src[(size_t)(cb + u) * sstride] : 0.0f;
-                        sc[u] = ok ? scale[c0 + cb + u] : 0.0f;
+                        x[u] = src[(size_t)(cb + u) * sstride];
+                        sc[u] = scale[c0 + cb + u];
                     }
 #pragma unroll
-                    for (int u = 0; u < 8; ++u)
-                        if (cb + u < nc) a = a + sc[u] * x[u];
+                    for (int u = 0; u < 8; ++u) a = a + sc[u] * x[u];
                 }
+                for (; cb < nc; ++cb) a = a + scale[c0 + cb] * src[(size_t)cb * sstride];
                 lv_out[(size_t)g2 * cols + jq] = a;
             }
             __syncthreads();
+            if (L == 0) MERGE_MARK(4);
+            if (L == 1) MERGE_MARK(7);
             lvp = lv_out;
             nkp = nk_out;
             lev_recs = false;
