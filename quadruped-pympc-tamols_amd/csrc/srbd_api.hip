@@ -27,11 +27,9 @@ using namespace srbd;
 namespace {
 thread_local std::string g_last_error;
 
-int rollout_threads(int n_local) {
-    if (n_local <= 16384) return 64;
-    if (n_local <= 65536) return 128;
-    return 256;
-}
+// The thread form always runs 256 samples (four leaves of the reduction tree) per block: its kernel is compiled for
+// that block size (the shapes it is the default for, N > 65 536, used it anyway).
+int rollout_threads(int) { return 256; }
 // Four lanes per sample unless the samples alone fill the GPU (measured crossover: zero-order
 // N ~ 65536, splines beyond 262144; scripts/kernel_sweep.py).  SRBD_ROLLOUT=thread|quad (read at create)
 // picks the other of the two forms at a shape (tests: both give the same costs bit for bit; measurement).
@@ -380,7 +378,9 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     c->nblocks = (mc.n_local + spb - 1) / spb;
     c->lpb = spb / LEAF_ROWS;
     c->nleaf = mc.nleaf;
-    if (c->nblocks > MAX_RECORDS) {
+    // the merge reads the level-1 records (the launch folds the leaves) or the leaf records
+    if (c->nblocks > MAX_RECORDS ||
+        (group_size(mc) > 1 ? (mc.nleaf + TREE_FAN - 1) / TREE_FAN : mc.nleaf) > MAX_RECORDS) {
         delete c;
         return fail(nullptr, SRBD_E_INVALID, "too many samples per rank");
     }

@@ -329,20 +329,9 @@ __device__ __forceinline__ float ld_rec(const float* p) {
 // Fold nb (<= TREE_FAN) child records staged in LDS (`st`, rec_stride apart, in order) into one node record `G`
 // (write-through stores): m = the children's minimum (cost, row) key, its record's tag; MPPI / CEM: s = sum_c
 // scale_c s_c and v[j] = sum_c scale_c v_c[j] child by child with scale_c = exp(-(m_c - m)); random sampling:
-// s = 1; the K smallest of the children's keys (one wave's K-round DPP minimum over their sorted lists).  The
-// merge kernel's tree levels (merge_body) and the host restatement (srbd_api.hip host_fold) are the same
-// arithmetic.  All threads of the block call it.
-template <int KM>
-__device__ __forceinline__ void fold_topk(const float* st, int rec_stride, int nb, int P, int K, uint64_t* out) {
-    const int lane = threadIdx.x & 63;
-    uint64_t lk[KM];
-    const float* R = st + (size_t)lane * rec_stride + REC_HDR + P;
-#pragma unroll
-    for (int q = 0; q < KM; ++q)
-        lk[q] = (lane < nb && q < K) ? ((uint64_t)__float_as_uint(R[2 * q + 1]) << 32) | __float_as_uint(R[2 * q])
-                                     : KEY_NONE;
-    wave_topk(lk, K, out);
-}
+// s = 1; the node's key (K == 1: the fold runs for MPPI / random sampling only, group_size).  The merge kernel's
+// tree levels (merge_body) and the host restatement (srbd_api.hip host_fold) are the same arithmetic.  All threads
+// of the block call it.
 __device__ __forceinline__ void fold_node_lds(const ModelConst& mc, const float* st, int rec_stride, int nb, float* G) {
     __shared__ float sc_sh[TREE_FAN];
     __shared__ float gh_sh[2];  // node m, tag
@@ -364,13 +353,7 @@ __device__ __forceinline__ void fold_node_lds(const ModelConst& mc, const float*
             gk_sh[MAXK] = gk;
         }
         if (have) sc_sh[tid] = rs ? 1.0f : expf(-1.0f * (m - beta));
-        if (K == 1) {
-            if (tid == 0) gk_sh[0] = gk;
-        } else if (K <= 10) {
-            fold_topk<10>(st, rec_stride, nb, P, K, gk_sh);
-        } else {
-            fold_topk<MAXK>(st, rec_stride, nb, P, K, gk_sh);
-        }
+        if (tid == 0) gk_sh[0] = gk;  // K == 1: the in-launch fold is not used for CEM (group_size)
     }
     __syncthreads();
     if (!rs) {  // column j < P: sum_c scale_c v_c[j]; column P: sum_c scale_c s_c (child order)
@@ -537,26 +520,6 @@ __device__ __forceinline__ void leaf_wsum_cols(const ModelConst& mc, const StepI
     if ((tid >> 6) == (T >> 6) - 1) {
         const float t = wave_sum_f32(e_sh[tid & 63]);
         if ((tid & 63) == 63) st_rec(&rec[1], t);
-    }
-    if constexpr (!ZS) {  // from global memory: the column's 16 float4 loads in flight together, the tree in place
-        for (int j = tid; j < P; j += T) {
-            const float sj = zs ? in->sigma[j] : 1.0f;  // x * 1 == x
-            const float4* row = reinterpret_cast<const float4*>(base + (size_t)j * ldn);
-            float x[64];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const float4 v = row[i];
-                x[4 * i] = v.x, x[4 * i + 1] = v.y, x[4 * i + 2] = v.z, x[4 * i + 3] = v.w;
-            }
-#pragma unroll
-            for (int i = 0; i < 32; ++i) x[i] = e_sh[2 * i] * (x[2 * i] * sj) + e_sh[2 * i + 1] * (x[2 * i + 1] * sj);
-#pragma unroll
-            for (int n = 16; n >= 1; n >>= 1)
-#pragma unroll
-                for (int i = 0; i < n; ++i) x[i] = x[2 * i] + x[2 * i + 1];
-            st_rec(&rec[REC_HDR + j], x[0]);
-        }
-        return;
     }
     for (int j = tid; j < P; j += T) {
         const float sj = zs ? in->sigma[j] : 1.0f;  // x * 1 == x

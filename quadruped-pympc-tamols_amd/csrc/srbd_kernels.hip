@@ -763,7 +763,7 @@ struct alignas(16) MergeShared {
     float tail_sh[4][40];
     float osh[sizeof(StepOutput) / sizeof(float)];  // the step outputs assembled for the burst
 };
-// smem: [STAGE: records] | scale[nrec_pad] | part[G*(ncol+1)] | erow[K*ncol] (merge_smem_bytes).  prestaged
+// smem: [STAGE: records] | scale[nrec_pad] | tree levels | node keys | erow[K*ncol] (merge_smem_bytes).  prestaged
 // (STAGE): the records are already in smem.  The staged body's sums use G = MERGE_STAGE_THREADS / (ncol + 1)
 // record groups whatever NT is, so a 256-thread block merges bit for bit as the 512-thread kernel does.
 template <int NT, bool STAGE>
@@ -820,15 +820,17 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     const bool do_tail = out && (!split || tailblk);
     const int cols = ncol + 1;
     const int nrec_pad = (nrec + 3) & ~3;
-    // the tree levels above the input records: n1 nodes at most (merge_smem_bytes)
-    const int n1 = (nrec + TREE_FAN - 1) / TREE_FAN, lvf = (n1 * cols + 3) & ~3;
+    // the tree levels above the input records (merge_smem_bytes): even levels in lvA / nkA (n1 nodes at most), odd
+    // levels in lvB / nkB (n1b), this block's cols columns each
+    const int n1 = (nrec + TREE_FAN - 1) / TREE_FAN, n1b = (n1 + TREE_FAN - 1) / TREE_FAN;
+    const int lvfA = (n1 * cols + 3) & ~3, lvfB = (n1b * cols + 3) & ~3;
     float* stage = smem;
     float* scale = STAGE ? smem + (size_t)nrec * rec_stride : smem;
     float* lvA = scale + nrec_pad;
-    float* lvB = lvA + lvf;
-    uint64_t* nkA = reinterpret_cast<uint64_t*>(lvB + lvf);  // 8-byte aligned: lvf and nrec_pad are multiples of 4
+    float* lvB = lvA + lvfA;
+    uint64_t* nkA = reinterpret_cast<uint64_t*>(lvB + lvfB);  // 8-byte aligned: lvf* and nrec_pad are multiples of 4
     uint64_t* nkB = nkA + n1;
-    float* erow = reinterpret_cast<float*>(nkB + n1);
+    float* erow = reinterpret_cast<float*>(nkB + n1b);
 
     // ---- L: loads.  The StepInput fields the output phases need are fetched first, so their latency
     // hides under the record loads instead of stalling the tail.
@@ -1621,8 +1623,11 @@ void launch_rollout(const ModelConst& mc, const StepInput* in, const float* nois
 
 int group_size(const ModelConst& mc) {
     // the level-1 fold runs in the launch when the merge would read more than GROUP_MIN_LEAVES leaf records, and
-    // the rank's rows start at a level-1 node (world 1, or an exchange level >= 1)
-    const bool use = mc.nleaf > GROUP_MIN_LEAVES && (mc.t_world == 1 || mc.t_xlevel >= 1);
+    // the rank's rows start at a level-1 node (world 1, or an exchange level >= 1).  Not for CEM: its folds (the
+    // K-key merge of 32 children on top of the sums) lengthen the rollout's tail by more than they take off the
+    // merge (C3 rollout 29.6 vs 38.3 us, merge 17 vs 13 us).
+    const bool use = mc.nleaf > GROUP_MIN_LEAVES && (mc.t_world == 1 || mc.t_xlevel >= 1) &&
+                     mc.method != SRBD_CEM_MPPI;
     return use ? TREE_FAN : 1;
 }
 
@@ -1644,11 +1649,12 @@ void launch_transpose(const float* src, int n, int P, int ldn, float* dst, hipSt
     hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, s, src, n, P, ldn, dst);
 }
 
-size_t merge_smem_bytes(int nrec, int P, int K) {
-    // scale[nrec_pad] | two tree-level value buffers of n1 x (P + 1) | two node-key arrays of n1 | erow[K P]
-    const int nrec_pad = (nrec + 3) & ~3, n1 = (nrec + TREE_FAN - 1) / TREE_FAN;
-    const size_t lvf = ((size_t)n1 * (P + 1) + 3) & ~(size_t)3;
-    return sizeof(float) * ((size_t)nrec_pad + 2 * lvf + 4 * (size_t)n1 + (size_t)K * P);
+size_t merge_smem_bytes(int nrec, int P, int K, int cols) {
+    // scale[nrec_pad] | tree-level values n1 x cols | n1b x cols | node keys n1 | n1b | erow[K P]  (merge_body)
+    if (cols <= 0) cols = P + 1;
+    const int nrec_pad = (nrec + 3) & ~3, n1 = (nrec + TREE_FAN - 1) / TREE_FAN, n1b = (n1 + TREE_FAN - 1) / TREE_FAN;
+    const size_t lvfA = ((size_t)n1 * cols + 3) & ~(size_t)3, lvfB = ((size_t)n1b * cols + 3) & ~(size_t)3;
+    return sizeof(float) * ((size_t)nrec_pad + lvfA + lvfB + 2 * (size_t)(n1 + n1b) + (size_t)K * P);
 }
 
 int merge_split_cols(const ModelConst& mc) {
@@ -1717,7 +1723,7 @@ int launch_merge(const ModelConst& mc, StepInput* in, const float* recs, int nre
     const int nb = cs ? merge_blocks(mc) : 1;
     size_t smem = 0;
     const bool stage = !cs && merge_stage_fits(nrec, rec_stride, mc.P, mc.K, &smem);
-    if (cs) smem = merge_smem_bytes(nrec, mc.P, mc.K);
+    if (cs) smem = merge_smem_bytes(nrec, mc.P, mc.K, (cs > mc.ntail ? cs : mc.ntail) + 1);
     launch_merge_kernel(stage, dim3(nb), smem, s, mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out,
                         chain, chain ? ctr_inc : 0, dbg, pub.flag, pub.seq, cs, pub.gate, levels_up);
     return nb;

@@ -76,7 +76,7 @@ void launch_rollout_ga_thread(const ModelConst& mc, const StepInput* in, const f
 void launch_rng(const ModelConst& mc, const StepInput* in, uint64_t seed, uint64_t ctr, int dev_ctr, int ctr_offset,
                 float* noise, hipStream_t s, const uint32_t* gate = nullptr);
 void launch_transpose(const float* src, int n, int P, int ldn, float* dst, hipStream_t s);
-size_t merge_smem_bytes(int nrec, int P, int K);
+size_t merge_smem_bytes(int nrec, int P, int K, int cols = 0);  // cols: a column-split block's columns + 1
 // Completion published to the host: after every output write is visible system-wide, the merge
 // stores `seq` into `flag` (host-mapped pinned memory); the host spins on it instead of a stream sync.
 struct Publish {

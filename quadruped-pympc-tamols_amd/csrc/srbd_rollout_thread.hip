@@ -46,7 +46,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
     const int S = CT ? ST : mc.S;
     const int PL = CT ? (KIND == SRBD_ZERO_ORDER ? 3 * HT : (KIND == SRBD_LINEAR_SPLINE ? 3 * (ST + 1) : 12 * ST))
                       : mc.PL;
-    const int tid = threadIdx.x, T = blockDim.x;
+    constexpr int T = 256;  // launched with 256 threads (rollout_threads)
+    const int tid = threadIdx.x;
     const int k = blockIdx.x * T + tid;  // local row (padded rows < ldn are readable zeros)
     const bool valid = k < mc.n_local;
     const size_t ldn = (size_t)mc.ldn;
@@ -259,6 +260,7 @@ static void launch_thread_t(const ModelConst& mc, const StepInput* in, const flo
                             int rec_stride, int threads, hipStream_t s, const RngJob* next, const GroupArgs& grp) {
     const RngJob job = next ? *next : RngJob{nullptr, 0, 0, 0, 0};
     const int extra = next ? (rng_grid(mc) < 1024 ? rng_grid(mc) : 1024) : 0;
+    threads = 256;  // the kernel is compiled for 256-thread blocks (rollout_threads)
     const int blocks = (mc.n_local + threads - 1) / threads;
     const dim3 grid(blocks + extra * (256 / threads));
     // thread form with the cost terms: runtime shapes only (the four-lane kernel is the default)
