@@ -529,7 +529,7 @@ def main(argv=None):
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     sys.path.insert(0, os.path.join(ROOT, "quadruped-pympc-tamols_amd"))
-    if world > 1:
+    if world > 1 or args.sharded:
         import torch  # noqa: F401  -- before libsrbd_hip.so: one HIP runtime per process (see _lib.py)
     import numpy as np
 
