@@ -321,6 +321,27 @@ __device__ __forceinline__ float ld_rec(const float* p) {
     return __uint_as_float(
         __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
+// Stage n floats (n even, src and dst 8-byte aligned) of records other blocks stored write-through: 8-byte sc1 loads,
+// U per thread in flight (half the load instructions and round trips of ld_rec).
+template <int U>
+__device__ __forceinline__ void stage_recs(const float* __restrict__ src, float* dst, int n) {
+    const int tid = threadIdx.x, T = blockDim.x, n2 = n >> 1;
+    const uint64_t* s2 = reinterpret_cast<const uint64_t*>(src);
+    uint64_t* d2 = reinterpret_cast<uint64_t*>(dst);
+    for (int i0 = 0; i0 < n2; i0 += U * T) {
+        uint64_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * T + tid;
+            v[u] = i < n2 ? __hip_atomic_load(s2 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * T + tid;
+            if (i < n2) d2[i] = v[u];
+        }
+    }
+}
 
 // ---- The reduction tree in the rollout launch (srbd_core.h): leaf records and the level-1 fold ----
 // Record words are stored write-through (st_rec) and read back with sc1 loads (ld_rec) by a level-1 node's last
@@ -392,7 +413,7 @@ __device__ __forceinline__ void fold_node_lds(const ModelConst& mc, const float*
 __device__ __forceinline__ bool level1_fold(const ModelConst& mc, const float* __restrict__ recs, int rec_stride,
                                             const GroupArgs& grp, int nroll, int lpb, float* st) {
     __shared__ int last_sh;
-    const int tid = threadIdx.x, T = blockDim.x;
+    const int tid = threadIdx.x;
     const int bpg = TREE_FAN / lpb;  // blocks per level-1 node
     const int g = (int)blockIdx.x / bpg;
     const int nblk = min(bpg, nroll - g * bpg);
@@ -406,24 +427,7 @@ __device__ __forceinline__ bool level1_fold(const ModelConst& mc, const float* _
     __syncthreads();
     if (!last_sh) return false;
     if (tid == 0) __hip_atomic_store(grp.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-    {  // stage the node's nb leaf records (sc1 loads, U per thread in flight)
-        constexpr int U = 16;
-        const int n = nb * rec_stride;
-        const float* src = recs + (size_t)g * TREE_FAN * rec_stride;
-        for (int i0 = 0; i0 < n; i0 += U * T) {
-            float v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int i = i0 + u * T + tid;
-                v[u] = i < n ? ld_rec(src + i) : 0.0f;
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int i = i0 + u * T + tid;
-                if (i < n) st[i] = v[u];
-            }
-        }
-    }
+    stage_recs<10>(recs + (size_t)g * TREE_FAN * rec_stride, st, nb * rec_stride);  // the node's nb leaf records
     __syncthreads();
     fold_node_lds(mc, st, rec_stride, nb, grp.grecs + (size_t)g * rec_stride);
     return true;
@@ -583,7 +587,7 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
     // lanes, consecutive words) instead of word by word from the lanes that finish each sum
     __shared__ float rbuf[ZS ? 1 : 4 * ((REC_HDR + MAXP + 2 * MAXK + 3) & ~3)];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int NW = (int)blockDim.x >> 6, lpb = SPB >> 6;
+    const int lpb = SPB >> 6;
     const int P = mc.P, K = mc.K;
     const int k0 = blockIdx.x * SPB;
     const bool rs = mc.method == SRBD_RANDOM_SAMPLING;

@@ -1412,21 +1412,7 @@ __device__ void final_merge(const ModelConst& mc, const StepInput* in, const flo
     if (threadIdx.x == 0) __hip_atomic_store(grp.gdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     MergeShared<NT>& sh = *reinterpret_cast<MergeShared<NT>*>(lds);
     float* smem = lds + (sizeof(MergeShared<NT>) + 15) / 16 * 4;  // 16-byte aligned
-    const int n = grp.ngroups * rec_stride;
-    constexpr int U = 16;  // sc1 loads in flight per thread (other CUs wrote the records)
-    for (int i0 = 0; i0 < n; i0 += U * NT) {
-        float v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = i0 + u * NT + (int)threadIdx.x;
-            v[u] = i < n ? ld_rec(grp.grecs + i) : 0.0f;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = i0 + u * NT + (int)threadIdx.x;
-            if (i < n) smem[i] = v[u];
-        }
-    }
+    stage_recs<10>(grp.grecs, smem, grp.ngroups * rec_stride);  // sc1 loads (other CUs wrote the records)
     __syncthreads();
     // sharded (grp.xa): pass 0 folds this rank's buffer, the exchange gathers the ranks' buffers (the exchange
     // level's node list), pass 1 merges them into the outputs.  One merge_body call site for both passes.
