@@ -23,7 +23,7 @@ int rng_grid(const ModelConst& mc);
 // the merge reads ceil(nleaf / TREE_FAN) records instead of nleaf.  gsize == TREE_FAN when on, 1 when off.
 struct XchgArgs;
 constexpr int GROUP_LDS_FLOATS = 6144;  // the last arriver stages its node's records in LDS (24 KB)
-constexpr int GROUP_MIN_LEAVES = 256;   // the merge reads the leaf records up to this many (C2: 157)
+constexpr int GROUP_MIN_LEAVES = 128;   // the merge reads the leaf records up to this many
 struct GroupArgs {
     float* grecs;   // ngroups x rec_stride (level-1 node records)
     uint32_t* cnt;  // ngroups arrival counters, zero between launches (each node's last arriver resets its own)
