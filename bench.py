@@ -396,6 +396,11 @@ def bench_single(_lib, w, args):
                                                           args.latency_steps)
         lat = list(l_us * 1e-6)
         k += args.latency_steps
+    # W more untimed steps in the same C loop right before the timed ones (the Python-driven warmup above ran
+    # before the latency sample)
+    _, best, state["sigma"] = ctx.bench_host_steps(states, refs, contacts, best, state["sigma"], keys.at(k), k,
+                                                   max(1, args.warmup))
+    k += max(1, args.warmup)
     t0 = time.perf_counter()
     t_us, best, state["sigma"] = ctx.bench_host_steps(states, refs, contacts, best, state["sigma"], keys.at(k), k,
                                                       args.steps)
@@ -430,7 +435,8 @@ def bench_single(_lib, w, args):
     kern = ctx.time_kernels(200)
     ctx.close()
     return dict(n_total=w.num_samples, n_local=w.num_samples, wall=wall, lat=lat, kern=kern, dev=dev,
-                transport=None, py_lat=py, armed=armed, other=other, arm_stats=(served, cancelled))
+                transport=None, py_lat=py, armed=armed, other=other, arm_stats=(served, cancelled),
+                timed_us=[round(float(x), 2) for x in t_us] if args.steps <= 64 else None)
 
 
 def bench_multi(_lib, w, args, rank, world, local_rank, scaling, steps=None, device_steps=None):
@@ -605,6 +611,7 @@ def main(argv=None):
                          "steps": len(out["py_lat"]), "path": "Context.step (ctypes) -> srbd_step"}
                         if out.get("py_lat") else None),
         "kernels_us": {k: round(v, 3) for k, v in out["kern"].items()},
+        **({"timed_step_us": out["timed_us"]} if out.get("timed_us") else {}),
         "roofline": roofline(w, out["n_local"], out["kern"], pmc_traffic(w.name)),
         **extra,
     }
