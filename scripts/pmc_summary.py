@@ -33,11 +33,12 @@ def per_kernel(d, counter):
 
 
 def short(name):
-    # the four-lane kernel's instantiations apart: <KIND, H, S, CEM, EXT, FM, KS> -- FM the in-launch final
-    # merge, KS the step input as kernel argument (both: the host step's launch)
+    # the four-lane kernel's instantiations apart: <KIND, H, S, CEM, EXT, FM, KS> -- FM 1 the in-launch final
+    # merge (2: with the sharded exchange), KS the step input as kernel argument (both: the host step's launch)
     if "rollout_quad_kernel<" in name:
         args = name.split("<", 1)[1].split(">")[0].replace(" ", "").split(",")
-        tag = ("_fm" if len(args) > 5 and args[5] == "true" else "") + ("_ks" if len(args) > 6 and args[6] == "true" else "")
+        fm = args[5] if len(args) > 5 else "0"
+        tag = ({"1": "_fm", "true": "_fm", "2": "_fmx"}.get(fm, "")) + ("_ks" if len(args) > 6 and args[6] == "true" else "")
         return "rollout_quad_kernel" + tag
     if "rollout_kernel<" in name:  # <KIND, H, S, CEM, EXT, KS>
         args = name.split("<", 1)[1].split(">")[0].replace(" ", "").split(",")
