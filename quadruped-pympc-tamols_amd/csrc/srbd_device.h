@@ -571,7 +571,9 @@ __device__ __forceinline__ void leaf_wsum_cols(const ModelConst& mc, const StepI
 //  (leaf_wsum_cols at one leaf per block, from the LDS stage `zst` (ZS: four-lane zero-order) or the SoA noise;
 //  leaf_wsum_lanes at 2 / 4 leaves per block).
 // Then the level-1 fold (grp.gsize > 1).  All threads call it; returns level1_fold's verdict (false without one).
-template <bool CEMT, bool ZS = false>
+// TF: the thread form (2 / 4 leaves per block: records assembled in LDS); the four-lane kernels pass false and carry
+// none of that LDS, nor (CEM: no in-launch fold) the fold's stage -- static LDS a fused launch's draw blocks share.
+template <bool CEMT, bool ZS = false, bool TF = false>
 __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepInput* __restrict__ in, const int SPB,
                                                int sib, bool valid, float cost, const float* __restrict__ noise,
                                                float* __restrict__ recs, int rec_stride, float tag,
@@ -585,7 +587,7 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
     __shared__ uint64_t lel[CEMT ? 4 : 1][CEMT ? MAXK : 1];
     // thread form with 2 / 4 leaves per block: the records are assembled in LDS and stored whole (consecutive
     // lanes, consecutive words) instead of word by word from the lanes that finish each sum
-    __shared__ float rbuf[ZS ? 1 : 4 * ((REC_HDR + MAXP + 2 * MAXK + 3) & ~3)];
+    __shared__ float rbuf[TF ? 4 * ((REC_HDR + MAXP + 2 * MAXK + 3) & ~3) : 1];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int lpb = SPB >> 6;
     const int P = mc.P, K = mc.K;
@@ -620,7 +622,7 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
         const bool zs = CEMT && zs_scaled(mc, in);
         if (SPB == 64)
             leaf_wsum_cols<ZS>(mc, in, noise + k0, zst, zstride, zs, e_sh, recs + (size_t)blockIdx.x * rec_stride);
-        else if constexpr (!ZS) {
+        else if constexpr (TF) {
             if (SPB == 128)
                 leaf_wsum_lanes<2>(mc, in, noise + k0, zs, e_sh, rbuf, rec_stride);
             else
@@ -628,7 +630,7 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
         }
     }
     SRBD_RSTAMP(4);
-    const bool via_lds = !ZS && SPB > 64;
+    const bool via_lds = TF && SPB > 64;
     float* const grec = recs + (size_t)blockIdx.x * lpb * rec_stride;  // the block's lpb records, consecutive
     auto put = [&](int b, int off, float v) {
         if (via_lds)
@@ -654,12 +656,14 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
         __syncthreads();
         for (int i = tid; i < lpb * rec_stride; i += (int)blockDim.x) st_rec(&grec[i], rbuf[i]);
     }
-    if (grp.gsize > 1) {
-        if constexpr (ZS) {
-            return level1_fold(mc, recs, rec_stride, grp, nroll, lpb, zst);
-        } else {
-            __shared__ float st[GROUP_LDS_FLOATS];
-            return level1_fold(mc, recs, rec_stride, grp, nroll, lpb, st);
+    if constexpr (!CEMT) {  // group_size: no in-launch fold for CEM
+        if (grp.gsize > 1) {
+            if constexpr (ZS) {
+                return level1_fold(mc, recs, rec_stride, grp, nroll, lpb, zst);
+            } else {
+                __shared__ float st[GROUP_LDS_FLOATS];
+                return level1_fold(mc, recs, rec_stride, grp, nroll, lpb, st);
+            }
         }
     }
     return false;

@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
     if (tid == 0) recs[blockIdx.x] = cost;
     return;
 #endif
-    block_epilogue<CEMT>(mc, in, T, tid, valid, cost, noise, recs, rec_stride, 0.0f, grp, nroll);
+    block_epilogue<CEMT, false, true>(mc, in, T, tid, valid, cost, noise, recs, rec_stride, 0.0f, grp, nroll);
 }
 
 template <int KIND>
@@ -251,7 +251,7 @@ __global__ void __launch_bounds__(256) rollout_ga_kernel(const ModelConst mc, co
     cost = cost + (df * 100.0f) * df;  // GA:500
     if (isnan(cost) || isinf(cost)) cost = 1000000.0f;
     if (valid && costs) costs[k] = cost;
-    block_epilogue<false>(mc, in, T, tid, valid, cost, noise, recs, rec_stride, f, grp, nroll);
+    block_epilogue<false, false, true>(mc, in, T, tid, valid, cost, noise, recs, rec_stride, f, grp, nroll);
 }
 
 // ------------------------------------------------------------------ launchers (srbd_launch.h)
