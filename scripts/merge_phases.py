@@ -45,11 +45,15 @@ def main():
         buf = np.zeros(64, np.uint64)
         assert lib.srbd_probe_merge_phases(ctx.h, buf.ctypes.data_as(C.POINTER(C.c_uint64))) == 0
         b0 = buf[:32].astype(np.int64)
-        rows.append({v: (b0[k] - b0[0]) / 100.0 if b0[k] else None for k, v in NAMES.items() if k != 0})
+        b1 = buf[32:].astype(np.int64)
+        r = {v: (b0[k] - b0[0]) / 100.0 if b0[k] else None for k, v in NAMES.items() if k != 0}
+        if b1[0]:  # block 1 (a column-split merge's first slice), relative to block 0's entry
+            r.update({"b1_" + v: (b1[k] - b0[0]) / 100.0 if b1[k] else None for k, v in NAMES.items()})
+        rows.append(r)
     ctx.close()
     out = {"workload": name, "n": n}
     for k in rows[0]:
-        vals = [r[k] for r in rows[5:] if r[k] is not None]
+        vals = [r[k] for r in rows[5:] if r.get(k) is not None]
         out[k] = round(float(np.median(vals)), 2) if vals else None
     print(json.dumps(out))
 

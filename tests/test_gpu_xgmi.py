@@ -3,7 +3,7 @@
 The box has one GPU, so the peers' mailboxes are connected in-process (srbd_xgmi_connect_local:
 the same kernel, device pointers instead of IPC-mapped ones).  The scenarios run in one worker
 process (tests/xgmi_worker.py, see its docstring for why): the merged step must equal the unsharded
-step (to reduction-order tolerance) and be bit-identical on every rank, across host steps and the
+step bit for bit (the fixed reduction tree) and be bit-identical on every rank, across host steps and the
 replayed device chain; a rank whose peer never arrives must fail after the bounded wait.
 """
 import json
@@ -28,7 +28,7 @@ def worker_results():
     return json.loads(p.stdout.strip().splitlines()[-1])
 
 
-@pytest.mark.parametrize("case", ["mppi", "cem_mppi", "random_sampling", "mppi_w3", "mppi_ga_w3", "c5_w8", "bench_w2",
-                                  "timeout"])
+@pytest.mark.parametrize("case", ["mppi", "cem_mppi", "random_sampling", "mppi_w3", "mppi_ga_w3", "c5_w8", "c5_weak_w2",
+                                  "bench_w2", "timeout"])
 def test_xgmi_exchange_in_process(worker_results, case):
     assert worker_results[case] == "ok", worker_results[case]

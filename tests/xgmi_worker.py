@@ -169,7 +169,10 @@ def main():
              ("mppi_w3", lambda: exchange_case("mppi", W=3, N=3001)),
              ("mppi_ga_w3", lambda: exchange_case("mppi", W=3, N=3001, ga=True)),
              # C5 (HyQReal bound MPPI, N=524 288) over 8 ranks of 65 536 rows: needs 8 hardware queues
-             ("c5_w8", lambda: exchange_case("mppi", W=8, N=524288, wkey="c5")), ("bench_w2", bench_case),
+             ("c5_w8", lambda: exchange_case("mppi", W=8, N=524288, wkey="c5")),
+             # bench.py's c5_weak line at N = 2: 524 288 rows per rank (thread form, level-1 folds in the launch,
+             # rank buffers of 8 level-2 nodes, merge_xchg_kernel)
+             ("c5_weak_w2", lambda: exchange_case("mppi", W=2, N=1048576, wkey="c5")), ("bench_w2", bench_case),
              ("timeout", timeout_case)]
     for name, fn in cases:
         try:
