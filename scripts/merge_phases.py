@@ -22,7 +22,7 @@ from quadruped_pympc_amd.synthetic import CONFIGS, inputs  # noqa: E402
 
 NAMES = {0: "entry", 7: "chunk0", 6: "staged", 1: "beta", 2: "sums", 3: "topk", 4: "outputs", 5: "published",
          16: "m_beta_scan", 17: "m_tail_prep", 18: "m_barrier", 19: "m_l0_keys", 20: "m_l0_sums", 22: "m_l1_keys",
-         23: "m_l1_sums", 21: "m_levels", 24: "m_end"}
+         23: "m_l1_sums", 21: "m_levels", 24: "m_end", 25: "k_minima", 26: "k_gather", 27: "k_loaded", 28: "k_wave_ranks", 29: "k_cand_ranks"}
 
 
 def main():
