@@ -413,7 +413,7 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     memset(c->h_in, 0, sizeof(StepInput));
     memset(c->h_out, 0, sizeof(StepOutput));
     const size_t noise_bytes = sizeof(float) * (size_t)mc.P * mc.ldn;
-    if ((e = hipMalloc((void**)&c->d_in, sizeof(StepInput))) != hipSuccess) return cleanup_fail("hipMalloc", e);
+    if ((e = hipMalloc((void**)&c->d_in, STEP_INPUT_ALLOC)) != hipSuccess) return cleanup_fail("hipMalloc", e);
     if ((e = hipMalloc((void**)&c->d_out, sizeof(StepOutput))) != hipSuccess) return cleanup_fail("hipMalloc", e);
     for (int b = 0; b < 2; ++b)
         if ((e = hipMalloc((void**)&c->d_noise[b], noise_bytes)) != hipSuccess) return cleanup_fail("hipMalloc", e);
@@ -439,7 +439,7 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     for (int b = 0; b < 2; ++b)
         if ((e = hipMemsetAsync(c->d_noise[b], 0, noise_bytes, c->stream)) != hipSuccess)
             return cleanup_fail("hipMemset", e);
-    if ((e = hipMemsetAsync(c->d_in, 0, sizeof(StepInput), c->stream)) != hipSuccess)
+    if ((e = hipMemsetAsync(c->d_in, 0, STEP_INPUT_ALLOC, c->stream)) != hipSuccess)
         return cleanup_fail("hipMemset", e);
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return cleanup_fail("hipStreamSynchronize", e);
     *out = c;

@@ -89,6 +89,20 @@ static_assert(sizeof(StepInput) % 16 == 0 && offsetof(StepInput, best) % 16 == 0
                   offsetof(StepInput, sigma) % 16 == 0,
               "StepInput is copied in 16-byte words (P is a multiple of 12, so P floats are too)");
 
+// A column-split merge's in-launch hand-off (merge_body), in device memory right after the context's StepInput
+// (d_in is allocated STEP_INPUT_ALLOC bytes): the slices' root sums of their columns and the weights' sum for the
+// tail block, the tail block's top-K keys for the slices.  Every word is stored once per launch as one 8-byte
+// atomic, tagged with the launch's epoch + 1 in its high half, so a reader polls the word itself (one memory
+// round trip, no flag behind the data); the tail block advances the epoch once it holds every slice's sums (every
+// slice read the epoch before storing them).
+struct SplitXchg {
+    uint32_t epoch;
+    uint32_t pad[3];
+    uint64_t elite[2 * MAXK];  // the top-K keys' low and high halves
+    uint64_t sums[MAXP + 1];   // column j: sum_r scale_r v_r[j]; [P]: sum_r scale_r s_r (float bits)
+};
+constexpr size_t STEP_INPUT_ALLOC = sizeof(StepInput) + sizeof(SplitXchg);
+
 // A host step's input passed by value as a kernel argument (KS rollout launches, srbd_step): StepInput's
 // prefix up to best[KSI_MAXP] -- no sigma, so MPPI / random sampling only.  The launch's block 0 writes it to
 // the device StepInput, which the merge and any later reader use; no upload kernel runs.

@@ -741,16 +741,21 @@ __device__ __forceinline__ void block_topk_rank(const float* __restrict__ recs, 
 // t.cnt[0, K K) = 0.  Caller syncs afterwards.
 template <int NT>
 __device__ __forceinline__ void block_topk_nodes(const float* __restrict__ recs, int nrec, int rec_stride, int P,
-                                                 int K, const uint64_t* nk, uint64_t* elite, TopkLds<NT>& t) {
+                                                 int K, const uint64_t* nk, uint64_t* elite, TopkLds<NT>& t,
+                                                 uint64_t* dbg = nullptr) {
     const int tid = threadIdx.x, KK = K * K;
+#define TOPK_MARK(i) \
+    if (dbg && tid == 0 && blockIdx.x < 2) dbg[32 * blockIdx.x + 25 + (i)] = __builtin_amdgcn_s_memrealtime()
     const int n1 = (nrec + TREE_FAN - 1) / TREE_FAN;
     if (tid < n1) {  // A
         const uint64_t y = nk[tid];
         int c = 0;
+#pragma unroll 8
         for (int g = 0; g < n1; ++g) c += nk[g] < y ? 1 : 0;
         if (c < K && y != KEY_NONE) t.sel[c] = tid;
     }
     __syncthreads();
+    TOPK_MARK(0);
     for (int i = tid; i < K * TREE_FAN; i += NT) {  // B
         const int sl = i / TREE_FAN, g = t.sel[sl];
         if (g < 0) continue;
@@ -771,13 +776,17 @@ __device__ __forceinline__ void block_topk_nodes(const float* __restrict__ recs,
             const int c = i / K, b = i - c * K;
             const uint64_t y = tab[c];
             if (y == KEY_NONE) continue;
+            const uint64_t* row = tab + b * K;
             int n = 0;
-            for (int q = 0; q < K; ++q) n += tab[b * K + q] < y ? 1 : 0;
+#pragma unroll
+            for (int q = 0; q < MAXK; ++q) n += q < K && row[q] < y ? 1 : 0;  // all loads in flight together
             if (n) atomicAdd(&t.cnt[c], n);
         }
     };
+    TOPK_MARK(1);
     table_ranks(t.cand);  // C
     __syncthreads();
+    TOPK_MARK(2);
     for (int c = tid; c < KK; c += NT) {
         const uint64_t y = t.cand[c];
         const int n = t.cnt[c];
@@ -794,8 +803,11 @@ __device__ __forceinline__ void block_topk_nodes(const float* __restrict__ recs,
     }
     if (tid < K) elite[tid] = KEY_NONE;
     __syncthreads();
+    TOPK_MARK(3);
     table_ranks(t.keys);
     __syncthreads();
+    TOPK_MARK(4);
+#undef TOPK_MARK
     for (int i = tid; i < KK; i += NT) {
         const uint64_t y = t.keys[i];
         const int n = t.cnt[i];
@@ -845,14 +857,14 @@ struct alignas(16) MergeShared {
 // smem: [STAGE: records] | scale[nrec_pad] | tree levels | node keys | erow[K*ncol] (merge_smem_bytes).  prestaged
 // (STAGE): the records are already in smem.  The staged body's sums use G = MERGE_STAGE_THREADS / (ncol + 1)
 // record groups whatever NT is, so a 256-thread block merges bit for bit as the 512-thread kernel does.
-template <int NT, bool STAGE>
+template <int NT, bool STAGE, bool SPLITX = false>
 __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __restrict__ in,
                                            const float* __restrict__ recs, int nrec, int rec_stride, int rows_in_rec,
                                            const float* __restrict__ noise, float* __restrict__ rank_out,
                                            StepOutput* __restrict__ out, int chain, int ctr_inc,
                                            uint64_t* __restrict__ dbg, uint32_t* __restrict__ flag, uint32_t seq,
                                            int split_cs, int fence_sys, MergeShared<NT>& sh, float* smem,
-                                           bool prestaged = false, int levels_up = 0) {
+                                           bool prestaged = false, int levels_up = 0, SplitXchg* xg = nullptr) {
     constexpr int NW = NT / 64;
     uint64_t* red = sh.red;
     uint64_t* elite = sh.elite;
@@ -990,7 +1002,29 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     uint64_t mine = KEY_NONE, kk0 = KEY_NONE;
     float mtag = 0.0f;
     // the top-K's record minima are these headers' keys: kept for it when one chunk holds them all
-    const bool pre_topk = K > 1 && !rank_out && (!tailblk || rs) && nrec <= T;
+    // Column split (SplitXchg after the StepInput): the slices fold every column's sums and publish them; the tail
+    // block folds none and reads its columns' sums back.  CEM: the tail block computes the top-K once and publishes
+    // it; the slices read it back (each slice recomputed it before: C3 15.5 -> see DESIGN).
+    const bool hand = SPLITX && split && !rs;  // SPLITX: merge_kernel, the only split launch, passes xg
+    const uint32_t ep = hand ? __hip_atomic_load(&xg->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
+    // a hand-off word (SplitXchg): polled until it carries this launch's tag, bounded (the tail block reports a
+    // timed-out wait as status 1)
+    int hand_late = 0;
+    auto poll = [&](const uint64_t* w) -> uint32_t {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint64_t v;
+        while ((uint32_t)((v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) != ep) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > XCHG_TIMEOUT_TICKS) {
+                hand_late = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        return (uint32_t)v;
+    };
+    auto tagged = [&](uint32_t x) { return ((uint64_t)ep << 32) | x; };
+    const bool topk_here = K > 1 && !rank_out && (!split || tailblk);
+    const bool pre_topk = topk_here && nrec <= T;
     const int nhw = STAGE ? (nrec + 63) >> 6 : NW;  // waves that hold a record (staged: <= RPT * NW)
     // the tree's first level rides along (srbd_core.h: 32 consecutive records per node, so a node is a 32-lane half
     // of a wave here): its node keys (nkA) and each record's scale exp(-(m_r - m_node)), formed in this pass
@@ -1035,7 +1069,8 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         }
     }
     MERGE_MARK(0);
-    if constexpr (!STAGE) tail_prep();
+    if constexpr (!STAGE)
+        if (!(SPLITX && hand && tailblk)) tail_prep();  // a hand-off tail block: after its top-K (off its critical path)
     MERGE_MARK(1);
     __syncthreads();
     MERGE_MARK(2);
@@ -1054,7 +1089,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     bool lev_recs = true;       // the current level is the input records
     const float* lvp = nullptr;  // values of the current level (lev_recs: the records)
     const uint64_t* nkp = nullptr;
-    if (!rs) {
+    if (!rs && !(hand && tailblk)) {
         float* lv_out = lvA;
         uint64_t* nk_out = nkA;
         for (int L = 0; rank_out ? L < levels_up : nlev > 1; ++L) {
@@ -1106,6 +1141,13 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         MERGE_MARK(5);
         if (!rank_out)  // the root
             for (int jj = tid; jj < cols; jj += T) Vs[jj] = lev_recs ? recs[off_of(jj)] : lvp[jj];
+    }
+    if (SPLITX && hand && !tailblk) {  // a slice publishes its columns' sums (block 1 also the weights' sum)
+        __syncthreads();
+        for (int i = tid; i <= ncol; i += T)
+            if (i < ncol || blockIdx.x == 1)
+                __hip_atomic_store(&xg->sums[i < ncol ? jc(i) : P], tagged(f2u(Vs[i])), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
     }
     MERGE_STAMP(2);
 
@@ -1167,14 +1209,28 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     // ---- 4. top-K keys (ascending; keys are unique).  The tail block of a CEM split never reads
     // elite rows (sigma belongs to the slices), so it skips them.
     const bool want_elite = !tailblk || rs;
-    if (K == 1 || !want_elite) {
+    if (K == 1) {
         if (tid == 0) elite[0] = bkey;
-        for (int e = 1 + tid; e < K; e += T) elite[e] = KEY_NONE;
+    } else if (SPLITX && !topk_here) {  // a CEM slice: the tail block's keys (halves: little-endian words)
+        if (tid < 2 * K) reinterpret_cast<uint32_t*>(elite)[tid] = poll(&xg->elite[tid]);
     } else {
         if (pre_topk)
-            block_topk_nodes<NT>(recs, nrec, rec_stride, P, K, nkA, elite, tk);
+            block_topk_nodes<NT>(recs, nrec, rec_stride, P, K, nkA, elite, tk, dbg);
         else
             block_topk_rank<NT>(recs, nrec, rec_stride, P, K, elite, tk);
+        if (SPLITX && split) {  // the tail block publishes them
+            __syncthreads();
+            if (tid < 2 * K)
+                __hip_atomic_store(&xg->elite[tid], tagged(reinterpret_cast<const uint32_t*>(elite)[tid]),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (SPLITX && hand && tailblk) {  // the tail block's sums: the slices'
+        if constexpr (!STAGE) tail_prep();
+        for (int i = tid; i <= ncol; i += T) Vs[i] = u2f(poll(&xg->sums[i < ncol ? jc(i) : P]));
+        __syncthreads();
+        // every slice has stored its sums, so every slice has read the epoch: advance it for the next launch
+        if (tid == 0) __hip_atomic_store(&xg->epoch, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     // record slot of every elite key (needed when rows travel inside the records)
@@ -1323,7 +1379,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
             ostore(&out->best_cost, beta);
             ostore(&out->best_index, __uint_as_float((uint32_t)bkey));
             ostore(&out->best_freq, tag_sh);
-            ostore(&out->status, __int_as_float(0));
+            ostore(&out->status, __int_as_float(SPLITX ? hand_late : 0));
             // chain: the next draws come from the device RNG.  (Split: slices read noise_scaled too, but a
             // chain's steps all run with it 0 already -- reset_noise_scaled -- so this store never changes it.)
             if (chain) in->noise_scaled = 0;
@@ -1388,8 +1444,8 @@ __global__ void __launch_bounds__(NT) merge_kernel(const ModelConst mc, StepInpu
     }
     __shared__ MergeShared<NT> sh;
     extern __shared__ __attribute__((aligned(16))) float dsm[];
-    merge_body<NT, STAGE>(mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag,
-                          seq, split_cs, fence_sys, sh, dsm, false, levels_up);
+    merge_body<NT, STAGE, true>(mc, in, recs, nrec, rec_stride, rows_in_rec, noise, rank_out, out, chain, ctr_inc, dbg, flag,
+                          seq, split_cs, fence_sys, sh, dsm, false, levels_up, reinterpret_cast<SplitXchg*>(in + 1));
 }
 
 // Sharded step without a collective launch (xGMI exchange).

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Phase stamps of one merge launch (probe build; measurement tool, GPU box).
 
-merge_body's stamps (block 0): 0 entry, 7 first record chunk loaded, 6 records staged, 1 beta, 2 tree sums done,
-3 top-K done, 4 outputs assembled, 5 published; marks 16 + i: 0 beta scan, 1 tail prep, 2 barrier, 3 / 4 level 0 keys /
-sums, 6 / 7 level 1 keys / sums, 5 tree levels, 8 end.  Prints one JSON line per workload: median over 30 launches of each stamp relative to entry (us).
+merge_body's stamps (blocks 0 and 1; b1_ = block 1, a column split's first slice): 0 entry, 7 first record chunk
+loaded, 6 records staged, 1 beta, 2 tree sums done, 3 top-K done, 4 outputs assembled, 5 published; marks 16 + i:
+0 beta scan, 1 tail prep, 2 barrier, 3 / 4 level 0 keys / sums, 6 / 7 level 1 keys / sums, 5 tree levels, 8 end;
+block_topk_nodes 25..29: selected nodes, candidate table, ranked, key lists loaded, done.  Prints one JSON line per workload: median over 30 launches of each stamp relative to entry (us).
 Usage: python scripts/merge_phases.py c2 [N]
 """
 import ctypes as C
@@ -22,7 +23,7 @@ from quadruped_pympc_amd.synthetic import CONFIGS, inputs  # noqa: E402
 
 NAMES = {0: "entry", 7: "chunk0", 6: "staged", 1: "beta", 2: "sums", 3: "topk", 4: "outputs", 5: "published",
          16: "m_beta_scan", 17: "m_tail_prep", 18: "m_barrier", 19: "m_l0_keys", 20: "m_l0_sums", 22: "m_l1_keys",
-         23: "m_l1_sums", 21: "m_levels", 24: "m_end", 25: "k_minima", 26: "k_gather", 27: "k_loaded", 28: "k_wave_ranks", 29: "k_cand_ranks"}
+         23: "m_l1_sums", 21: "m_levels", 24: "m_end", 25: "k_nodes", 26: "k_table", 27: "k_ranked", 28: "k_lists", 29: "k_done"}
 
 
 def main():
