@@ -21,8 +21,20 @@ __device__ uint64_t g_rstamp[RSTAMP_BLOCKS * RSTAMP_N];
             g_rstamp[blockIdx.x * RSTAMP_N + (i)] = __builtin_amdgcn_s_memrealtime(); \
         }                                                                               \
     } while (0)
+// The step launch's tail: level1_fold marks per block (no drain), and the final merger's own marks
+// (g_fstamp[0] = its block + 1, [1..4] final_merge, [32..63] its merge_body stamps).
+__device__ uint64_t g_lstamp[RSTAMP_BLOCKS * 4];
+__device__ uint64_t g_fstamp[64];
+#define SRBD_LSTAMP(i)                                                                            \
+    do {                                                                                          \
+        if (threadIdx.x == 0 && blockIdx.x < RSTAMP_BLOCKS)                                       \
+            g_lstamp[blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memrealtime();                    \
+    } while (0)
 #else
 #define SRBD_RSTAMP(i) \
+    do {               \
+    } while (0)
+#define SRBD_LSTAMP(i) \
     do {               \
     } while (0)
 #endif
@@ -418,17 +430,21 @@ __device__ __forceinline__ bool level1_fold(const ModelConst& mc, const float* _
     const int g = (int)blockIdx.x / bpg;
     const int nblk = min(bpg, nroll - g * bpg);
     const int nb = min(TREE_FAN, mc.nleaf - g * TREE_FAN);  // the node's leaves
+    SRBD_LSTAMP(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's record stores have completed
     __syncthreads();
+    SRBD_LSTAMP(1);
     if (tid == 0) {
         const uint32_t old = __hip_atomic_fetch_add(grp.cnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last_sh = old == (uint32_t)(nblk - 1);
     }
     __syncthreads();
     if (!last_sh) return false;
+    SRBD_LSTAMP(2);
     if (tid == 0) __hip_atomic_store(grp.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
     stage_recs<10>(recs + (size_t)g * TREE_FAN * rec_stride, st, nb * rec_stride);  // the node's nb leaf records
     __syncthreads();
+    SRBD_LSTAMP(3);
     fold_node_lds(mc, st, rec_stride, nb, grp.grecs + (size_t)g * rec_stride);
     return true;
 }

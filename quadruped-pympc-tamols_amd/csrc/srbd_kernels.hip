@@ -854,6 +854,42 @@ struct alignas(16) MergeShared {
     float tail_sh[4][40];
     float osh[sizeof(StepOutput) / sizeof(float)];  // the step outputs assembled for the burst
 };
+// The merge's tail lanes (0..3, component qc of the four-lane layout): the step inputs they use (tail_pre: fzref[0],
+// the legs' contact at step 0, p / v / rpy / omega and the feet, component qc), the force-independent part of the
+// predicted state (NMPC:752-784 via CMJ:93-174) and the ModelConst values of the final GRFs, into the lane's row of
+// tail_sh -- read back in one batch by the outputs phase.
+__device__ __forceinline__ void merge_tail_load(const StepInput* in, int qc, float* tail_pre) {
+    tail_pre[0] = in->fzref[0];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) tail_pre[1 + l] = in->contact[l][0];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tail_pre[5 + q] = in->state[3 * q + qc];  // p, v, rpy, omega
+#pragma unroll
+    for (int l = 0; l < 4; ++l) tail_pre[9 + l] = in->state[12 + 3 * l + qc];  // feet
+}
+__device__ __forceinline__ void merge_tail_lane(const ModelConst& mc, int qc, const float* tail_pre, float* row) {
+    const QuadLane L = quad_lane(mc, qc);
+    const QuadRB rb = quad_rb_prep(L, tail_pre[7], tail_pre[8]);
+    row[36] = L.Ii0;
+    row[37] = L.Ii1;
+    row[38] = L.Ii2;
+    row[39] = L.g;
+#pragma unroll
+    for (int i = 0; i < 13; ++i) row[i] = tail_pre[i];
+    row[13] = rb.er;
+    row[14] = rb.R0;
+    row[15] = rb.R1;
+    row[16] = rb.R2;
+    row[17] = rb.a1;
+    const int iv[5] = {mc.kind, mc.H, mc.PL, mc.S, mc.fidx};
+#pragma unroll
+    for (int i = 0; i < 5; ++i) row[18 + i] = __int_as_float(iv[i]);
+    const float fv[13] = {mc.fq, mc.fomq, mc.fa, mc.fb, mc.fc, mc.fd, mc.grf_min,
+                          mc.grf_max, mc.mu, mc.neg_mu, mc.inv_m, mc.dts[0], 0.0f};
+#pragma unroll
+    for (int i = 0; i < 13; ++i) row[23 + i] = fv[i];
+}
+
 // smem: [STAGE: records] | scale[nrec_pad] | tree levels | node keys | erow[K*ncol] (merge_smem_bytes).  prestaged
 // (STAGE): the records are already in smem.  The staged body's sums use G = MERGE_STAGE_THREADS / (ncol + 1)
 // record groups whatever NT is, so a 256-thread block merges bit for bit as the 512-thread kernel does.
@@ -874,12 +910,13 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     float* nb = sh.nb;
     float& tag_sh = sh.tag_sh;
     auto& tail_sh = sh.tail_sh;
+    const int sblk = split_cs > 0 ? (int)blockIdx.x : 0;  // stamps: a split launch's blocks 0 and 1, else this block
 #define MERGE_STAMP(i) \
-    if (dbg && threadIdx.x == 0 && blockIdx.x < 2) dbg[32 * blockIdx.x + (i)] = __builtin_amdgcn_s_memrealtime()
+    if (dbg && threadIdx.x == 0 && sblk < 2) dbg[32 * sblk + (i)] = __builtin_amdgcn_s_memrealtime()
     // finer marks (diagnostic build of the phases call only: dbg[16 + i])
 #define MERGE_MARK(i) MERGE_STAMP(16 + (i))
     MERGE_STAMP(0);
-    if (dbg && threadIdx.x == 0 && blockIdx.x < 2) dbg[32 * blockIdx.x + 8] = __builtin_amdgcn_s_memtime();  // clock
+    if (dbg && threadIdx.x == 0 && sblk < 2) dbg[32 * sblk + 8] = __builtin_amdgcn_s_memtime();  // clock
 
     // T: the launch's block size, a template constant (blockDim.x is a dependent load)
     const int tid = threadIdx.x, T = NT, lane = tid & 63, wv = tid >> 6;
@@ -929,41 +966,12 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     const int qc = tid < 3 ? tid : 2;  // tail lanes 0..3: component of the four-lane layout
     const bool tail_lane = do_tail && tid < 4;
     float tail_pre[13];  // kept in tail_sh across the merge (register pressure: 1024-thread block)
-    if (tail_lane) {
-        tail_pre[0] = in->fzref[0];
-#pragma unroll
-        for (int l = 0; l < 4; ++l) tail_pre[1 + l] = in->contact[l][0];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) tail_pre[5 + q] = in->state[3 * q + qc];  // p, v, rpy, omega
-#pragma unroll
-        for (int l = 0; l < 4; ++l) tail_pre[9 + l] = in->state[12 + 3 * l + qc];  // feet
-    }
+    if (tail_lane) merge_tail_load(in, qc, tail_pre);
     const float state_hi = (do_tail && tid >= 12 && tid < 24) ? in->state[tid] : 0.0f;
     // the predicted state's force-independent part (NMPC:752-784 via CMJ:93-174), formed while the
     // record loads are in flight
     auto tail_prep = [&]() {
-        if (tail_lane) {
-            const QuadLane L = quad_lane(mc, qc);
-            const QuadRB rb = quad_rb_prep(L, tail_pre[7], tail_pre[8]);
-            tail_sh[tid][36] = L.Ii0;
-            tail_sh[tid][37] = L.Ii1;
-            tail_sh[tid][38] = L.Ii2;
-            tail_sh[tid][39] = L.g;
-#pragma unroll
-            for (int i = 0; i < 13; ++i) tail_sh[tid][i] = tail_pre[i];
-            tail_sh[tid][13] = rb.er;
-            tail_sh[tid][14] = rb.R0;
-            tail_sh[tid][15] = rb.R1;
-            tail_sh[tid][16] = rb.R2;
-            tail_sh[tid][17] = rb.a1;
-            const int iv[5] = {mc.kind, mc.H, mc.PL, mc.S, mc.fidx};
-#pragma unroll
-            for (int i = 0; i < 5; ++i) tail_sh[tid][18 + i] = __int_as_float(iv[i]);
-            const float fv[13] = {mc.fq, mc.fomq, mc.fa, mc.fb, mc.fc, mc.fd, mc.grf_min,
-                                  mc.grf_max, mc.mu, mc.neg_mu, mc.inv_m, mc.dts[0], 0.0f};
-#pragma unroll
-            for (int i = 0; i < 13; ++i) tail_sh[tid][23 + i] = fv[i];
-        }
+        if (tail_lane) merge_tail_lane(mc, qc, tail_pre, tail_sh[tid]);
     };
     if constexpr (STAGE) {
         constexpr int U = 8;
@@ -1409,7 +1417,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     }
     MERGE_STAMP(5);
     MERGE_MARK(8);
-    if (dbg && threadIdx.x == 0 && blockIdx.x < 2) dbg[32 * blockIdx.x + 9] = __builtin_amdgcn_s_memtime();
+    if (dbg && threadIdx.x == 0 && sblk < 2) dbg[32 * sblk + 9] = __builtin_amdgcn_s_memtime();
 #undef MERGE_STAMP
 #undef MERGE_MARK
     if (flag) {  // every thread's output writes have completed before thread 0 publishes `seq`
@@ -1553,19 +1561,38 @@ template <int NT, bool XG>
 __device__ void final_merge(const ModelConst& mc, const StepInput* in, const float* noise, int rec_stride,
                             const GroupArgs& grp, float* lds) {
     __shared__ int fin;
+#ifdef SRBD_ROLLOUT_STAMPS
+    const uint64_t f1 = __builtin_amdgcn_s_memrealtime();
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's group record stores have completed
     __syncthreads();
+#ifdef SRBD_ROLLOUT_STAMPS
+    const uint64_t f2 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (threadIdx.x == 0) {
         const uint32_t old = __hip_atomic_fetch_add(grp.gdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         fin = old == (uint32_t)(grp.ngroups - 1);
     }
     __syncthreads();
     if (!fin) return;
+    uint64_t* dbg = nullptr;
+#ifdef SRBD_ROLLOUT_STAMPS
+    if (threadIdx.x == 0) {
+        g_fstamp[0] = blockIdx.x + 1;
+        g_fstamp[1] = f1;
+        g_fstamp[2] = f2;
+        g_fstamp[3] = __builtin_amdgcn_s_memrealtime();
+    }
+    dbg = g_fstamp + 32;
+#endif
     if (threadIdx.x == 0) __hip_atomic_store(grp.gdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     MergeShared<NT>& sh = *reinterpret_cast<MergeShared<NT>*>(lds);
     float* smem = lds + (sizeof(MergeShared<NT>) + 15) / 16 * 4;  // 16-byte aligned
     stage_recs<10>(grp.grecs, smem, grp.ngroups * rec_stride);  // sc1 loads (other CUs wrote the records)
     __syncthreads();
+#ifdef SRBD_ROLLOUT_STAMPS
+    if (threadIdx.x == 0) g_fstamp[4] = __builtin_amdgcn_s_memrealtime();
+#endif
     // sharded (grp.xa): pass 0 folds this rank's buffer, the exchange gathers the ranks' buffers (the exchange
     // level's node list), pass 1 merges them into the outputs.  One merge_body call site for both passes.
     int nrec = grp.ngroups, stride = rec_stride;
@@ -1573,7 +1600,8 @@ __device__ void final_merge(const ModelConst& mc, const StepInput* in, const flo
         const bool rank_pass = XG && pass == 0;
         float* mine = rank_pass ? grp.xa->stage + (size_t)grp.xa->rank * grp.xa->stride : nullptr;
         merge_body<NT, true>(mc, const_cast<StepInput*>(in), smem, nrec, stride, 0, noise, mine,
-                             rank_pass ? nullptr : grp.out, 0, 0, nullptr, rank_pass ? nullptr : grp.flag, grp.seq, 0,
+                             rank_pass ? nullptr : grp.out, 0, 0, rank_pass ? nullptr : dbg,
+                             rank_pass ? nullptr : grp.flag, grp.seq, 0,
                              grp.fence_sys, sh, smem, true, rank_pass ? grp.levels_up : 0);
         if (!rank_pass) return;
         __syncthreads();
@@ -1987,6 +2015,17 @@ void launch_div_selftest(const float* a, const float* b, int n, float* o, hipStr
 }  // namespace srbd
 
 #ifdef SRBD_ROLLOUT_STAMPS
+// Probe build only: the last step launch's tail stamps -- host[0, 64) g_fstamp, then n4 words of g_lstamp.
+extern "C" int srbd_probe_fstamps(uint64_t* host, int n4) {
+    if (n4 < 0 || n4 > srbd::RSTAMP_BLOCKS * 4) return -1;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(srbd::g_fstamp), sizeof(uint64_t) * 64) != hipSuccess) return -2;
+    return hipMemcpyFromSymbol(host + 64, HIP_SYMBOL(srbd::g_lstamp), sizeof(uint64_t) * n4) == hipSuccess ? 0 : -2;
+}
+extern "C" int srbd_probe_fstamps_clear() {
+    static uint64_t z[srbd::RSTAMP_BLOCKS * 4] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(srbd::g_fstamp), z, sizeof(uint64_t) * 64) != hipSuccess) return -2;
+    return hipMemcpyToSymbol(HIP_SYMBOL(srbd::g_lstamp), z, sizeof(z)) == hipSuccess ? 0 : -2;
+}
 // Probe build only: copy out the last rollout launch's block stamps (n <= RSTAMP_BLOCKS * RSTAMP_N).
 extern "C" int srbd_probe_rstamps(uint64_t* host, int n) {
     if (n > srbd::RSTAMP_BLOCKS * srbd::RSTAMP_N) return -1;
