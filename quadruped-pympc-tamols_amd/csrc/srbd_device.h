@@ -23,12 +23,12 @@ __device__ uint64_t g_rstamp[RSTAMP_BLOCKS * RSTAMP_N];
     } while (0)
 // The step launch's tail: level1_fold marks per block (no drain), and the final merger's own marks
 // (g_fstamp[0] = its block + 1, [1..4] final_merge, [32..63] its merge_body stamps).
-__device__ uint64_t g_lstamp[RSTAMP_BLOCKS * 4];
+__device__ uint64_t g_lstamp[RSTAMP_BLOCKS * 8];
 __device__ uint64_t g_fstamp[64];
 #define SRBD_LSTAMP(i)                                                                            \
     do {                                                                                          \
         if (threadIdx.x == 0 && blockIdx.x < RSTAMP_BLOCKS)                                       \
-            g_lstamp[blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memrealtime();                    \
+            g_lstamp[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();                    \
     } while (0)
 #else
 #define SRBD_RSTAMP(i) \
@@ -389,6 +389,7 @@ __device__ __forceinline__ void fold_node_lds(const ModelConst& mc, const float*
         if (tid == 0) gk_sh[0] = gk;  // K == 1: the in-launch fold is not used for CEM (group_size)
     }
     __syncthreads();
+    SRBD_LSTAMP(4);
     if (!rs) {  // column j < P: sum_c scale_c v_c[j]; column P: sum_c scale_c s_c (child order)
         for (int j = tid; j <= P; j += T) {
             const int off = j < P ? REC_HDR + j : 1;
@@ -405,6 +406,7 @@ __device__ __forceinline__ void fold_node_lds(const ModelConst& mc, const float*
             st_rec(&G[off], a);
         }
     }
+    SRBD_LSTAMP(5);
     if (tid == 0) {
         st_rec(&G[0], gh_sh[0]);
         if (rs) st_rec(&G[1], 1.0f);

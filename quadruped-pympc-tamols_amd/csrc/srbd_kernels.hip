@@ -2015,14 +2015,14 @@ void launch_div_selftest(const float* a, const float* b, int n, float* o, hipStr
 }  // namespace srbd
 
 #ifdef SRBD_ROLLOUT_STAMPS
-// Probe build only: the last step launch's tail stamps -- host[0, 64) g_fstamp, then n4 words of g_lstamp.
+// Probe build only: the last step launch's tail stamps -- host[0, 64) g_fstamp, then n4 words of g_lstamp (8 a block).
 extern "C" int srbd_probe_fstamps(uint64_t* host, int n4) {
-    if (n4 < 0 || n4 > srbd::RSTAMP_BLOCKS * 4) return -1;
+    if (n4 < 0 || n4 > srbd::RSTAMP_BLOCKS * 8) return -1;
     if (hipMemcpyFromSymbol(host, HIP_SYMBOL(srbd::g_fstamp), sizeof(uint64_t) * 64) != hipSuccess) return -2;
     return hipMemcpyFromSymbol(host + 64, HIP_SYMBOL(srbd::g_lstamp), sizeof(uint64_t) * n4) == hipSuccess ? 0 : -2;
 }
 extern "C" int srbd_probe_fstamps_clear() {
-    static uint64_t z[srbd::RSTAMP_BLOCKS * 4] = {};
+    static uint64_t z[srbd::RSTAMP_BLOCKS * 8] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(srbd::g_fstamp), z, sizeof(uint64_t) * 64) != hipSuccess) return -2;
     return hipMemcpyToSymbol(HIP_SYMBOL(srbd::g_lstamp), z, sizeof(z)) == hipSuccess ? 0 : -2;
 }

@@ -46,9 +46,9 @@ def main():
         lib.srbd_probe_fstamps_clear()
         best, _, _, _ = ctx.step(s, r, c, best, counter=k)
         rs = np.zeros(NB * NS, np.uint64)
-        fs = np.zeros(64 + NB * 4, np.uint64)
+        fs = np.zeros(64 + NB * 8, np.uint64)
         assert lib.srbd_probe_rstamps(rs.ctypes.data_as(C.POINTER(C.c_uint64)), rs.size) == 0
-        assert lib.srbd_probe_fstamps(fs.ctypes.data_as(C.POINTER(C.c_uint64)), NB * 4) == 0
+        assert lib.srbd_probe_fstamps(fs.ctypes.data_as(C.POINTER(C.c_uint64)), NB * 8) == 0
         st = rs.reshape(-1, NS).astype(np.int64)
         if fs[0] == 0:
             continue  # no final merge in this launch
@@ -56,12 +56,13 @@ def main():
         roll = st[:, 2] > 0
         t0 = st[st[:, 0] > 0, 0].min()
         us = lambda t: round((int(t) - t0) / 100.0, 2) if t else None  # noqa: E731
-        lst = fs[64:].reshape(-1, 4)
+        lst = fs[64:].reshape(-1, 8)
         row = {"last_leaf_sums": us(st[roll, 4].max()), "fm_block_leaf_sums": us(st[b, 4]),
                "fold_entry": us(lst[b, 0]), "fold_drained": us(lst[b, 1]), "fold_last": us(lst[b, 2]),
-               "fold_staged": us(lst[b, 3]), "fm_entry": us(fs[1]), "fm_drained": us(fs[2]), "fm_last": us(fs[3]),
+               "fold_staged": us(lst[b, 3]), "fold_headers": us(lst[b, 4]), "fold_sums": us(lst[b, 5]),
+               "fm_entry": us(fs[1]), "fm_drained": us(fs[2]), "fm_last": us(fs[3]),
                "fm_staged": us(fs[4])}
-        for i, nm in ((0, "m_entry"), (16, "m_beta_scan"), (17, "m_tail_prep"), (18, "m_barrier"), (1, "m_beta"),
+        for i, nm in ((0, "m_entry"), (6, "m_staged"), (16, "m_beta_scan"), (17, "m_tail_prep"), (18, "m_barrier"), (1, "m_beta"),
                       (20, "m_l0_sums"), (21, "m_levels"), (2, "m_sums"), (3, "m_topk"), (4, "m_outputs"),
                       (5, "m_published")):
             row[nm] = us(fs[32 + i])
