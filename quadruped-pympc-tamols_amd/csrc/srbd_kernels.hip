@@ -823,13 +823,14 @@ __device__ __forceinline__ void block_topk_nodes(const float* __restrict__ recs,
 //  4. top-K keys: per-thread sorted lists -> per-wave K-round DPP minima -> one wave over the 16
 //     wave lists; 5. elite rows -> LDS;  6. outputs: rank record and/or final step outputs; with
 //     `chain` the new parameters, sigma and RNG counter are written back into `in` (warm start).
-// Column-split launch (split_cs > 0, final step outputs only): the blocks share no data.  Every block
-// reads all record headers (beta, the sums' normaliser and the top-K are recomputed per block, in the
-// same order, so they agree bit for bit) but only its own columns of the weighted sums and elite rows:
-// block 0 (the tail block) the mc.tailc columns final_grf_pred decodes -- it writes those parameters,
-// the GRFs, the predicted state and the step scalars; block b >= 1 the columns [(b-1)cs, b cs) -- it
-// writes the other parameters and sigma.  Each block publishes flag[blockIdx.x] = seq.  This spreads
-// the record reads over CUs and drops the single block's serial column loop (C2: 8.8 -> see DESIGN).
+// Column-split launch (split_cs > 0, final step outputs only): every block reads all record headers (beta
+// and the normaliser are recomputed per block, in the same order, so they agree bit for bit); block b >= 1
+// (a slice) folds the columns [(b-1)cs, b cs) and writes the non-tail ones and sigma; block 0 (the tail
+// block) writes the mc.tailc columns final_grf_pred decodes, the GRFs, the predicted state and the step
+// scalars.  They meet through SplitXchg (srbd_core.h) inside the launch: the slices publish their root sums
+// and the tail block reads its columns' back (it folds none itself); for CEM the tail block computes the
+// top-K once and the slices read it back.  Each block publishes flag[blockIdx.x] = seq.  This spreads the
+// record reads over CUs and drops the single block's serial column loop (C2: 8.8 -> see DESIGN).
 // STAGE: the block first copies its records into LDS with 16-byte loads (one memory round trip,
 // a quarter of the load instructions of dword column reads; the whole per-block record array at C2 is
 // 157 x 152 floats = 95 KB) and every later phase reads them from LDS.

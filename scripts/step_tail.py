@@ -61,7 +61,7 @@ def main():
                "fold_entry": us(lst[b, 0]), "fold_drained": us(lst[b, 1]), "fold_last": us(lst[b, 2]),
                "fold_staged": us(lst[b, 3]), "fold_headers": us(lst[b, 4]), "fold_sums": us(lst[b, 5]),
                "fm_entry": us(fs[1]), "fm_drained": us(fs[2]), "fm_last": us(fs[3]),
-               "fm_staged": us(fs[4]), "dry_merge_start": us(fs[5]), "dry_merge_end": us(fs[6])}
+               "fm_staged": us(fs[4])}
         for i, nm in ((0, "m_entry"), (6, "m_staged"), (16, "m_beta_scan"), (17, "m_tail_prep"), (18, "m_barrier"), (1, "m_beta"),
                       (20, "m_l0_sums"), (21, "m_levels"), (2, "m_sums"), (3, "m_topk"), (4, "m_outputs"),
                       (5, "m_published")):
