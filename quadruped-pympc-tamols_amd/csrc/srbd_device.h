@@ -478,10 +478,15 @@ __device__ __forceinline__ float wave_sum_f32(float v) { return lane_tree_f32<6>
 // them in registers (the tree's first log2 SPL levels) and the DPP rows finish each leaf (64 / SPL lanes): leaf b's
 // sum lands in lane (b + 1) 64 / SPL - 1, which writes it into the block's records in LDS (rbuf; block_epilogue
 // stores them whole).  Column P: the e alone.  CB columns' loads are in flight together.
-template <int SPL>
+// Thread form, 4 leaves per block, MPPI on the device Philox stream: the first REGEN_QUADS column quads of the
+// draws are regenerated here (the same Philox4x32-10 call and Box-Muller pairs rng_item made, so the same bits)
+// instead of re-read; the rest are re-read.  That trades VALU issue for HBM reads where the launch has both to
+// spare (C5 issue 71.6 of 104 us, 656 MB read).
+constexpr int REGEN_QUADS = 16;  // C5 step launch 106.8 / 98.3 / 96.5 / 97.1 / 98.7 us at 0 / 12 / 16 / 20 / 24 of 36
+template <int SPL, bool RG>
 __device__ __forceinline__ void leaf_wsum_lanes(const ModelConst& mc, const StepInput* __restrict__ in,
                                                 const float* __restrict__ base, bool zs, const float* e_sh,
-                                                float* rbuf, int rec_stride) {
+                                                float* rbuf, int rec_stride, int k0) {
     constexpr int CB = SPL == 4 ? 8 : 12;
     constexpr int LPL = 64 / SPL;  // lanes per leaf
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, NW = blockDim.x >> 6;
@@ -492,7 +497,39 @@ __device__ __forceinline__ void leaf_wsum_lanes(const ModelConst& mc, const Step
     for (int u = 0; u < SPL; ++u) e[u] = e_sh[SPL * lane + u];
     float* rec = rbuf + (lane / LPL) * rec_stride;
     const bool writer = (lane % LPL) == LPL - 1;
-    for (int j0 = w; j0 <= P; j0 += CB * NW) {
+    int jreg = 0;  // columns [0, jreg) regenerated
+    if constexpr (RG && SPL == 4) {
+        if (mc.method == SRBD_MPPI && mc.rng == RNG_PHILOX && in->noise_scaled == 0 && 4 * REGEN_QUADS <= P) {
+            const uint32_t key0 = in->seed_lo, key1 = in->seed_hi, c2 = in->ctr_lo, c3 = in->ctr_hi;
+            for (int q = w; q < REGEN_QUADS; q += NW) {
+                float zq[4][SPL];  // [column 4q + i][row u]
+#pragma unroll
+                for (int u = 0; u < SPL; ++u) {
+                    const int k = k0 + SPL * lane + u, r = mc.row0 + k;
+                    uint32_t c[4] = {(uint32_t)(r - 1), (uint32_t)q, c2, c3};
+                    philox4x32_10(c, key0, key1);
+                    float v[4];
+                    box_muller(c[0], c[1], v[0], v[1]);
+                    box_muller(c[2], c[3], v[2], v[3]);
+                    // rng_item's value; row 0 (the warm start) and rows past n_local hold zeros in the buffer
+                    const bool live = r > 0 && k < mc.n_local;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) zq[i][u] = live ? mc.sigma_mppi * v[i] : 0.0f;
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float p[SPL];
+#pragma unroll
+                    for (int u = 0; u < SPL; ++u) p[u] = e[u] * (zq[i][u] * 1.0f);  // the read path's x * 1
+                    float a = (p[0] + p[1]) + (p[2] + p[3]);
+                    a = lane_tree_f32<4>(a);
+                    if (writer) rec[REC_HDR + 4 * q + i] = a;
+                }
+            }
+            jreg = 4 * REGEN_QUADS;
+        }
+    }
+    for (int j0 = jreg + w; j0 <= P; j0 += CB * NW) {
         float z[CB][SPL];
 #pragma unroll
         for (int b = 0; b < CB; ++b) {
@@ -591,7 +628,7 @@ __device__ __forceinline__ void leaf_wsum_cols(const ModelConst& mc, const StepI
 // Then the level-1 fold (grp.gsize > 1).  All threads call it; returns level1_fold's verdict (false without one).
 // TF: the thread form (2 / 4 leaves per block: records assembled in LDS); the four-lane kernels pass false and carry
 // none of that LDS, nor (CEM: no in-launch fold) the fold's stage -- static LDS a fused launch's draw blocks share.
-template <bool CEMT, bool ZS = false, bool TF = false>
+template <bool CEMT, bool ZS = false, bool TF = false, bool RG = false>
 __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepInput* __restrict__ in, const int SPB,
                                                int sib, bool valid, float cost, const float* __restrict__ noise,
                                                float* __restrict__ recs, int rec_stride, float tag,
@@ -642,9 +679,9 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
             leaf_wsum_cols<ZS>(mc, in, noise + k0, zst, zstride, zs, e_sh, recs + (size_t)blockIdx.x * rec_stride);
         else if constexpr (TF) {
             if (SPB == 128)
-                leaf_wsum_lanes<2>(mc, in, noise + k0, zs, e_sh, rbuf, rec_stride);
+                leaf_wsum_lanes<2, RG>(mc, in, noise + k0, zs, e_sh, rbuf, rec_stride, k0);
             else
-                leaf_wsum_lanes<4>(mc, in, noise + k0, zs, e_sh, rbuf, rec_stride);
+                leaf_wsum_lanes<4, RG>(mc, in, noise + k0, zs, e_sh, rbuf, rec_stride, k0);
         }
     }
     SRBD_RSTAMP(4);

@@ -153,7 +153,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
     if (tid == 0) recs[blockIdx.x] = cost;
     return;
 #endif
-    block_epilogue<CEMT, false, true>(mc, in, T, tid, valid, cost, noise, recs, rec_stride, 0.0f, grp, nroll);
+    // RG: zero-order MPPI regenerates part of its draws in the epilogue (leaf_wsum_lanes, REGEN_QUADS)
+    block_epilogue<CEMT, false, true, KIND == SRBD_ZERO_ORDER && !CEMT && !EXT>(mc, in, T, tid, valid, cost, noise,
+                                                                               recs, rec_stride, 0.0f, grp, nroll);
 }
 
 template <int KIND>
