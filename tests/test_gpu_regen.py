@@ -1,0 +1,46 @@
+"""GPU: the thread-form epilogue's regenerated draws (srbd_device.h leaf_wsum_lanes, REGEN_QUADS).
+
+Zero-order MPPI on the device Philox stream regenerates part of its draws in the epilogue instead of re-reading
+them.  A step with device draws must equal, bit for bit, the same step fed those draws as injected noise (read
+back with srbd_draw_noise), which takes the read path for every column.
+"""
+import numpy as np
+import pytest
+
+from helpers import f32, make_case, product_cfg
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from quadruped_pympc_amd import _lib
+
+    if _lib.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X")
+    return _lib
+
+
+@pytest.mark.parametrize("wkey,N,H", [("c2", 262144, 12), ("c5", 524288, 12), ("c2", 100003, 10)])
+def test_regenerated_draws_equal_read_draws(lib, wkey, N, H):
+    case = make_case(wkey, N=N, method="mppi", par="zero_order", H=H, seed=N % 71)
+    seed, counter = 1234, 5
+    cx = lib.Context(product_cfg(case))
+    try:
+        drawn = cx.draw_noise(seed, counter)
+        assert not np.any(drawn[0])  # row 0: the warm start
+        b_dev, _, r_dev, c_dev = cx.step(case["state"], case["ref"], case["contact"], case["best"], seed=seed,
+                                         counter=counter, want_costs=True)
+    finally:
+        cx.close()
+    cx = lib.Context(product_cfg(case))
+    try:
+        b_inj, _, r_inj, c_inj = cx.step(case["state"], case["ref"], case["contact"], case["best"],
+                                         noise=np.ascontiguousarray(drawn), want_costs=True)
+    finally:
+        cx.close()
+    np.testing.assert_array_equal(c_dev, c_inj)
+    assert r_dev.best_index == r_inj.best_index
+    np.testing.assert_array_equal(b_dev, b_inj)
+    np.testing.assert_array_equal(np.array(r_dev.grf, f32), np.array(r_inj.grf, f32))
+    np.testing.assert_array_equal(np.array(r_dev.predicted_state, f32), np.array(r_inj.predicted_state, f32))
