@@ -1013,7 +1013,7 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     // the top-K's record minima are these headers' keys: kept for it when one chunk holds them all
     // Column split (SplitXchg after the StepInput): the slices fold every column's sums and publish them; the tail
     // block folds none and reads its columns' sums back.  CEM: the tail block computes the top-K once and publishes
-    // it; the slices read it back (each slice recomputed it before: C3 15.5 -> see DESIGN).
+    // it; the slices read it back (each slice recomputed both before: C3 merge 15.5 -> 12.8 us).
     const bool hand = SPLITX && split && !rs;  // SPLITX: merge_kernel, the only split launch, passes xg
     const uint32_t ep = hand ? __hip_atomic_load(&xg->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
     // a hand-off word (SplitXchg): polled until it carries this launch's tag, bounded (the tail block reports a
