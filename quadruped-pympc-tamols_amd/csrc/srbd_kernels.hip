@@ -1622,15 +1622,15 @@ size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride) {
     return (sizeof(MergeShared<256>) + 15) / 16 * 16 + (a > b ? a : b);
 }
 
-// The zero-order four-lane kernel with the LDS noise stage (ZST: H 10 / 12, no cost terms), MPPI / random
-// sampling, grouped records, and the merge's LDS inside the stage (64 x 12 H floats).
-// The step input as a kernel argument (StepInputK): the zero-order four-lane kernel with the LDS noise stage,
-// MPPI / random sampling (no sigma in the argument), P <= KSI_MAXP; SRBD_KS=0 disables (read per context).
+// The step input as a kernel argument (StepInputK): zero-order H 10 / 12 rollouts (four-lane with the LDS noise
+// stage, or the thread form), MPPI / random sampling (no sigma in the argument), P <= KSI_MAXP.
 bool ks_ok(const ModelConst& mc, int mode) {
     if ((mode != ROLLOUT_QUAD && mode != ROLLOUT_THREAD) || mc.kind != SRBD_ZERO_ORDER) return false;
     return (mc.H == 10 || mc.H == 12) && mc.method != SRBD_CEM_MPPI && mc.P <= KSI_MAXP;
 }
 
+// The in-launch final merge: the zero-order four-lane kernel with the LDS noise stage (H 10 / 12), MPPI / random
+// sampling, grouped records, and the merge's LDS inside the stage (64 x (12 H + 1) floats).
 bool final_merge_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride) {
     // (the gait-adaptive rollout and the cost terms, which can be switched on later, are checked per launch)
     if (mode != ROLLOUT_QUAD || mc.kind != SRBD_ZERO_ORDER) return false;
