@@ -310,6 +310,10 @@ int srbd_debug_merge_phases(srbd_ctx* ctx, int32_t iters, float* out_us);
 /* Self-test of the correctly rounded division used in the rollout (a/b; b == 3 uses the constant
  * path).  Host results always; device results when out_dev != NULL (needs a GPU). */
 int srbd_selftest_div(const float* a, const float* b, int32_t n, float* out_host, float* out_dev);
+/* Self-test of the reference noise stream's log1p (jax.random.normal's erf_inv argument, NMPC:654/811/957): the
+ * float of log1p(t) evaluated as float64 (t in (-1, 0]), on the host (out_host, with *nfallback = the arguments the
+ * float64 log1p itself decided) and / or the device (out_dev).  Either output may be NULL. */
+int srbd_selftest_log1p(const float* t, int32_t n, float* out_host, float* out_dev, int64_t* nfallback);
 
 /* ------------------------------------------------------------------ TAMOLS */
 typedef struct srbd_tamols_params {

@@ -110,6 +110,9 @@ struct srbd_ctx {
     // in-launch final merge (final_merge_ok): the rollout's last group writes the host step's outputs
     bool final_merge = false;
     uint32_t* d_gdone = nullptr;
+    // fast_tail (fast_tail_ok, SRBD_FAST_TAIL=0 turns it off): the node records the folders hand over, tagged words
+    bool fast_tail = false;
+    uint64_t* d_gtag = nullptr;
     // host steps pass the step input to the rollout as a kernel argument (ks_ok): no upload kernel
     bool ks = false;
     hipGraphExec_t g_dev2 = nullptr, g_dev1 = nullptr;
@@ -433,6 +436,12 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
         if ((e = hipMalloc((void**)&c->d_gdone, sizeof(uint32_t))) != hipSuccess ||
             (e = hipMemsetAsync(c->d_gdone, 0, sizeof(uint32_t), c->stream)) != hipSuccess)
             c->final_merge = false;
+        const char* ft = getenv("SRBD_FAST_TAIL");
+        if (c->final_merge && fast_tail_ok(mc, c->mode, c->ngroups, c->wrec_stride) && !(ft && !strcmp(ft, "0"))) {
+            const size_t tb = sizeof(uint64_t) * (size_t)c->ngroups * (REC_HDR + mc.P);
+            c->fast_tail = hipMalloc((void**)&c->d_gtag, tb) == hipSuccess &&
+                           hipMemsetAsync(c->d_gtag, 0, tb, c->stream) == hipSuccess;
+        }
         if ((e = hipMemsetAsync(c->d_gcnt, 0, sizeof(uint32_t) * (size_t)c->ngroups, c->stream)) != hipSuccess)
             return cleanup_fail("hipMemset", e);
     }
@@ -470,6 +479,7 @@ extern "C" void srbd_destroy(srbd_ctx* c) {
     (void)hipFree(c->d_grec);
     (void)hipFree(c->d_gcnt);
     (void)hipFree(c->d_gdone);
+    (void)hipFree(c->d_gtag);
     (void)hipFree(c->d_ga_freq);
     if (c->h_in) (void)hipHostFree(c->h_in);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -592,6 +602,10 @@ static int enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput
         grp.gdone = c->d_gdone;
         grp.ngroups = c->ngroups;
         grp.fence_sys = merge_fence_sys();
+        if (c->fast_tail) {
+            grp.fast = 1;
+            grp.gtag = c->d_gtag;
+        }
         launch_rollout(mc, c->d_in, c->d_noise[buf], costs ? costs : c->d_costs, c->d_wrec, c->wrec_stride, c->mode,
                        c->threads, c->stream, fuse_next ? &next : nullptr, grp);
         return 1;
@@ -642,6 +656,21 @@ static int wait_published(srbd_ctx* c, uint32_t seq, int nflags = 1, int* cancel
         }
         __builtin_ia32_pause();
     }
+}
+
+// A step whose merge reported a timed-out in-launch hand-off (StepOutput::status != 0: fast_tail -1, the column
+// split's tail block / a slice 1 / 2): drain the stream, so no block of that launch is still writing, reset the
+// hand-off state (the split's epoch and tagged words, the arrival counts) and fail the call.  The host zeroes
+// status before each launch (the column split only ORs its late bits in).
+static int check_handoff(srbd_ctx* c) {
+    if (__atomic_load_n(&c->h_out->status, __ATOMIC_ACQUIRE) == 0) return SRBD_OK;
+    const int st = c->h_out->status;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, hipMemset(reinterpret_cast<char*>(c->d_in) + sizeof(StepInput), 0, sizeof(SplitXchg)));
+    if (c->d_gcnt) HIP_TRY(c, hipMemset(c->d_gcnt, 0, sizeof(uint32_t) * (size_t)c->ngroups));
+    if (c->d_gdone) HIP_TRY(c, hipMemset(c->d_gdone, 0, sizeof(uint32_t)));
+    c->h_out->status = 0;
+    return fail(c, SRBD_E_HIP, "merge hand-off timed out (status " + std::to_string(st) + ")");
 }
 
 static int copy_out(srbd_ctx* c, float* best, float* sigma, srbd_result* out) {
@@ -720,6 +749,7 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
         return fail(c, rc, "invalid step arguments");
     }
     c->h_in->noise_scaled = noise ? 1 : 0;
+    c->h_out->status = 0;  // check_handoff
     const bool want_arm = c->arm_mode && !noise;
     int nflags = 1;
     uint32_t seq = 0;
@@ -803,6 +833,7 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         if (want_arm) arm();
     }
+    if ((rc = check_handoff(c))) return rc;
     c->input_ready = true;
     return copy_out(c, best, sigma, out);
 }
@@ -1907,6 +1938,10 @@ extern "C" int srbd_time_launch(srbd_ctx* c, int32_t which, int32_t iters, float
                     grp.gdone = c->d_gdone;
                     grp.ngroups = c->ngroups;
                     grp.fence_sys = merge_fence_sys();
+                    if (c->fast_tail) {
+                        grp.fast = 1;
+                        grp.gtag = c->d_gtag;
+                    }
                 }
                 launch_rollout(mc, c->d_in, c->d_noise[0], c->d_costs, c->d_wrec, c->wrec_stride, c->mode, c->threads,
                                c->stream, fuse ? &next : nullptr, grp);
@@ -1995,6 +2030,37 @@ extern "C" int srbd_selftest_div(const float* a, const float* b, int32_t n, floa
         hipError_t e = hipMemcpy(out_dev, dout, bytes, hipMemcpyDeviceToHost);
         (void)hipFree(da);
         (void)hipFree(db);
+        (void)hipFree(dout);
+        if (e != hipSuccess) return fail(nullptr, SRBD_E_HIP, hipGetErrorString(e));
+    }
+    return SRBD_OK;
+}
+
+// The JAX normal's log1p (srbd_jaxrng.h log1p_fast) on the host and / or the device; *nfallback (host) counts the
+// arguments the float64 log1p decided.
+extern "C" int srbd_selftest_log1p(const float* t, int32_t n, float* out_host, float* out_dev, int64_t* nfallback) {
+    if (!t || n < 0) return SRBD_E_INVALID;
+    if (out_host) {
+        int64_t fb = 0;
+        for (int i = 0; i < n; ++i) {
+            float f;
+            if (!log1p_try(t[i], &f)) {
+                f = log1p_cr(t[i]);
+                ++fb;
+            }
+            out_host[i] = f;
+        }
+        if (nfallback) *nfallback = fb;
+    }
+    if (out_dev) {
+        float *dt = nullptr, *dout = nullptr;
+        const size_t bytes = sizeof(float) * (size_t)(n > 0 ? n : 1);
+        if (hipMalloc((void**)&dt, bytes) != hipSuccess || hipMalloc((void**)&dout, bytes) != hipSuccess)
+            return fail(nullptr, SRBD_E_NODEVICE, "device unavailable");
+        (void)hipMemcpy(dt, t, bytes, hipMemcpyHostToDevice);
+        launch_log1p_selftest(dt, n, dout, nullptr);
+        hipError_t e = hipMemcpy(out_dev, dout, bytes, hipMemcpyDeviceToHost);
+        (void)hipFree(dt);
         (void)hipFree(dout);
         if (e != hipSuccess) return fail(nullptr, SRBD_E_HIP, hipGetErrorString(e));
     }

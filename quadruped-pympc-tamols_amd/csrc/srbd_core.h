@@ -170,15 +170,29 @@ struct TreeShape {
     bool ok;                                  // every rank holds at least one node
 };
 // N rows over `world` ranks, rank `rank`'s share.  X: the highest level at which every rank gets at least one node
-// (world 1: the root level, one node holding everything).
+// and the largest rank share (ceil(nodes / W) nodes) is within 1/8 of the smallest largest share any level allows
+// (world 1: the root level, one node holding everything).  Only the levels the ranks fold to and exchange move with
+// X; the tree and so the bits do not.  Without the balance test, N just past a node boundary gave one rank nearly
+// all the rows (N = 70 001, W = 2: 65 536 and 4 465 rows at level 2; 36 864 and 33 137 at level 1).
+SRBD_HD long long tree_share(int leaves, long long N, int world, int x) {  // largest rank share at level x, 0: invalid
+    const int n = tree_nodes(leaves, x), per = (n + world - 1) / world;
+    if ((long long)(world - 1) * per >= n) return 0;
+    const long long r = (long long)per * tree_node_rows(x);
+    return r < N ? r : N;
+}
 SRBD_HD TreeShape tree_shape(long long N, int world, int rank) {
     TreeShape t;
     t.leaves = (int)((N + LEAF_ROWS - 1) / LEAF_ROWS);
     t.depth = tree_depth(t.leaves);
+    long long best = 0;
+    for (int l = 0; l <= t.depth; ++l) {
+        const long long s = tree_share(t.leaves, N, world, l);
+        if (s > 0 && (best == 0 || s < best)) best = s;
+    }
     int x = t.depth;
-    for (;; --x) {
-        const int n = tree_nodes(t.leaves, x), per = (n + world - 1) / world;
-        if ((long long)(world - 1) * per < n || x == 0) break;
+    for (; x > 0; --x) {
+        const long long s = tree_share(t.leaves, N, world, x);
+        if (s > 0 && 8 * s <= 9 * best) break;
     }
     t.xlevel = x;
     t.xnodes = tree_nodes(t.leaves, x);

@@ -713,6 +713,7 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
     }
     if constexpr (!CEMT) {  // group_size: no in-launch fold for CEM
         if (grp.gsize > 1) {
+            if (grp.fast) return true;  // the caller's fast_tail counts, folds and merges (srbd_kernels.hip)
             if constexpr (ZS) {
                 return level1_fold(mc, recs, rec_stride, grp, nroll, lpb, zst);
             } else {

@@ -19,7 +19,8 @@
 //       element i < h is word 0 of that pair's output, element h + i word 1; split(key) = bits of M = 4 as (2, 2).
 //   bits -> [0, 1): bitcast((b >> 9) | 0x3F800000) - 1;  uniform = max(lo, fma(f, hi - lo, lo));
 //   normal = sqrt(2) * erf_inv(uniform(nextafter(-1, 0), 1)), erf_inv: Giles' single-precision form with a
-//   fused Horner chain; log1p correctly rounded (float64, one rounding).
+//   fused Horner chain; log1p: float64's, rounded once to float (log1p_fast: the same float from a short float64
+//   evaluation, the float64 log1p only where that one is too close to a rounding boundary).
 #pragma once
 
 #include <math.h>
@@ -125,6 +126,104 @@ SRBD_HD float jax_uniform(uint32_t b, float lo, float range) {
 
 SRBD_HD float log1p_cr(float x) { return (float)log1p((double)x); }
 
+// ---- log1p_cr without float64's log1p on the common path (jax_erf_inv's argument t = -x^2 in (-1, 0]).
+// LOG1P_TAB[k] = {c_k, -log(c_k)}: c_k = 1 / (1 + (k + 1/2) / 128) rounded to a multiple of 2^-8 (so m c_k - 1 is
+// small, |.| <= 2^-7.4, for m in bin k of [1, 2)), -log(c_k) to double from a 60-digit evaluation
+// (tests/test_jax_random.py checks the function against the float64 log1p).
+struct Log1pEnt {
+    double c, nlogc;
+};
+constexpr Log1pEnt LOG1P_TAB[128] = {
+    {0.99609375, 0.003913899321136329}, {0.98828125, 0.01178795575204224}, {0.98046875, 0.01972450534777859}, {0.97265625, 0.027724548014854862},
+    {0.96484375, 0.03578910785158528}, {0.95703125, 0.04391923393483549}, {0.953125, 0.048009219186360606}, {0.9453125, 0.05623971832287608},
+    {0.9375, 0.06453852113757118}, {0.9296875, 0.07290677080808779}, {0.92578125, 0.07711730334443129}, {0.91796875, 0.08559193033540351},
+    {0.91015625, 0.09413899091386191}, {0.90625, 0.09844007281325252}, {0.8984375, 0.1070981355563671}, {0.890625, 0.1158318155251217},
+    {0.88671875, 0.1202274269981598}, {0.87890625, 0.12907704227514236}, {0.875, 0.13353139262452263}, {0.8671875, 0.14250006260728304},
+    {0.86328125, 0.14701474296180966}, {0.85546875, 0.15610571466306167}, {0.8515625, 0.16068238169047347}, {0.84375, 0.16989903679539747},
+    {0.83984375, 0.17453941635189968}, {0.83203125, 0.18388527877013736}, {0.828125, 0.18859116980755003}, {0.82421875, 0.19331931100349597},
+    {0.81640625, 0.20284319251475147}, {0.8125, 0.2076393647782445}, {0.80859375, 0.2124586512141934}, {0.80078125, 0.2221674653411543},
+    {0.796875, 0.22705745063534608}, {0.79296875, 0.23197146543777514}, {0.7890625, 0.2369097470783577}, {0.78125, 0.24686007793152578},
+    {0.77734375, 0.2518726197550701}, {0.7734375, 0.2569104137850272}, {0.76953125, 0.26197371574157396}, {0.765625, 0.26706278524904525},
+    {0.7578125, 0.27731928541623435}, {0.75390625, 0.2824872555746769}, {0.75, 0.2876820724517809}, {0.74609375, 0.2929040164329326},
+    {0.7421875, 0.29815337231907635}, {0.73828125, 0.3034304294199201}, {0.734375, 0.3087354816496133}, {0.73046875, 0.31406882762497584},
+    {0.7265625, 0.3194307707663612}, {0.72265625, 0.32482161940123766}, {0.71875, 0.33024168687057687}, {0.71484375, 0.33569129163814154},
+    {0.7109375, 0.34117075740276714}, {0.70703125, 0.3466804132137367}, {0.703125, 0.3522205935893521}, {0.69921875, 0.3577916386388075},
+    {0.6953125, 0.3633938941874773}, {0.69140625, 0.36902771190573336}, {0.6875, 0.3746934494414107}, {0.68359375, 0.38039147055604844},
+    {0.6796875, 0.38612214526503347}, {0.67578125, 0.39188584998178355}, {0.671875, 0.39768296766610944}, {0.66796875, 0.40351388797690263},
+    {0.6640625, 0.4093790074293007}, {0.66015625, 0.415278729556489}, {0.65625, 0.42121346507630353}, {0.65625, 0.42121346507630353},
+    {0.65234375, 0.42718363206280735}, {0.6484375, 0.43318965612301924}, {0.64453125, 0.4392319705789819}, {0.640625, 0.44531101665536404},
+    {0.63671875, 0.4514272436728001}, {0.63671875, 0.4514272436728001}, {0.6328125, 0.4575811092471784}, {0.62890625, 0.4637730794950995},
+    {0.625, 0.4700036292457356}, {0.62109375, 0.47627324225933093}, {0.62109375, 0.47627324225933093}, {0.6171875, 0.48258241145259567},
+    {0.61328125, 0.4889316391312544}, {0.609375, 0.4953214372300254}, {0.609375, 0.4953214372300254}, {0.60546875, 0.5017523275603158},
+    {0.6015625, 0.5082248420659333}, {0.59765625, 0.514739523087127}, {0.59765625, 0.514739523087127}, {0.59375, 0.5212969236332861},
+    {0.58984375, 0.5278976076646381}, {0.58984375, 0.5278976076646381}, {0.5859375, 0.5345421503833068}, {0.58203125, 0.5412311385341033},
+    {0.58203125, 0.5412311385341033}, {0.578125, 0.5479651707154474}, {0.57421875, 0.5547448577008262}, {0.57421875, 0.5547448577008262},
+    {0.5703125, 0.561570822771226}, {0.56640625, 0.5684437020589881}, {0.56640625, 0.5684437020589881}, {0.5625, 0.5753641449035618},
+    {0.55859375, 0.5823328142196552}, {0.55859375, 0.5823328142196552}, {0.5546875, 0.5893503868783018}, {0.5546875, 0.5893503868783018},
+    {0.55078125, 0.5964175541013942}, {0.546875, 0.6035350218702582}, {0.546875, 0.6035350218702582}, {0.54296875, 0.6107035113488707},
+    {0.54296875, 0.6107035113488707}, {0.5390625, 0.6179237593223578}, {0.53515625, 0.6251965186514375}, {0.53515625, 0.6251965186514375},
+    {0.53125, 0.6325225587435105}, {0.53125, 0.6325225587435105}, {0.52734375, 0.639902666041133}, {0.52734375, 0.639902666041133},
+    {0.5234375, 0.6473376445286511}, {0.51953125, 0.6548283162578087}, {0.51953125, 0.6548283162578087}, {0.515625, 0.6623755218931916},
+    {0.515625, 0.6623755218931916}, {0.51171875, 0.6699801212784109}, {0.51171875, 0.6699801212784109}, {0.5078125, 0.6776429940239801},
+    {0.5078125, 0.6776429940239801}, {0.50390625, 0.6853650401178903}, {0.50390625, 0.6853650401178903}, {0.5, 0.6931471805599453},
+};
+
+// The float64 evaluation: |t| < 2^-7 the Taylor polynomial to t^7 / 7 (truncation < 2^-59 relative; t is exact in
+// float64); else y = 1 + t (exact) = 2^e m, m in [1, 2), k = m's top 7 fraction bits, r = m c_k - 1 (one rounding:
+// the product has <= 62 bits), log y = e ln2 + (-log c_k) + log1p(r) (polynomial to r^7 / 7).  Error < 2^-44
+// relative (|log y| >= 2^-7 on this branch, so the absolute 2^-51 of the sum stays small).
+SRBD_HD double log1p_poly(double t) {
+    constexpr double C7 = 1.0 / 7, C6 = -1.0 / 6, C5 = 1.0 / 5, C4 = -1.0 / 4, C3 = 1.0 / 3, C2 = -1.0 / 2;
+    double p = fma(t, C7, C6);
+    p = fma(p, t, C5);
+    p = fma(p, t, C4);
+    p = fma(p, t, C3);
+    p = fma(p, t, C2);
+    p = fma(p, t, 1.0);
+    return p * t;
+}
+SRBD_HD double log1p_tab(float t) {
+    if (t > -0.0078125f) return log1p_poly((double)t);
+    const double y = 1.0 + (double)t;  // exact: t's last bit is >= 2^-31 here
+    union { double d; uint64_t u; } b;
+    b.d = y;
+    const int e = (int)((b.u >> 52) & 0x7FF) - 1023;
+    const int k = (int)((b.u >> 45) & 127);
+    b.u = (b.u & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;  // m in [1, 2)
+    const double r = fma(b.d, LOG1P_TAB[k].c, -1.0);
+    constexpr double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;  // hi: 32 bits
+    const double ed = (double)e;
+    return (ed * LN2_HI + LOG1P_TAB[k].nlogc) + (log1p_poly(r) + ed * LN2_LO);
+}
+// log1p_cr(t) for t in (-1, 0] -- jax_erf_inv's argument -x^2 -- at a fraction of float64 log1p's cost, the same
+// float: log1p_tab's value is rounded to float when it lies farther than 2^-40 relative (16 times its error bound)
+// from both rounding boundaries of the result (Ziv's test), so the float64 log1p rounds the same way; else (about one
+// draw in 2^15) the float64 log1p itself is evaluated.  |t| < 2^-29: log1p(t) lies within 2^-30 relative of t, so it
+// rounds to t.
+// log1p_try: the float, or false where the float64 log1p must decide (srbd_selftest_log1p counts those).
+SRBD_HD bool log1p_try(float t, float* out) {
+    bool ok = t > -1.0f && t <= 0.0f;
+    float f = t;
+    if (ok && t <= -1.862645149230957e-09f) {  // 2^-29
+        const double L = log1p_tab(t);
+        f = (float)L;
+        union { float f; uint32_t u; } a, lo, hi;
+        a.f = f;  // f < 0: the next float toward zero has the bit pattern - 1, away from zero + 1
+        lo.u = a.u + 1u;
+        hi.u = a.u - 1u;
+        const double d_lo = 0.5 * ((double)f + (double)lo.f), d_hi = 0.5 * ((double)f + (double)hi.f);  // boundaries
+        const double tol = -L * 9.094947017729282e-13;  // 2^-40 |L|
+        ok = L - d_lo > tol && d_hi - L > tol;
+    }
+    *out = f;
+    return ok;
+}
+SRBD_HD float log1p_fast(float t) {
+    float f;
+    if (!log1p_try(t, &f)) f = log1p_cr(t);
+    return f;
+}
+
 SRBD_HD float sqrt_rn(float x) {
 #ifdef __HIP_DEVICE_COMPILE__
     return __fsqrt_rn(x);
@@ -139,7 +238,7 @@ SRBD_HD float jax_erf_inv(float x) {
                             -0.00125372503f, -0.00417768164f, 0.246640727f,    1.50140941f};
     constexpr float B[9] = {-0.000200214257f, 0.000100950558f, 0.00134934322f, -0.00367342844f, 0.00573950773f,
                             -0.0076224613f,   0.00943887047f,  1.00167406f,    2.83297682f};
-    float w = -log1p_cr(x * (-x));
+    float w = -log1p_fast(x * (-x));
     const bool lt = w < 5.0f;
     w = lt ? w - 2.5f : sqrt_rn(w) - 3.0f;
     float p = lt ? A[0] : B[0];

@@ -159,6 +159,10 @@ __device__ __forceinline__ float quad_cross(float vl, float fl) {
 template <int NT, bool XG>
 __device__ void final_merge(const ModelConst& mc, const StepInput* in, const float* noise, int rec_stride,
                             const GroupArgs& grp, float* lds);
+// The level-1 fold and the root merge of unsharded host steps with <= TREE_FAN level-1 nodes (GroupArgs::fast),
+// defined after merge_body.
+__device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float* noise, const float* recs,
+                          int rec_stride, const GroupArgs& grp, int nroll, float* st);
 
 // FM: 1 the instantiation with the in-launch final merge (launched when GroupArgs::out is set), 2 with the sharded
 // step's exchange too (GroupArgs::xa); the others carry none of its code (C2's launch, which never merges
@@ -508,8 +512,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
 #endif
     const bool glast = block_epilogue<CEMT, ZST>(mc, in, SPB, q4 == 0 ? sib : -1, valid, cost, noise, recs, rec_stride,
                                                  0.0f, grp, nroll, ZST ? zst : nullptr, ZSTR);
-    if constexpr (FM && ZST && !CEMT)
-        if (glast) final_merge<256, FM == 2>(mc, in, noise, rec_stride, grp, zst);
+    if constexpr (FM && ZST && !CEMT) {
+        if (FM == 1 && grp.fast) {
+            if (glast) fast_tail(mc, in, noise, recs, rec_stride, grp, nroll, zst);
+        } else if (glast) {
+            final_merge<256, FM == 2>(mc, in, noise, rec_stride, grp, zst);
+        }
+    }
     SRBD_RSTAMP(5);
 }
 
@@ -890,6 +899,74 @@ __device__ __forceinline__ void merge_tail_lane(const ModelConst& mc, int qc, co
 #pragma unroll
     for (int i = 0; i < 13; ++i) row[23 + i] = fv[i];
 }
+// Final GRFs (NMPC:695-750) and the predicted state (NMPC:752-784) on tail lane c (four-lane layout, all four lanes
+// of the quad active): lane c decodes component c of every leg from the new parameters `nb` (decode_leg at step 0.0,
+// horizon_leg 1), shapes and clips it as shape_leg does (the rollout's component form), then one Euler step from
+// the prepared rigid-body terms.  ts: the lane's merge_tail_lane row.  One straight-line read of the legs' parameters
+// per kind, so the reads issue together.  merge_body and fast_tail share it, so both give the same bits.
+__device__ __forceinline__ void merge_tail_grf(int c, const float* ts, const float* nb, float f[4], float& p, float& v,
+                                               float& r, float& w) {
+    const float* tail_pre = ts;
+    const QuadRB rb{ts[13], ts[14], ts[15], ts[16], ts[17]};
+    const int kind = __float_as_int(ts[18]), H = __float_as_int(ts[19]), PL = __float_as_int(ts[20]),
+              S = __float_as_int(ts[21]), fidx = __float_as_int(ts[22]);
+    const float fq = ts[23], fomq = ts[24], fa = ts[25], fb = ts[26], fc = ts[27], fd = ts[28];
+    const float gmin = ts[29], gmax = ts[30], mu = ts[31], neg_mu = ts[32];
+    float raw[4];
+    if (kind == SRBD_ZERO_ORDER) {
+#pragma unroll
+        for (int l = 0; l < 4; ++l) raw[l] = nb[l * PL + c * H];
+    } else if (kind == SRBD_LINEAR_SPLINE) {
+        float x0[4], x1[4];
+        const int o = fidx + c * (S + 1);
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            x0[l] = nb[l * PL + o];
+            x1[l] = nb[l * PL + o + 1];
+        }
+#pragma unroll
+        for (int l = 0; l < 4; ++l) raw[l] = fomq * x0[l] + fq * x1[l];
+    } else {
+        float x[4][4];
+        const int o = 10 * fidx + 4 * c;
+#pragma unroll
+        for (int l = 0; l < 4; ++l)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x[l][k] = nb[l * PL + o + k];
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            const float p0 = x[l][0], p1 = x[l][1], p2 = x[l][2], p3 = x[l][3];
+            const float phi = 0.5f * ((p2 - p1) + (p1 - p0));
+            const float phin = 0.5f * ((p3 - p2) + (p2 - p1));
+            raw[l] = fa * p1 + fb * phi + fc * p2 + fd * phin;
+        }
+    }
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+        const float cl = tail_pre[1 + l];
+        const float zp = clamp_cs((tail_pre[0] + raw[l]) * cl, gmin, gmax);
+        const float xy = third(raw[l] * cl);
+        const float fz = qp<QP_B2>(c == 2 ? zp : xy);
+        f[l] = c == 2 ? fz : clamp_cs(xy, neg_mu * fz, mu * fz);
+    }
+    p = tail_pre[5], v = tail_pre[6], r = tail_pre[7], w = tail_pre[8];
+    const float c0 = tail_pre[1], c1 = tail_pre[2], c2 = tail_pre[3], c3 = tail_pre[4];
+    const float temp = (f[0] * c0 + f[1] * c1) + (f[2] * c2 + f[3] * c3);  // integrate()'s order
+    const float temp2 = (quad_cross(tail_pre[9] - p, f[0]) * c0 + quad_cross(tail_pre[10] - p, f[1]) * c1) +
+                        (quad_cross(tail_pre[11] - p, f[2]) * c2 + quad_cross(tail_pre[12] - p, f[3]) * c3);
+    {  // quad_rb_apply with the copies of inv_m / dt and this lane's constants
+        const float lin = ts[33] * temp + ts[39];
+        const float Rt = rb.R0 * qp<QP_B0>(temp2) + rb.R1 * qp<QP_B1>(temp2) + rb.R2 * qp<QP_B2>(temp2);
+        const float a2 = ts[36] * qp<QP_B0>(Rt) + ts[37] * qp<QP_B1>(Rt) + ts[38] * qp<QP_B2>(Rt);
+        const float aa = -rb.a1 + a2;
+        const float dt = ts[34];
+        const float pn = p + v * dt, vn = v + lin * dt, rn = r + rb.er * dt, wn = w + aa * dt;
+        p = pn;
+        v = vn;
+        r = rn;
+        w = wn;
+    }
+}
 
 // smem: [STAGE: records] | scale[nrec_pad] | tree levels | node keys | erow[K*ncol] (merge_smem_bytes).  prestaged
 // (STAGE): the records are already in smem.  The staged body's sums use G = MERGE_STAGE_THREADS / (ncol + 1)
@@ -1237,10 +1314,13 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     if (SPLITX && hand && tailblk) {  // the tail block's sums: the slices'
         if constexpr (!STAGE) tail_prep();
         for (int i = tid; i <= ncol; i += T) Vs[i] = u2f(poll(&xg->sums[i < ncol ? jc(i) : P]));
-        __syncthreads();
-        // every slice has stored its sums, so every slice has read the epoch: advance it for the next launch
-        if (tid == 0) __hip_atomic_store(&xg->epoch, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // any thread's timed-out word fails the step (status bit 1; the host then resets SplitXchg)
+        hand_late = __syncthreads_or(hand_late);
+        // every slice has stored its sums, so every slice has read the epoch: advance it for the next launch.  Not
+        // after a timeout: a slice may not have read it yet (it would tag its late sums with the next launch's epoch)
+        if (tid == 0 && !hand_late) __hip_atomic_store(&xg->epoch, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (SPLITX && hand && !tailblk && !topk_here && K > 1) hand_late = __syncthreads_or(hand_late);  // elite keys
     __syncthreads();
     // record slot of every elite key (needed when rows travel inside the records)
     const bool need_rows = want_elite && (rs || cem);  // MPPI's update is the weighted sum alone
@@ -1308,72 +1388,9 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
             float ts[40];  // one batch of LDS reads
 #pragma unroll
             for (int i = 0; i < 40; ++i) ts[i] = tail_sh[tid][i];
-            const float* tail_pre = ts;
-            const QuadRB rb{ts[13], ts[14], ts[15], ts[16], ts[17]};
-            const int kind = __float_as_int(ts[18]), H = __float_as_int(ts[19]), PL = __float_as_int(ts[20]),
-                      S = __float_as_int(ts[21]), fidx = __float_as_int(ts[22]);
-            const float fq = ts[23], fomq = ts[24], fa = ts[25], fb = ts[26], fc = ts[27], fd = ts[28];
-            const float gmin = ts[29], gmax = ts[30], mu = ts[31], neg_mu = ts[32];
-            // final GRFs (NMPC:695-750) and the predicted state (NMPC:752-784), four-lane layout: lane c
-            // decodes component c of every leg (decode_leg at step 0.0, horizon_leg 1), shapes and clips it
-            // as shape_leg does (the rollout's component form), then one Euler step from rb.  One
-            // straight-line read of the legs' parameters per kind, so the LDS reads issue together.
             const int c = qc;
-            float raw[4];
-            if (kind == SRBD_ZERO_ORDER) {
-#pragma unroll
-                for (int l = 0; l < 4; ++l) raw[l] = nb[l * PL + c * H];
-            } else if (kind == SRBD_LINEAR_SPLINE) {
-                float x0[4], x1[4];
-                const int o = fidx + c * (S + 1);
-#pragma unroll
-                for (int l = 0; l < 4; ++l) {
-                    x0[l] = nb[l * PL + o];
-                    x1[l] = nb[l * PL + o + 1];
-                }
-#pragma unroll
-                for (int l = 0; l < 4; ++l) raw[l] = fomq * x0[l] + fq * x1[l];
-            } else {
-                float x[4][4];
-                const int o = 10 * fidx + 4 * c;
-#pragma unroll
-                for (int l = 0; l < 4; ++l)
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) x[l][k] = nb[l * PL + o + k];
-#pragma unroll
-                for (int l = 0; l < 4; ++l) {
-                    const float p0 = x[l][0], p1 = x[l][1], p2 = x[l][2], p3 = x[l][3];
-                    const float phi = 0.5f * ((p2 - p1) + (p1 - p0));
-                    const float phin = 0.5f * ((p3 - p2) + (p2 - p1));
-                    raw[l] = fa * p1 + fb * phi + fc * p2 + fd * phin;
-                }
-            }
-            float f[4];
-#pragma unroll
-            for (int l = 0; l < 4; ++l) {
-                const float cl = tail_pre[1 + l];
-                const float zp = clamp_cs((tail_pre[0] + raw[l]) * cl, gmin, gmax);
-                const float xy = third(raw[l] * cl);
-                const float fz = qp<QP_B2>(c == 2 ? zp : xy);
-                f[l] = c == 2 ? fz : clamp_cs(xy, neg_mu * fz, mu * fz);
-            }
-            float p = tail_pre[5], v = tail_pre[6], r = tail_pre[7], w = tail_pre[8];
-            const float c0 = tail_pre[1], c1 = tail_pre[2], c2 = tail_pre[3], c3 = tail_pre[4];
-            const float temp = (f[0] * c0 + f[1] * c1) + (f[2] * c2 + f[3] * c3);  // integrate()'s order
-            const float temp2 = (quad_cross(tail_pre[9] - p, f[0]) * c0 + quad_cross(tail_pre[10] - p, f[1]) * c1) +
-                                (quad_cross(tail_pre[11] - p, f[2]) * c2 + quad_cross(tail_pre[12] - p, f[3]) * c3);
-            {  // quad_rb_apply with the LDS copies of inv_m / dt and this lane's constants
-                const float lin = ts[33] * temp + ts[39];
-                const float Rt = rb.R0 * qp<QP_B0>(temp2) + rb.R1 * qp<QP_B1>(temp2) + rb.R2 * qp<QP_B2>(temp2);
-                const float a2 = ts[36] * qp<QP_B0>(Rt) + ts[37] * qp<QP_B1>(Rt) + ts[38] * qp<QP_B2>(Rt);
-                const float aa = -rb.a1 + a2;
-                const float dt = ts[34];
-                const float pn = p + v * dt, vn = v + lin * dt, rn = r + rb.er * dt, wn = w + aa * dt;
-                p = pn;
-                v = vn;
-                r = rn;
-                w = wn;
-            }
+            float f[4], p, v, r, w;
+            merge_tail_grf(c, ts, nb, f, p, v, r, w);
             if (tid < 3) {
 #pragma unroll
                 for (int l = 0; l < 4; ++l) ostore(&out->grf[3 * l + c], f[l]);
@@ -1388,7 +1405,8 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
             ostore(&out->best_cost, beta);
             ostore(&out->best_index, __uint_as_float((uint32_t)bkey));
             ostore(&out->best_freq, tag_sh);
-            ostore(&out->status, __int_as_float(SPLITX ? hand_late : 0));
+            // a column split: the host zeroes status before the launch, and a late block ORs its bit in (below)
+            if (!split) ostore(&out->status, __int_as_float(0));
             // chain: the next draws come from the device RNG.  (Split: slices read noise_scaled too, but a
             // chain's steps all run with it 0 already -- reset_noise_scaled -- so this store never changes it.)
             if (chain) in->noise_scaled = 0;
@@ -1421,6 +1439,10 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     if (dbg && threadIdx.x == 0 && sblk < 2) dbg[32 * sblk + 9] = __builtin_amdgcn_s_memtime();
 #undef MERGE_STAMP
 #undef MERGE_MARK
+    // a hand-off word of the column split never arrived (bounded poll): tail block bit 1, a slice bit 2
+    if (SPLITX && hand && hand_late && tid == 0 && out)
+        __hip_atomic_fetch_or(reinterpret_cast<uint32_t*>(&out->status), tailblk ? 1u : 2u, __ATOMIC_RELAXED,
+                              sysout ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT);
     if (flag) {  // every thread's output writes have completed before thread 0 publishes `seq`
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -1620,6 +1642,259 @@ size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride) {
     const size_t b =
         sizeof(float) * (size_t)mc.t_xnodes * rec_floats_rank(mc.P, mc.K) + merge_smem_bytes(mc.t_xnodes, mc.P, mc.K);
     return (sizeof(MergeShared<256>) + 15) / 16 * 16 + (a > b ? a : b);
+}
+
+// ---- fast_tail: unsharded host steps whose launch folds level 1 into 2..TREE_FAN node records (GroupArgs::fast,
+// fast_tail_ok; MPPI / random sampling, zero-order four-lane, FM = 1).  The tree's arithmetic is that of the level-1
+// fold (fold_node_lds) and of merge_body over <= TREE_FAN records (one level to the root), operation for operation,
+// so the bits equal the two-stage form's; what changes is the hand-offs after the last leaf record:
+//  - a node's last arriving block counts itself in *gdone as soon as it knows (the count's round trip overlaps the
+//    staging of the node's leaf records), instead of after its fold and the drain of its node record;
+//  - the node's headers are formed on every wave alike (lane c = child c, scales broadcast with readlane), so the
+//    column sums follow them without a block barrier;
+//  - a folder that is not the last to count stores its node record as 8-byte words tagged with the launch's seq and
+//    exits.  The last to count keeps its own node's sums in registers, loads the other node records' words straight
+//    into registers (each polled until it carries seq: their folders counted earlier and are running), and folds
+//    the root: column j by thread j, the root key and the weights' sum on every wave alike;
+//  - outputs go straight to the host-mapped StepOutput (system-scope stores); after one barrier the tail lanes form
+//    the GRFs and the predicted state (merge_tail_grf); every wave drains its stores, one lane publishes seq.
+// LDS (carved from the rollout's noise stage `st`): the node's leaf records, then nb[P], then the tail lanes' rows.
+// A word that never arrives (bounded wait) makes the step publish status -1 (the host returns an error).
+__device__ __forceinline__ uint64_t tag_word(uint32_t seq, float v) { return ((uint64_t)seq << 32) | f2u(v); }
+__device__ __forceinline__ void st_tag(uint64_t* p, uint64_t w) {
+    __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float rdl(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ void st_sys(void* p, float v) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float* noise, const float* recs,
+                          int rec_stride, const GroupArgs& grp, int nroll, float* st) {
+    __shared__ int last_sh, fin_sh;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int P = mc.P, TW = REC_HDR + P;  // TW: words of a tagged node record
+    const bool rs = mc.method == SRBD_RANDOM_SAMPLING;
+    const int g = (int)blockIdx.x / TREE_FAN;  // one leaf per four-lane block
+    const int nblk = min(TREE_FAN, nroll - g * TREE_FAN);
+    const int nb = min(TREE_FAN, mc.nleaf - g * TREE_FAN);  // the node's leaves
+    const int ng = grp.ngroups;
+    const uint32_t seq = grp.seq;
+    SRBD_LSTAMP(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's leaf record stores have completed
+    __syncthreads();
+    SRBD_LSTAMP(1);
+    if (tid == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(grp.cnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_sh = old == (uint32_t)(nblk - 1);
+    }
+    __syncthreads();
+    if (!last_sh) return;
+    SRBD_LSTAMP(2);
+    uint32_t gd = 0;
+    if (tid == 0) {
+        __hip_atomic_store(grp.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+        gd = __hip_atomic_fetch_add(grp.gdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    stage_recs<10>(recs + (size_t)g * TREE_FAN * rec_stride, st, nb * rec_stride);  // sc1 loads (other CUs' records)
+    if (tid == 0) fin_sh = gd == (uint32_t)(ng - 1);
+    __syncthreads();
+    SRBD_LSTAMP(3);
+    const bool fin = fin_sh;
+    float* nbv = st + TREE_FAN * rec_stride;  // the new parameters (the tail lanes read them)
+    float* tsh = nbv + ((P + 3) & ~3);        // the tail lanes' merge_tail_lane rows, 4 x 40
+    const int j = tid;
+    const bool col = !rs && j < P;
+    // the last folder: the other nodes' words into registers, in two batches of TREE_FAN / 2 nodes (all 32 at once
+    // spilled): the headers and batch A in flight during the own fold, batch B right after it
+    constexpr int HB = TREE_FAN / 2;
+    uint64_t xa[HB], xb[HB], hw[4];
+    // the words through a buffer descriptor: word w of node h at voffset 8 w, soffset 8 h TW (one VGPR of address
+    // per thread, not a 64-bit pointer per node), sc1 as an agent-scope atomic load has it.  Not volatile: the
+    // compiler then waits for each such load before the next (16 round trips in a row); the poll's re-reads are
+    // kept apart by an asm memory clobber instead.
+    const auto grs = __builtin_amdgcn_make_buffer_rsrc((void*)grp.gtag, (short)0, ng * TW * 8, 0x00020000);
+    auto ldw = [&](int h, int w) -> uint64_t {  // h uniform (an SGPR offset; a lane-varying one is a waterfall loop)
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(grs, 8 * w, 8 * h * TW, 16);
+        return ((uint64_t)v[1] << 32) | v[0];
+    };
+    auto ldh = [&](int i) -> uint64_t {  // header word i of node `lane`
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(grs, 8 * (lane * TW + i), 0, 16);
+        return ((uint64_t)v[1] << 32) | v[0];
+    };
+    auto want = [&](int h) { return col && h < ng && h != g; };
+    float b0 = 0.0f;
+    const bool hv = lane < ng && lane != g;  // header lanes (every wave): node `lane`'s words 0..3
+    auto issue = [&](uint64_t(&x)[HB], int h0) {
+#pragma unroll
+        for (int u = 0; u < HB; ++u) x[u] = want(h0 + u) ? ldw(h0 + u, REC_HDR + j) : tag_word(seq, 0.0f);
+    };
+    // bounded poll: re-read every word of `x` (nodes h0..) whose tag is not this launch's seq
+    int late = 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    auto poll = [&](uint64_t* x, int n, auto&& reload) {
+        for (;;) {
+            bool p = false;
+            for (int u = 0; u < n; ++u) p |= (uint32_t)(x[u] >> 32) != seq;
+            if (!p) return;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > XCHG_TIMEOUT_TICKS) {
+                late = 1;
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            asm volatile("" ::: "memory");  // the words may have changed: re-read them
+            for (int u = 0; u < n; ++u)
+                if ((uint32_t)(x[u] >> 32) != seq) x[u] = reload(u);
+        }
+    };
+    if (fin) {
+        if (tid < 4) {  // the predicted state's force-independent part (before the words: registers)
+            float tail_pre[13];
+            merge_tail_load(in, tid < 3 ? tid : 2, tail_pre);
+            merge_tail_lane(mc, tid < 3 ? tid : 2, tail_pre, tsh + 40 * tid);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) hw[i] = hv ? ldh(i) : tag_word(seq, 0.0f);
+        issue(xa, 0);
+        if (j < P) b0 = in->best[j];  // the input parameters, read early (kernel argument or device StepInput)
+    }
+    // ---- the node (fold_node_lds's arithmetic): key and child scales on every wave (lane c = child c)
+    const float* R = st + (size_t)(lane < TREE_FAN ? lane : 0) * rec_stride;
+    const bool have = lane < nb;
+    const float m = have ? R[0] : 0.0f;
+    const uint64_t key = have ? ((uint64_t)__float_as_uint(m) << 32) | __float_as_uint(R[2]) : KEY_NONE;
+    const float r3 = have ? R[3] : 0.0f;
+    const uint64_t gk = wave_min_u64(key);
+    const float gm = __uint_as_float((uint32_t)(gk >> 32));
+    const float sc = have ? (rs ? 1.0f : expf(-1.0f * (m - gm))) : 0.0f;
+    const float gtg = rdl(r3, (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(key == gk)));  // keys are unique
+    SRBD_LSTAMP(4);
+    // column j < P: sum_c sc_c v_c[j]; column P: sum_c sc_c s_c, child by child (8 LDS loads in flight)
+    float a = 0.0f;
+    if (!rs && j <= P) {
+        const float* src = st + (j < P ? REC_HDR + j : 1);
+        int cb = 0;
+        for (; cb + 8 <= nb; cb += 8) {
+            float x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = src[(size_t)(cb + u) * rec_stride];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a = a + rdl(sc, cb + u) * x[u];
+        }
+        for (; cb < nb; ++cb) a = a + rdl(sc, cb) * src[(size_t)cb * rec_stride];
+    }
+    SRBD_LSTAMP(5);
+    if (!fin) {  // hand the node record over: tagged words, no drain, no second count
+        uint64_t* G = grp.gtag + (size_t)g * TW;
+        if (col) st_tag(G + REC_HDR + j, tag_word(seq, a));
+        if (!rs && j == P) st_tag(G + 1, tag_word(seq, a));
+        if (tid == 0) {
+            st_tag(G, tag_word(seq, gm));
+            if (rs) st_tag(G + 1, tag_word(seq, 1.0f));
+            st_tag(G + 2, tag_word(seq, __uint_as_float((uint32_t)gk)));
+            st_tag(G + 3, tag_word(seq, gtg));
+        }
+        return;
+    }
+    if (ng > HB) issue(xb, HB);
+#ifdef SRBD_ROLLOUT_STAMPS
+    if (tid == 0) {
+        g_fstamp[0] = blockIdx.x + 1;
+        g_fstamp[1] = __builtin_amdgcn_s_memrealtime();  // own fold done
+    }
+#endif
+    // the own node's weights' sum, on every lane alike (column P of the fold above)
+    float s_own = 1.0f;
+    if (!rs) {
+        s_own = 0.0f;
+        for (int c = 0; c < nb; ++c) s_own = s_own + rdl(sc, c) * st[(size_t)c * rec_stride + 1];
+    }
+    // ---- the root (merge_body over ng records, one level): key, scales and the weights' sum on every wave alike
+    poll(hw, 4, [&](int i) { return ldh(i); });
+#ifdef SRBD_ROLLOUT_STAMPS
+    if (tid == 0) g_fstamp[2] = __builtin_amdgcn_s_memrealtime();  // the other nodes' headers in
+#endif
+    const bool hl = lane < ng;
+    const float mh = lane == g ? gm : __uint_as_float((uint32_t)hw[0]);
+    const float sh = lane == g ? s_own : __uint_as_float((uint32_t)hw[1]);
+    const uint32_t rowh = lane == g ? (uint32_t)gk : (uint32_t)hw[2];
+    const float th = lane == g ? gtg : __uint_as_float((uint32_t)hw[3]);
+    const uint64_t kh = hl ? ((uint64_t)__float_as_uint(mh) << 32) | rowh : KEY_NONE;
+    const uint64_t bk = wave_min_u64(kh);
+    const float beta = __uint_as_float((uint32_t)(bk >> 32));
+    const float nsc = hl && !rs ? expf(-1.0f * (mh - beta)) : 0.0f;
+    const float btag = rdl(th, (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(kh == bk)));
+    float s_root = 0.0f, V = 0.0f;
+    if (!rs) {
+        for (int h = 0; h < ng; ++h) s_root = s_root + rdl(nsc, h) * rdl(sh, h);
+        // column j, node by node in order: batch A, then batch B
+        auto accum = [&](const uint64_t(&x)[HB], int h0) {
+#pragma unroll
+            for (int u = 0; u < HB; ++u)
+                if (h0 + u < ng) V = V + rdl(nsc, h0 + u) * (h0 + u == g ? a : __uint_as_float((uint32_t)x[u]));
+        };
+        poll(xa, HB, [&](int u) { return ldw(u, REC_HDR + j); });
+        accum(xa, 0);
+        if (ng > HB) {
+            poll(xb, HB, [&](int u) { return ldw(HB + u, REC_HDR + j); });
+            accum(xb, HB);
+        }
+    }
+#ifdef SRBD_ROLLOUT_STAMPS
+    if (tid == 0) g_fstamp[3] = __builtin_amdgcn_s_memrealtime();  // root sums
+#endif
+    // ---- outputs (merge_body's values): best[j], then the tail lanes' GRFs / prediction from nb
+    StepOutput* out = grp.out;
+    if (j < P) {
+        const float v = rs ? b0 + noise[(size_t)j * mc.ldn + ((int)(uint32_t)bk - mc.row0)] : b0 + V / s_root;
+        nbv[j] = v;
+        st_sys(&out->best[j], v);
+    }
+    if (tid >= 12 && tid < 24) st_sys(&out->pred[tid], in->state[tid]);
+    late = __syncthreads_or(late);
+    if (tid == 0) {
+        st_sys(&out->best_cost, beta);
+        st_sys(&out->best_index, __uint_as_float((uint32_t)bk));
+        st_sys(&out->best_freq, btag);
+        st_sys(&out->status, __int_as_float(late ? -1 : 0));
+    }
+    if (tid < 4) {
+        float ts[40];
+#pragma unroll
+        for (int i = 0; i < 40; ++i) ts[i] = tsh[40 * tid + i];
+        const int c = tid < 3 ? tid : 2;
+        float f[4], p, v, r, w;
+        merge_tail_grf(c, ts, nbv, f, p, v, r, w);
+        if (tid < 3) {
+#pragma unroll
+            for (int l = 0; l < 4; ++l) st_sys(&out->grf[3 * l + c], f[l]);
+            st_sys(&out->pred[c], p);
+            st_sys(&out->pred[3 + c], v);
+            st_sys(&out->pred[6 + c], r);
+            st_sys(&out->pred[9 + c], w);
+        }
+    }
+#ifdef SRBD_ROLLOUT_STAMPS
+    if (tid == 0) g_fstamp[32 + 4] = __builtin_amdgcn_s_memrealtime();  // outputs issued
+#endif
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's output stores have completed
+    __syncthreads();
+    if (tid == 0) {
+        __hip_atomic_store(grp.gdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+        __hip_atomic_store(grp.flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#ifdef SRBD_ROLLOUT_STAMPS
+        g_fstamp[32 + 5] = __builtin_amdgcn_s_memrealtime();
+#endif
+    }
+}
+
+// fast_tail's LDS fits the zero-order noise stage, the threads cover the columns, and the root is one level.
+bool fast_tail_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride) {
+    if (!final_merge_ok(mc, mode, ngroups, rec_stride) || ngroups < 2 || ngroups > TREE_FAN || mc.P + 1 > 256)
+        return false;
+    const int zst = 64 * (12 * mc.H + 1) > GROUP_LDS_FLOATS ? 64 * (12 * mc.H + 1) : GROUP_LDS_FLOATS;
+    return TREE_FAN * rec_stride + ((mc.P + 3) & ~3) + 4 * 40 <= zst;
 }
 
 // The step input as a kernel argument (StepInputK): zero-order H 10 / 12 rollouts (four-lane with the LDS noise
@@ -2011,6 +2286,14 @@ void launch_advance(const ModelConst& mc, StepInput* in, const StepOutput* out, 
 
 void launch_div_selftest(const float* a, const float* b, int n, float* o, hipStream_t s) {
     hipLaunchKernelGGL(div_selftest_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a, b, n, o);
+}
+
+__global__ void log1p_selftest_kernel(const float* t, int n, float* o) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) o[i] = log1p_fast(t[i]);
+}
+void launch_log1p_selftest(const float* t, int n, float* o, hipStream_t s) {
+    if (n > 0) hipLaunchKernelGGL(log1p_selftest_kernel, dim3((n + 255) / 256), dim3(256), 0, s, t, n, o);
 }
 
 }  // namespace srbd

@@ -46,8 +46,14 @@ struct GroupArgs {
     // (device copy of the context's XchgArgs)
     const XchgArgs* xa = nullptr;
     int levels_up = 0;
+    // unsharded host steps with 2..TREE_FAN level-1 nodes (fast_tail_ok): the node folders count in *gdone before
+    // they fold, the last to count folds the root itself; the others hand their node records over as 8-byte words
+    // tagged with `seq` in gtag (ngroups x (REC_HDR + P) words), polled word by word (fast_tail)
+    int fast = 0;
+    uint64_t* gtag = nullptr;
 };
 bool ks_ok(const ModelConst& mc, int mode);
+bool fast_tail_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride);
 // LDS the in-launch final merge needs (merge_body<256> of ngroups records) and whether the launch can do it
 size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride);
 bool final_merge_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride);
@@ -134,6 +140,7 @@ constexpr uint32_t ARM_CANCEL = 0x80000000u;
 void launch_arm_copy(const uint32_t* go, uint32_t seq, uint64_t deadline_ticks, const void* src, void* dst,
                      size_t bytes0, size_t off1, size_t bytes1, uint32_t* fired, hipStream_t s);
 void launch_div_selftest(const float* a, const float* b, int n, float* o, hipStream_t s);
+void launch_log1p_selftest(const float* t, int n, float* o, hipStream_t s);
 
 // TAMOLS (tamols_kernel.hip)
 constexpr int TAMOLS_NQ = 19;        // nearest-neighbour queries per candidate

@@ -96,6 +96,7 @@ SIGNATURES = {
     "srbd_get_state": (_I, [_P, _FP, _FP, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "srbd_set_state": (_I, [_P, _FP, _FP, C.c_uint64, C.c_uint64]),
     "srbd_selftest_div": (_I, [_FP, _FP, _I, _FP, _FP]),
+    "srbd_selftest_log1p": (_I, [_FP, _I, _FP, _FP, C.POINTER(C.c_int64)]),
     "srbd_debug_merge_phases": (_I, [_P, _I, _FP]),
     "srbd_comm_get_unique_id": (_I, [C.c_char_p, _P]),
     "srbd_comm_init": (_I, [_P, C.c_char_p, _P]),

@@ -57,15 +57,20 @@ def main():
         t0 = st[st[:, 0] > 0, 0].min()
         us = lambda t: round((int(t) - t0) / 100.0, 2) if t else None  # noqa: E731
         lst = fs[64:].reshape(-1, 8)
+        fast = fs[32] == 0 and fs[32 + 5] != 0  # fast_tail: no merge_body stamps
         row = {"last_leaf_sums": us(st[roll, 4].max()), "fm_block_leaf_sums": us(st[b, 4]),
                "fold_entry": us(lst[b, 0]), "fold_drained": us(lst[b, 1]), "fold_last": us(lst[b, 2]),
-               "fold_staged": us(lst[b, 3]), "fold_headers": us(lst[b, 4]), "fold_sums": us(lst[b, 5]),
-               "fm_entry": us(fs[1]), "fm_drained": us(fs[2]), "fm_last": us(fs[3]),
-               "fm_staged": us(fs[4])}
-        for i, nm in ((0, "m_entry"), (6, "m_staged"), (16, "m_beta_scan"), (17, "m_tail_prep"), (18, "m_barrier"), (1, "m_beta"),
-                      (20, "m_l0_sums"), (21, "m_levels"), (2, "m_sums"), (3, "m_topk"), (4, "m_outputs"),
-                      (5, "m_published")):
-            row[nm] = us(fs[32 + i])
+               "fold_staged": us(lst[b, 3]), "fold_headers": us(lst[b, 4]), "fold_sums": us(lst[b, 5])}
+        if fast:  # fast_tail's marks: own fold done, other nodes' headers in, root sums, outputs issued, published
+            for i, nm in ((1, "ft_own_fold"), (2, "ft_headers_in"), (3, "ft_root_sums"), (36, "ft_outputs"),
+                          (37, "ft_published")):
+                row[nm] = us(fs[i])
+        else:
+            row.update({"fm_entry": us(fs[1]), "fm_drained": us(fs[2]), "fm_last": us(fs[3]), "fm_staged": us(fs[4])})
+            for i, nm in ((0, "m_entry"), (6, "m_staged"), (16, "m_beta_scan"), (17, "m_tail_prep"), (18, "m_barrier"),
+                          (1, "m_beta"), (20, "m_l0_sums"), (21, "m_levels"), (2, "m_sums"), (3, "m_topk"),
+                          (4, "m_outputs"), (5, "m_published")):
+                row[nm] = us(fs[32 + i])
         row["fm_block_exit"] = us(st[b, 5])
         row["launch_end"] = us(st[st[:, 0] > 0, 5].max())
         rows.append(row)

@@ -95,3 +95,22 @@ def test_shard_rows_cover_problem():
             for (a, n), (b, _) in zip(spans, spans[1:]):
                 assert a + n == b
                 assert a % 64 == 0 and n > 0  # whole leaves (tree nodes)
+
+
+def test_shard_rows_balanced():
+    """The exchange level is the highest one whose largest rank share is within 1/8 of the best any level allows
+    (srbd_core.h tree_shape): no rank is left with a sliver when N sits just past a node boundary."""
+    from quadruped_pympc_amd.sharded import shard_rows
+
+    # the fixed cases: C5 on 8 GPUs keeps one level-2 node per rank; 70 001 / 100 000 rows over 2 ranks drop to
+    # level 1 (at level 2: 65 536 + 4 465 and 65 536 + 34 464 rows)
+    assert [shard_rows(524288, r, 8) for r in range(8)] == [(65536 * r, 65536) for r in range(8)]
+    assert [shard_rows(70001, r, 2) for r in range(2)] == [(0, 36864), (36864, 33137)]
+    assert [shard_rows(100000, r, 2) for r in range(2)] == [(0, 51200), (51200, 48800)]
+    for N in (4097, 10000, 65537, 70001, 100000, 131073, 300000, 524288, 524289):
+        for W in (2, 3, 5, 8):
+            spans = [shard_rows(N, r, W) for r in range(W)]
+            big = max(n for _, n in spans)
+            ideal = -(-N // W)
+            # within 1/8 of the largest share whole 64-row leaves allow, or that share itself
+            assert 8 * big <= 9 * max(ideal, 64 * -(-(-(-N // 64)) // W)), (N, W, spans)

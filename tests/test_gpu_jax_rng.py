@@ -234,3 +234,17 @@ def test_end_to_end_c2_interface_on_jax_stream(lib, part):
             best_ref = ref["best"]
     finally:
         mpc.close()
+
+
+def test_log1p_fast_device_equals_host(lib):
+    """The device log1p_fast (float64 polynomial + table, Ziv's test, OCML's float64 log1p as the fallback) gives the
+    host's float32 for every sampled t in (-1, 0] (tests/test_jax_random.py pins the host against float64 log1p)."""
+    import ctypes
+
+    from test_jax_random import _log1p_sample
+
+    t = _log1p_sample()
+    host, dev = np.empty_like(t), np.empty_like(t)
+    nfb = ctypes.c_int64(0)
+    assert lib.lib.srbd_selftest_log1p(lib.fptr(t), t.size, lib.fptr(host), lib.fptr(dev), ctypes.byref(nfb)) == 0
+    np.testing.assert_array_equal(dev.view(np.uint32), host.view(np.uint32))

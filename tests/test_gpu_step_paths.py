@@ -138,3 +138,42 @@ def test_grouped_gait_adaptive_against_oracle(lib):
     assert r.best_index == ref["best_index"]
     np.testing.assert_allclose(best, ref["best"], rtol=1e-5, atol=1e-4)
     assert r.best_freq == freqs[r.best_index]
+
+
+@pytest.mark.parametrize("method,N,H,noise", [
+    ("mppi", 8257, 12, False),             # 130 leaves: the fewest level-1 nodes (5) that fold in the launch
+    ("mppi", 10000, 12, False),            # C2
+    ("mppi", 10000, 12, True),
+    ("random_sampling", 10000, 12, False),
+    ("mppi", 32832, 10, True),             # 17 nodes: both register batches of the root
+    ("random_sampling", 40000, 12, True),
+    ("mppi", 65536, 12, False),            # 32 nodes (north-star)
+])
+def test_fast_tail_equals_two_stage(lib, monkeypatch, method, N, H, noise):
+    """fast_tail (the level-1 fold and the root merge with one arrival count, tagged node-record hand-off) against
+    the two-stage in-launch final merge (SRBD_FAST_TAIL=0: folds, a second count, merge_body) over six successive
+    host steps on each context -- the tagged words are rewritten launch after launch -- bit for bit."""
+    case = make_case("c2", N=N, method=method, H=H, seed=zlib.crc32(f"ft{method}{N}{H}".encode()))
+    monkeypatch.setenv("SRBD_FAST_TAIL", "0")
+    slow = lib.Context(product_cfg(case))
+    monkeypatch.delenv("SRBD_FAST_TAIL")
+    fast = lib.Context(product_cfg(case))
+    try:
+        bf, bs = case["best"].copy(), case["best"].copy()
+        for k in range(6):
+            st = case["state"].copy()
+            st[1] += 0.005 * k
+            nz = case["noise"] if noise else None
+            a = fast.step(st, case["ref"], case["contact"], bf, noise=nz, seed=3, counter=k, want_costs=k == 0)
+            b = slow.step(st, case["ref"], case["contact"], bs, noise=nz, seed=3, counter=k, want_costs=k == 0)
+            np.testing.assert_array_equal(a[0], b[0])
+            np.testing.assert_array_equal(np.array(a[2].grf), np.array(b[2].grf))
+            np.testing.assert_array_equal(np.array(a[2].predicted_state), np.array(b[2].predicted_state))
+            assert (a[2].best_index, a[2].best_cost, a[2].best_freq, a[2].status) == \
+                   (b[2].best_index, b[2].best_cost, b[2].best_freq, b[2].status)
+            if k == 0:
+                np.testing.assert_array_equal(a[3], b[3])
+            bf, bs = a[0], b[0]
+    finally:
+        fast.close()
+        slow.close()

@@ -205,3 +205,39 @@ def test_controller_key_schedule_is_the_reference_s():
             k = jr.with_newkey(k, part)
             np.testing.assert_array_equal(mpc.master_key, k)
         assert mpc.master_key.dtype == np.uint32
+
+
+def _log1p_sample():
+    """Every 61st float32 in (-1, 0] (bit patterns 0x80000000 .. 0xBF7FFFFF), its neighbours of 1 and 0, and values
+    whose float64 log1p lies near a float32 rounding boundary (the Ziv fallback's territory)."""
+    u = np.arange(0x80000000, 0xBF800000, 61, dtype=np.uint64).astype(np.uint32)
+    t = u.view(f32)
+    edge = np.array([-0.0, 0.0, -np.finfo(f32).tiny, -1.862645149230957e-09, -1.8626452e-09, -0.0078125,
+                     np.nextafter(f32(-0.0078125), f32(0)), np.nextafter(f32(-0.0078125), f32(-1)),
+                     np.nextafter(f32(-1), f32(0)), -0.5, -0.25, -0.75], f32)
+    # boundary cases: t whose log1p(t) (float64) is within 2^-34 relative of a float32 midpoint
+    rng = np.random.default_rng(5)
+    c = -rng.random(4_000_000).astype(f32)
+    L = np.log1p(c.astype(np.float64))
+    f = L.astype(f32).astype(np.float64)
+    up = np.nextafter(L.astype(f32), f32(0)).astype(np.float64)
+    dn = np.nextafter(L.astype(f32), f32(-np.inf)).astype(np.float64)
+    near = np.minimum(np.abs(L - 0.5 * (f + up)), np.abs(L - 0.5 * (f + dn))) < np.abs(L) * 2.0 ** -34
+    return np.concatenate([t, edge, c[near]])
+
+
+def test_log1p_fast_equals_float64_log1p():
+    """log1p_fast (the JAX normal's erf_inv argument, srbd_jaxrng.h): a short float64 evaluation rounded to float
+    unless it lies within 2^-40 relative of a rounding boundary, else the float64 log1p itself -- the same float32 as
+    float32(log1p(float64 t)) for every t in (-1, 0] sampled, with fallbacks rare (about 2^-15 of uniform draws)."""
+    from quadruped_pympc_amd import _lib
+
+    t = _log1p_sample()
+    out = np.empty_like(t)
+    nfb = __import__("ctypes").c_int64(0)
+    assert _lib.lib.srbd_selftest_log1p(_lib.fptr(t), t.size, _lib.fptr(out), None, __import__("ctypes").byref(nfb)) == 0
+    want = np.log1p(t.astype(np.float64)).astype(f32)
+    bad = np.flatnonzero(out.view(np.uint32) != want.view(np.uint32))
+    assert bad.size == 0, (t[bad[:5]], out[bad[:5]], want[bad[:5]])
+    # the uniform part of the sample: fallbacks well under 1e-3 of it
+    assert nfb.value < 1e-3 * t.size, nfb.value
