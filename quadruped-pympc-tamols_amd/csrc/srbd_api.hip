@@ -48,6 +48,7 @@ int quad_samples_per_block(int n_local) {
     return 64;
 }
 constexpr int MAX_RECORDS = 8192;  // merge_kernel holds 8 record minima per thread x 1024 threads
+constexpr int TAGGED_OUT = -1;     // enqueue_device_step: the launch writes tagged outputs (wait_tagged), no flag
 }  // namespace
 
 struct srbd_ctx {
@@ -113,6 +114,9 @@ struct srbd_ctx {
     // fast_tail (fast_tail_ok, SRBD_FAST_TAIL=0 turns it off): the node records the folders hand over, tagged words
     bool fast_tail = false;
     uint64_t* d_gtag = nullptr;
+    // its host-step outputs as tagged words (GroupArgs::outt, tagged_outputs), host-mapped
+    uint64_t* h_outt = nullptr;
+    uint64_t* d_outt = nullptr;
     // host steps pass the step input to the rollout as a kernel argument (ks_ok): no upload kernel
     bool ks = false;
     hipGraphExec_t g_dev2 = nullptr, g_dev1 = nullptr;
@@ -438,9 +442,14 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
             c->final_merge = false;
         const char* ft = getenv("SRBD_FAST_TAIL");
         if (c->final_merge && fast_tail_ok(mc, c->mode, c->ngroups, c->wrec_stride) && !(ft && !strcmp(ft, "0"))) {
-            const size_t tb = sizeof(uint64_t) * (size_t)c->ngroups * (REC_HDR + mc.P);
+            const size_t tb = sizeof(uint64_t) * (size_t)FT_GTAG_WORDS(mc.P);
+            const size_t ob = sizeof(uint64_t) * (size_t)(mc.P + TAGGED_OUT_EXTRA);
             c->fast_tail = hipMalloc((void**)&c->d_gtag, tb) == hipSuccess &&
-                           hipMemsetAsync(c->d_gtag, 0, tb, c->stream) == hipSuccess;
+                           hipMemsetAsync(c->d_gtag, 0, tb, c->stream) == hipSuccess &&
+                           hipHostMalloc((void**)&c->h_outt, ob, hipHostMallocMapped | hipHostMallocCoherent) ==
+                               hipSuccess &&
+                           hipHostGetDevicePointer((void**)&c->d_outt, c->h_outt, 0) == hipSuccess;
+            if (c->h_outt) memset(c->h_outt, 0, ob);
         }
         if ((e = hipMemsetAsync(c->d_gcnt, 0, sizeof(uint32_t) * (size_t)c->ngroups, c->stream)) != hipSuccess)
             return cleanup_fail("hipMemset", e);
@@ -480,6 +489,7 @@ extern "C" void srbd_destroy(srbd_ctx* c) {
     (void)hipFree(c->d_gcnt);
     (void)hipFree(c->d_gdone);
     (void)hipFree(c->d_gtag);
+    if (c->h_outt) (void)hipHostFree(c->h_outt);
     (void)hipFree(c->d_ga_freq);
     if (c->h_in) (void)hipHostFree(c->h_in);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -605,10 +615,11 @@ static int enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput
         if (c->fast_tail) {
             grp.fast = 1;
             grp.gtag = c->d_gtag;
+            if (!pub.gate) grp.outt = c->d_outt;  // armed chains keep the flag (their cancel token travels in it)
         }
         launch_rollout(mc, c->d_in, c->d_noise[buf], costs ? costs : c->d_costs, c->d_wrec, c->wrec_stride, c->mode,
                        c->threads, c->stream, fuse_next ? &next : nullptr, grp);
-        return 1;
+        return grp.outt ? TAGGED_OUT : 1;
     }
     launch_rollout(mc, c->d_in, c->d_noise[buf], costs ? costs : c->d_costs, c->d_wrec, c->wrec_stride, c->mode,
                    c->threads, c->stream, fuse_next ? &next : nullptr, grp);
@@ -671,6 +682,44 @@ static int check_handoff(srbd_ctx* c) {
     if (c->d_gdone) HIP_TRY(c, hipMemset(c->d_gdone, 0, sizeof(uint32_t)));
     c->h_out->status = 0;
     return fail(c, SRBD_E_HIP, "merge hand-off timed out (status " + std::to_string(st) + ")");
+}
+
+// A fast_tail host step wrote its outputs as tagged words (GroupArgs::outt): wait until every word carries `seq`
+// (word by word from the last, so a spin reads one word), then unpack them into h_out for copy_out.  The GPU's
+// stores reach host memory in any order; a word is whole (one 8-byte store), so a tagged word is that step's value.
+static int wait_tagged(srbd_ctx* c, uint32_t seq) {
+    const int P = c->mc.P, n = P + TAGGED_OUT_EXTRA;
+    const uint64_t* w = c->h_outt;
+    auto tag_ok = [&](int i) { return (uint32_t)(__atomic_load_n(w + i, __ATOMIC_ACQUIRE) >> 32) == seq; };
+    int i = n - 1;
+    for (uint64_t it = 1; i >= 0; ++it) {
+        if (tag_ok(i)) {
+            --i;
+            continue;
+        }
+        if ((it & 4095) == 0) {
+            const hipError_t e = hipStreamQuery(c->stream);
+            if (e == hipSuccess) {  // drained: every store of the launch has landed
+                while (i >= 0 && tag_ok(i)) --i;
+                if (i < 0) break;
+                if (c->d_gcnt) (void)hipMemsetAsync(c->d_gcnt, 0, sizeof(uint32_t) * (size_t)c->ngroups, c->stream);
+                if (c->d_gdone) (void)hipMemsetAsync(c->d_gdone, 0, sizeof(uint32_t), c->stream);
+                return fail(c, SRBD_E_HIP, "step completed without publishing its outputs");
+            }
+            if (e != hipErrorNotReady) HIP_TRY(c, e);
+        }
+        __builtin_ia32_pause();
+    }
+    StepOutput& o = *c->h_out;
+    auto val = [&](int k) { return (uint32_t)__atomic_load_n(w + k, __ATOMIC_RELAXED); };
+    for (int j = 0; j < P; ++j) o.best[j] = u2f(val(j));
+    for (int k = 0; k < 12; ++k) o.grf[k] = u2f(val(P + k));
+    for (int k = 0; k < 24; ++k) o.pred[k] = u2f(val(P + 12 + k));
+    o.best_cost = u2f(val(P + 36));
+    o.best_index = (int32_t)val(P + 37);
+    o.best_freq = u2f(val(P + 38));
+    o.status = (int32_t)val(P + 39);
+    return SRBD_OK;
 }
 
 static int copy_out(srbd_ctx* c, float* best, float* sigma, srbd_result* out) {
@@ -805,7 +854,8 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
     }
     if (want_arm && !out_costs) arm();
     int cancelled = 0;
-    if ((rc = wait_published(c, seq, nflags, fire ? &cancelled : nullptr))) return rc;
+    if ((rc = nflags == TAGGED_OUT ? wait_tagged(c, seq) : wait_published(c, seq, nflags, fire ? &cancelled : nullptr)))
+        return rc;
     if (cancelled) {
         // The claimed chain had already given up (its copy kernel's deadline passed before the go word, e.g.
         // this thread was preempted between the claim and the go store): it computed nothing and published
@@ -825,7 +875,7 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
         c->pref_ctr = counter;
         if ((rc = launch_unarmed())) return rc;
         if (want_arm && !out_costs) arm();
-        if ((rc = wait_published(c, seq, nflags))) return rc;
+        if ((rc = nflags == TAGGED_OUT ? wait_tagged(c, seq) : wait_published(c, seq, nflags))) return rc;
     }
     if (out_costs) {
         HIP_TRY(c, hipMemcpyAsync(out_costs, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,

@@ -868,7 +868,8 @@ struct alignas(16) MergeShared {
 // the legs' contact at step 0, p / v / rpy / omega and the feet, component qc), the force-independent part of the
 // predicted state (NMPC:752-784 via CMJ:93-174) and the ModelConst values of the final GRFs, into the lane's row of
 // tail_sh -- read back in one batch by the outputs phase.
-__device__ __forceinline__ void merge_tail_load(const StepInput* in, int qc, float* tail_pre) {
+template <class IN>
+__device__ __forceinline__ void merge_tail_load(const IN* in, int qc, float* tail_pre) {
     tail_pre[0] = in->fzref[0];
 #pragma unroll
     for (int l = 0; l < 4; ++l) tail_pre[1 + l] = in->contact[l][0];
@@ -1650,37 +1651,46 @@ size_t final_merge_lds(const ModelConst& mc, int ngroups, int rec_stride) {
 // so the bits equal the two-stage form's; what changes is the hand-offs after the last leaf record:
 //  - a node's last arriving block counts itself in *gdone as soon as it knows (the count's round trip overlaps the
 //    staging of the node's leaf records), instead of after its fold and the drain of its node record;
-//  - the node's headers are formed on every wave alike (lane c = child c, scales broadcast with readlane), so the
-//    column sums follow them without a block barrier;
-//  - a folder that is not the last to count stores its node record as 8-byte words tagged with the launch's seq and
-//    exits.  The last to count keeps its own node's sums in registers, loads the other node records' words straight
-//    into registers (each polled until it carries seq: their folders counted earlier and are running), and folds
-//    the root: column j by thread j, the root key and the weights' sum on every wave alike;
-//  - outputs go straight to the host-mapped StepOutput (system-scope stores); after one barrier the tail lanes form
-//    the GRFs and the predicted state (merge_tail_grf); every wave drains its stores, one lane publishes seq.
-// LDS (carved from the rollout's noise stage `st`): the node's leaf records, then nb[P], then the tail lanes' rows.
-// A word that never arrives (bounded wait) makes the step publish status -1 (the host returns an error).
+//  - headers are formed on every wave alike (lane c = child c) and broadcast through a per-wave LDS row, so the
+//    column sums (thread j: column j, thread P: the weights' sum) follow without a block barrier;
+//  - a folder that is not the last to count hands its node record over as 8-byte words tagged with the launch's seq
+//    (the header words as soon as the node key is known) and exits.  The last to count keeps its own node's sums in
+//    registers, loads the other nodes' words straight into registers (each polled until it carries seq) and folds
+//    the root column by column;
+//  - outputs: the root sums go to LDS; after a barrier thread j forms best[j] = best_in[j] + V[j] / V[P] and writes
+//    it to the host (as a tagged word, tagged_outputs, or into StepOutput followed by the flag); after a second
+//    barrier the tail lanes (wave 3, which holds no column) form the GRFs and the predicted state (merge_tail_grf).
+// LDS (carved from the rollout's noise stage `st`, ft_lds_floats): the node's leaf records, nb[P], V[P + 1], the tail
+// lanes' rows (4 x 40), per-wave broadcast rows (child scales, root scales: 2 x 4 x 64).
+// The tagged node records (gtag, FT_GTAG_WORDS): header words [64 nodes][4] (m, -, best row, tag), then column
+// words [node][P + 1] (v[0..P), s).  A word that never arrives (bounded wait) makes the step publish status -1.
 __device__ __forceinline__ uint64_t tag_word(uint32_t seq, float v) { return ((uint64_t)seq << 32) | f2u(v); }
 __device__ __forceinline__ void st_tag(uint64_t* p, uint64_t w) {
     __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ float rdl(float v, int l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
 __device__ __forceinline__ void st_sys(void* p, float v) {
     __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+constexpr int FT_TAIL0 = 192;  // the tail lanes: a quad of wave 3 (the P + 1 <= 192 columns sit in waves 0-2)
+__host__ __device__ constexpr int ft_lds_floats(int P, int rec_stride) {
+    return TREE_FAN * rec_stride + ((P + 3) & ~3) + ((P + 4) & ~3) + 4 * 40 + 2 * 4 * 64;
 }
 __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float* noise, const float* recs,
                           int rec_stride, const GroupArgs& grp, int nroll, float* st) {
     __shared__ int last_sh, fin_sh;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int P = mc.P, TW = REC_HDR + P;  // TW: words of a tagged node record
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int P = mc.P, TWV = P + 1;  // TWV: column words of a tagged node record
     const bool rs = mc.method == SRBD_RANDOM_SAMPLING;
     const int g = (int)blockIdx.x / TREE_FAN;  // one leaf per four-lane block
     const int nblk = min(TREE_FAN, nroll - g * TREE_FAN);
     const int nb = min(TREE_FAN, mc.nleaf - g * TREE_FAN);  // the node's leaves
     const int ng = grp.ngroups;
     const uint32_t seq = grp.seq;
+#ifdef SRBD_ROLLOUT_STAMPS  // probe build: thread 0's time at mark i of the last folder
+#define FT_MARK(i) if (tid == 0) g_fstamp[i] = __builtin_amdgcn_s_memrealtime()
+#else
+#define FT_MARK(i)
+#endif
     SRBD_LSTAMP(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's leaf record stores have completed
     __syncthreads();
@@ -1702,62 +1712,28 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
     __syncthreads();
     SRBD_LSTAMP(3);
     const bool fin = fin_sh;
+    // the step input through a global pointer: generic (flat) loads count in lgkmcnt too, so every LDS read after
+    // them would wait for their memory round trip (the kernel argument segment is global memory as well)
+    const auto gin = (const __attribute__((address_space(1))) StepInput*)in;
     float* nbv = st + TREE_FAN * rec_stride;  // the new parameters (the tail lanes read them)
-    float* tsh = nbv + ((P + 3) & ~3);        // the tail lanes' merge_tail_lane rows, 4 x 40
+    float* vsh = nbv + ((P + 3) & ~3);        // the root sums V[0..P]
+    float* tsh = vsh + ((P + 4) & ~3);        // the tail lanes' merge_tail_lane rows, 4 x 40
+    float* wsc = tsh + 4 * 40 + 64 * wv;      // this wave's broadcast rows: child scales,
+    float* wnsc = wsc + 4 * 64;               // root scales
     const int j = tid;
-    const bool col = !rs && j < P;
-    // the last folder: the other nodes' words into registers, in two batches of TREE_FAN / 2 nodes (all 32 at once
-    // spilled): the headers and batch A in flight during the own fold, batch B right after it
-    constexpr int HB = TREE_FAN / 2;
-    uint64_t xa[HB], xb[HB], hw[4];
-    // the words through a buffer descriptor: word w of node h at voffset 8 w, soffset 8 h TW (one VGPR of address
-    // per thread, not a 64-bit pointer per node), sc1 as an agent-scope atomic load has it.  Not volatile: the
-    // compiler then waits for each such load before the next (16 round trips in a row); the poll's re-reads are
-    // kept apart by an asm memory clobber instead.
-    const auto grs = __builtin_amdgcn_make_buffer_rsrc((void*)grp.gtag, (short)0, ng * TW * 8, 0x00020000);
-    auto ldw = [&](int h, int w) -> uint64_t {  // h uniform (an SGPR offset; a lane-varying one is a waterfall loop)
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(grs, 8 * w, 8 * h * TW, 16);
-        return ((uint64_t)v[1] << 32) | v[0];
-    };
-    auto ldh = [&](int i) -> uint64_t {  // header word i of node `lane`
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(grs, 8 * (lane * TW + i), 0, 16);
-        return ((uint64_t)v[1] << 32) | v[0];
-    };
-    auto want = [&](int h) { return col && h < ng && h != g; };
-    float b0 = 0.0f;
-    const bool hv = lane < ng && lane != g;  // header lanes (every wave): node `lane`'s words 0..3
-    auto issue = [&](uint64_t(&x)[HB], int h0) {
-#pragma unroll
-        for (int u = 0; u < HB; ++u) x[u] = want(h0 + u) ? ldw(h0 + u, REC_HDR + j) : tag_word(seq, 0.0f);
-    };
-    // bounded poll: re-read every word of `x` (nodes h0..) whose tag is not this launch's seq
-    int late = 0;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    auto poll = [&](uint64_t* x, int n, auto&& reload) {
-        for (;;) {
-            bool p = false;
-            for (int u = 0; u < n; ++u) p |= (uint32_t)(x[u] >> 32) != seq;
-            if (!p) return;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > XCHG_TIMEOUT_TICKS) {
-                late = 1;
-                return;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            asm volatile("" ::: "memory");  // the words may have changed: re-read them
-            for (int u = 0; u < n; ++u)
-                if ((uint32_t)(x[u] >> 32) != seq) x[u] = reload(u);
-        }
-    };
-    if (fin) {
-        if (tid < 4) {  // the predicted state's force-independent part (before the words: registers)
+    const bool col = !rs && j <= P;                  // column j (P: the weights' sum s)
+    const int jw = j < P ? REC_HDR + j : 1;          // its word in a record
+    const bool tl = tid >= FT_TAIL0 && tid < FT_TAIL0 + 4;  // tail lanes, component tid - FT_TAIL0 (lane 3 = z)
+    const int qc = tid - FT_TAIL0 < 3 ? tid - FT_TAIL0 : 2;
+    float b0 = 0.0f, state_hi = 0.0f;
+    if (fin) {  // step-input values the outputs need, in flight during the fold
+        if (tl) {  // the predicted state's force-independent part
             float tail_pre[13];
-            merge_tail_load(in, tid < 3 ? tid : 2, tail_pre);
-            merge_tail_lane(mc, tid < 3 ? tid : 2, tail_pre, tsh + 40 * tid);
+            merge_tail_load(gin, qc, tail_pre);
+            merge_tail_lane(mc, qc, tail_pre, tsh + 40 * (tid - FT_TAIL0));
         }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) hw[i] = hv ? ldh(i) : tag_word(seq, 0.0f);
-        issue(xa, 0);
-        if (j < P) b0 = in->best[j];  // the input parameters, read early (kernel argument or device StepInput)
+        if (j < P) b0 = gin->best[j];
+        if (tid >= 12 && tid < 24) state_hi = gin->state[tid];  // the prediction's pass-through half
     }
     // ---- the node (fold_node_lds's arithmetic): key and child scales on every wave (lane c = child c)
     const float* R = st + (size_t)(lane < TREE_FAN ? lane : 0) * rec_stride;
@@ -1768,133 +1744,195 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
     const uint64_t gk = wave_min_u64(key);
     const float gm = __uint_as_float((uint32_t)(gk >> 32));
     const float sc = have ? (rs ? 1.0f : expf(-1.0f * (m - gm))) : 0.0f;
-    const float gtg = rdl(r3, (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(key == gk)));  // keys are unique
+    const float gtg = __int_as_float(
+        __builtin_amdgcn_readlane(__float_as_int(r3), (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(key == gk))));
+    wsc[lane] = sc;  // this wave's row: read back below by its own lanes (in order, no barrier)
+    uint64_t* GH = grp.gtag + 4 * g;                // node g's header words
+    uint64_t* GV = grp.gtag + 256 + (size_t)g * TWV;  // its column words
+    if (!fin && tid == 0) {  // the header words first: the last folder's root key needs them before the sums
+        st_tag(GH, tag_word(seq, gm));
+        st_tag(GH + 2, tag_word(seq, __uint_as_float((uint32_t)gk)));
+        st_tag(GH + 3, tag_word(seq, gtg));
+        if (rs) st_tag(GV + P, tag_word(seq, 1.0f));
+    }
     SRBD_LSTAMP(4);
-    // column j < P: sum_c sc_c v_c[j]; column P: sum_c sc_c s_c, child by child (8 LDS loads in flight)
+    // column j: sum_c sc_c x_c in child order (fold_node_lds), 8 children's LDS loads in flight
     float a = 0.0f;
-    if (!rs && j <= P) {
-        const float* src = st + (j < P ? REC_HDR + j : 1);
+    if (col) {
+        const float* src = st + jw;
         int cb = 0;
         for (; cb + 8 <= nb; cb += 8) {
             float x[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) x[u] = src[(size_t)(cb + u) * rec_stride];
+            const float4 y0 = *reinterpret_cast<const float4*>(wsc + cb);
+            const float4 y1 = *reinterpret_cast<const float4*>(wsc + cb + 4);
+            const float y[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
 #pragma unroll
-            for (int u = 0; u < 8; ++u) a = a + rdl(sc, cb + u) * x[u];
+            for (int u = 0; u < 8; ++u) a = a + y[u] * x[u];
         }
-        for (; cb < nb; ++cb) a = a + rdl(sc, cb) * src[(size_t)cb * rec_stride];
+        for (; cb < nb; ++cb) a = a + wsc[cb] * src[(size_t)cb * rec_stride];
     }
     SRBD_LSTAMP(5);
     if (!fin) {  // hand the node record over: tagged words, no drain, no second count
-        uint64_t* G = grp.gtag + (size_t)g * TW;
-        if (col) st_tag(G + REC_HDR + j, tag_word(seq, a));
-        if (!rs && j == P) st_tag(G + 1, tag_word(seq, a));
-        if (tid == 0) {
-            st_tag(G, tag_word(seq, gm));
-            if (rs) st_tag(G + 1, tag_word(seq, 1.0f));
-            st_tag(G + 2, tag_word(seq, __uint_as_float((uint32_t)gk)));
-            st_tag(G + 3, tag_word(seq, gtg));
-        }
+        if (col) st_tag(GV + j, tag_word(seq, a));
         return;
     }
+    FT_MARK(1);  // own fold done
+#ifdef SRBD_ROLLOUT_STAMPS
+    if (tid == 0) g_fstamp[0] = blockIdx.x + 1;
+#endif
+    // ---- the other nodes' words into registers, two batches of TREE_FAN / 2 nodes (all 32 at once spilled), through a
+    // buffer descriptor (h uniform: an SGPR offset, one VGPR of address per thread), sc1 as an agent-scope atomic load
+    // has it.  Every load unconditional and unmasked (a branch per load, or a select on its result right after it,
+    // costs a wait per load); the words a thread does not need are skipped by the poll (`need`) and the sums.  The
+    // gtag allocation covers every address formed here; the poll's re-reads are kept apart by an asm memory clobber.
+    constexpr int HB = TREE_FAN / 2;
+    const auto grs = __builtin_amdgcn_make_buffer_rsrc((void*)grp.gtag, (short)0, FT_GTAG_WORDS(P) * 8, 0x00020000);
+    auto ldv = [&](int h) -> uint64_t {  // column word j of node h
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(grs, 8 * (256 + j), 8 * h * TWV, 16);
+        return ((uint64_t)v[1] << 32) | v[0];
+    };
+    auto ldh = [&](int i) -> uint64_t {  // header word i of node `lane`
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(grs, 8 * (4 * lane + i), 0, 16);
+        return ((uint64_t)v[1] << 32) | v[0];
+    };
+    const bool hv = lane < ng && lane != g;
+    uint64_t xa[HB], xb[HB], hw[3];
+    auto issue = [&](uint64_t(&x)[HB], int h0) {
+#pragma unroll
+        for (int u = 0; u < HB; ++u) x[u] = ldv(h0 + u);
+    };
+    hw[0] = ldh(0);
+    hw[1] = ldh(2);
+    hw[2] = ldh(3);
+    issue(xa, 0);
     if (ng > HB) issue(xb, HB);
-#ifdef SRBD_ROLLOUT_STAMPS
-    if (tid == 0) {
-        g_fstamp[0] = blockIdx.x + 1;
-        g_fstamp[1] = __builtin_amdgcn_s_memrealtime();  // own fold done
-    }
-#endif
-    // the own node's weights' sum, on every lane alike (column P of the fold above)
-    float s_own = 1.0f;
-    if (!rs) {
-        s_own = 0.0f;
-        for (int c = 0; c < nb; ++c) s_own = s_own + rdl(sc, c) * st[(size_t)c * rec_stride + 1];
-    }
-    // ---- the root (merge_body over ng records, one level): key, scales and the weights' sum on every wave alike
-    poll(hw, 4, [&](int i) { return ldh(i); });
-#ifdef SRBD_ROLLOUT_STAMPS
-    if (tid == 0) g_fstamp[2] = __builtin_amdgcn_s_memrealtime();  // the other nodes' headers in
-#endif
+    FT_MARK(2);  // words issued
+    int late = 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    auto poll = [&](uint64_t* x, int n, auto&& need, auto&& reload) {  // bounded: re-read needed words not tagged seq
+        for (;;) {
+            bool p = false;
+            for (int u = 0; u < n; ++u) p |= need(u) && (uint32_t)(x[u] >> 32) != seq;
+            if (!p) return;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > XCHG_TIMEOUT_TICKS) {
+                late = 1;
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            asm volatile("" ::: "memory");  // the words may have changed: re-read them
+            for (int u = 0; u < n; ++u)
+                if (need(u) && (uint32_t)(x[u] >> 32) != seq) x[u] = reload(u);
+        }
+    };
+    // ---- the root (merge_body over ng records, one level): key and scales on every wave alike
+    poll(hw, 3, [&](int) { return hv; }, [&](int i) { return ldh(i == 0 ? 0 : i + 1); });
+    FT_MARK(3);  // headers in
     const bool hl = lane < ng;
     const float mh = lane == g ? gm : __uint_as_float((uint32_t)hw[0]);
-    const float sh = lane == g ? s_own : __uint_as_float((uint32_t)hw[1]);
-    const uint32_t rowh = lane == g ? (uint32_t)gk : (uint32_t)hw[2];
-    const float th = lane == g ? gtg : __uint_as_float((uint32_t)hw[3]);
+    const uint32_t rowh = lane == g ? (uint32_t)gk : (uint32_t)hw[1];
+    const float th = lane == g ? gtg : __uint_as_float((uint32_t)hw[2]);
     const uint64_t kh = hl ? ((uint64_t)__float_as_uint(mh) << 32) | rowh : KEY_NONE;
     const uint64_t bk = wave_min_u64(kh);
     const float beta = __uint_as_float((uint32_t)(bk >> 32));
     const float nsc = hl && !rs ? expf(-1.0f * (mh - beta)) : 0.0f;
-    const float btag = rdl(th, (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(kh == bk)));
-    float s_root = 0.0f, V = 0.0f;
-    if (!rs) {
-        for (int h = 0; h < ng; ++h) s_root = s_root + rdl(nsc, h) * rdl(sh, h);
-        // column j, node by node in order: batch A, then batch B
+    const float btag = __int_as_float(
+        __builtin_amdgcn_readlane(__float_as_int(th), (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(kh == bk))));
+    wnsc[lane] = nsc;
+    FT_MARK(4);  // root key and scales
+    if (col) {
+        // column j's root sum V = sum_h nsc_h x_h in node order (merge_body's level): straight-line over all TREE_FAN
+        // nodes, each term added only for h < ng (V never holds -0, so skipping and adding nothing agree)
+        float V = 0.0f;
+        auto need = [&](int h) { return h < ng && h != g; };
         auto accum = [&](const uint64_t(&x)[HB], int h0) {
+            float w[HB];  // this batch's scales (registers: a whole row beside both batches spilled)
 #pragma unroll
-            for (int u = 0; u < HB; ++u)
-                if (h0 + u < ng) V = V + rdl(nsc, h0 + u) * (h0 + u == g ? a : __uint_as_float((uint32_t)x[u]));
+            for (int q = 0; q < HB / 4; ++q) {
+                const float4 t = *reinterpret_cast<const float4*>(wnsc + h0 + 4 * q);
+                w[4 * q] = t.x, w[4 * q + 1] = t.y, w[4 * q + 2] = t.z, w[4 * q + 3] = t.w;
+            }
+#pragma unroll
+            for (int u = 0; u < HB; ++u) {
+                const int h = h0 + u;
+                const float t = w[u] * (h == g ? a : __uint_as_float((uint32_t)x[u]));
+                V = h < ng ? V + t : V;
+            }
         };
-        poll(xa, HB, [&](int u) { return ldw(u, REC_HDR + j); });
+        poll(xa, HB, [&](int u) { return need(u); }, [&](int u) { return ldv(u); });
+        FT_MARK(6);  // batch A in
         accum(xa, 0);
         if (ng > HB) {
-            poll(xb, HB, [&](int u) { return ldw(HB + u, REC_HDR + j); });
+            poll(xb, HB, [&](int u) { return need(HB + u); }, [&](int u) { return ldv(HB + u); });
+            FT_MARK(8);  // batch B in
             accum(xb, HB);
         }
+        vsh[j] = V;
     }
-#ifdef SRBD_ROLLOUT_STAMPS
-    if (tid == 0) g_fstamp[3] = __builtin_amdgcn_s_memrealtime();  // root sums
-#endif
-    // ---- outputs (merge_body's values): best[j], then the tail lanes' GRFs / prediction from nb
-    StepOutput* out = grp.out;
-    if (j < P) {
-        const float v = rs ? b0 + noise[(size_t)j * mc.ldn + ((int)(uint32_t)bk - mc.row0)] : b0 + V / s_root;
-        nbv[j] = v;
-        st_sys(&out->best[j], v);
-    }
-    if (tid >= 12 && tid < 24) st_sys(&out->pred[tid], in->state[tid]);
+    FT_MARK(9);  // root sums
     late = __syncthreads_or(late);
-    if (tid == 0) {
-        st_sys(&out->best_cost, beta);
-        st_sys(&out->best_index, __uint_as_float((uint32_t)bk));
-        st_sys(&out->best_freq, btag);
-        st_sys(&out->status, __int_as_float(late ? -1 : 0));
+    FT_MARK(10);
+    // ---- outputs (merge_body's values): best[j] = best_in[j] + V[j] / V[P], then the tail lanes' GRFs / prediction.
+    // Host steps (GroupArgs::outt) write them as 8-byte words tagged with seq (tagged_outputs): the host takes the step
+    // when every word carries it, so no wave waits for its stores and no flag follows them; else StepOutput + flag.
+    StepOutput* out = grp.out;
+    uint64_t* ot = grp.outt;
+    auto put = [&](int w, float* dst, float v) {
+        if (ot)
+            __hip_atomic_store(ot + w, tag_word(seq, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else
+            st_sys(dst, v);
+    };
+    if (j < P) {
+        const float v = rs ? b0 + noise[(size_t)j * mc.ldn + ((int)(uint32_t)bk - mc.row0)] : b0 + vsh[j] / vsh[P];
+        nbv[j] = v;
+        put(j, &out->best[j], v);
     }
-    if (tid < 4) {
+    if (tid >= 12 && tid < 24) put(P + 12 + tid, &out->pred[tid], state_hi);
+    if (tid == 0) {
+        put(P + 36, &out->best_cost, beta);
+        put(P + 37, reinterpret_cast<float*>(&out->best_index), __uint_as_float((uint32_t)bk));
+        put(P + 38, &out->best_freq, btag);
+        put(P + 39, reinterpret_cast<float*>(&out->status), __int_as_float(late ? -1 : 0));
+    }
+    FT_MARK(11);  // best stored
+    __syncthreads();  // nb complete for the tail lanes
+    if (tl) {
         float ts[40];
 #pragma unroll
-        for (int i = 0; i < 40; ++i) ts[i] = tsh[40 * tid + i];
-        const int c = tid < 3 ? tid : 2;
+        for (int i = 0; i < 40; ++i) ts[i] = tsh[40 * (tid - FT_TAIL0) + i];
         float f[4], p, v, r, w;
-        merge_tail_grf(c, ts, nbv, f, p, v, r, w);
-        if (tid < 3) {
+        merge_tail_grf(qc, ts, nbv, f, p, v, r, w);
+        if (tid - FT_TAIL0 < 3) {
 #pragma unroll
-            for (int l = 0; l < 4; ++l) st_sys(&out->grf[3 * l + c], f[l]);
-            st_sys(&out->pred[c], p);
-            st_sys(&out->pred[3 + c], v);
-            st_sys(&out->pred[6 + c], r);
-            st_sys(&out->pred[9 + c], w);
+            for (int l = 0; l < 4; ++l) put(P + 3 * l + qc, &out->grf[3 * l + qc], f[l]);
+            put(P + 12 + qc, &out->pred[qc], p);
+            put(P + 15 + qc, &out->pred[3 + qc], v);
+            put(P + 18 + qc, &out->pred[6 + qc], r);
+            put(P + 21 + qc, &out->pred[9 + qc], w);
         }
     }
-#ifdef SRBD_ROLLOUT_STAMPS
-    if (tid == 0) g_fstamp[32 + 4] = __builtin_amdgcn_s_memrealtime();  // outputs issued
-#endif
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's output stores have completed
-    __syncthreads();
+    FT_MARK(12);  // outputs issued (thread 0's)
+    if (!ot) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's output stores have completed
+        __syncthreads();
+    }
     if (tid == 0) {
         __hip_atomic_store(grp.gdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-        __hip_atomic_store(grp.flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#ifdef SRBD_ROLLOUT_STAMPS
-        g_fstamp[32 + 5] = __builtin_amdgcn_s_memrealtime();
-#endif
+        if (!ot) __hip_atomic_store(grp.flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    FT_MARK(13);  // published
+#undef FT_MARK
 }
 
-// fast_tail's LDS fits the zero-order noise stage, the threads cover the columns, and the root is one level.
+// fast_tail's LDS fits the zero-order noise stage, the P + 1 columns sit in waves 0-2 (wave 3's quad is the tail's),
+// and the root is one level.
 bool fast_tail_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride) {
-    if (!final_merge_ok(mc, mode, ngroups, rec_stride) || ngroups < 2 || ngroups > TREE_FAN || mc.P + 1 > 256)
+    if (!final_merge_ok(mc, mode, ngroups, rec_stride) || ngroups < 2 || ngroups > TREE_FAN || mc.P + 1 > FT_TAIL0)
         return false;
     const int zst = 64 * (12 * mc.H + 1) > GROUP_LDS_FLOATS ? 64 * (12 * mc.H + 1) : GROUP_LDS_FLOATS;
-    return TREE_FAN * rec_stride + ((mc.P + 3) & ~3) + 4 * 40 <= zst;
+    return ft_lds_floats(mc.P, rec_stride) <= zst;
 }
 
 // The step input as a kernel argument (StepInputK): zero-order H 10 / 12 rollouts (four-lane with the LDS noise

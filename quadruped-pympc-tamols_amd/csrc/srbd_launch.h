@@ -51,7 +51,14 @@ struct GroupArgs {
     // tagged with `seq` in gtag (ngroups x (REC_HDR + P) words), polled word by word (fast_tail)
     int fast = 0;
     uint64_t* gtag = nullptr;
+    // fast_tail's outputs as tagged words (host-mapped, P + 40 of them: best[P] | grf 12 | pred 24 | best_cost,
+    // best_index, best_freq, status, each (seq << 32 | bits)) instead of StepOutput + flag (tagged_outputs)
+    uint64_t* outt = nullptr;
 };
+constexpr int TAGGED_OUT_EXTRA = 40;
+// words of the gtag buffer: header words [64][4] (a lane per node), then column words [64][P + 1] -- 64 node slots,
+// so every address fast_tail's unconditional loads form (nodes < TREE_FAN, columns < 256) lies in the allocation
+#define FT_GTAG_WORDS(P) (256 + 64 * ((P) + 1) + 256)
 bool ks_ok(const ModelConst& mc, int mode);
 bool fast_tail_ok(const ModelConst& mc, int mode, int ngroups, int rec_stride);
 // LDS the in-launch final merge needs (merge_body<256> of ngroups records) and whether the launch can do it

@@ -342,7 +342,12 @@ class Sampling_MPC:
         step, since srbd_set_state needs that step's state/reference inputs.  A fresh controller drops the
         device part with a RuntimeWarning: its compute calls start from the host part anyway."""
         self.best_control_parameters = np.array(st["best_control_parameters"], dtype=f32).reshape(-1)
-        self.master_key = np.array(st["master_key"], dtype=np.uint64 if self.rng == "philox" else np.uint32).reshape(-1)
+        want = np.uint64 if self.rng == "philox" else np.uint32  # (seed, counter) / a JAX key
+        key = np.asarray(st["master_key"])
+        if key.dtype != want or key.size != 2:
+            raise ValueError(f"set_state: master_key {key.dtype}[{key.size}] does not fit rng={self.rng!r} "
+                             f"(expects {np.dtype(want).name}[2]); the checkpoint was taken with another stream")
+        self.master_key = key.astype(want).reshape(-1)
         if "sigma_cem_mppi" in st:
             self.sigma_cem_mppi = np.array(st["sigma_cem_mppi"], dtype=f32)
         if "device_best" in st:

@@ -51,12 +51,18 @@ def main():
         st = buf.reshape(-1, NS).astype(np.int64)
         used = st[:, 0] > 0
         st = st[used]
+        if not len(st):  # no stamps (e.g. the launch timed was not a rollout of this build): skip the repetition
+            continue
         roll = st[:, 2] > 0
         t0 = st[:, 0].min()
         rel = (st - t0) / 100.0  # 100 MHz ticks -> us
         rows.append((rel, roll))
     ctx.close()
     out = {"workload": name, "n": n, "mode": os.environ.get("SRBD_ROLLOUT", "default")}
+    if not rows:
+        out["error"] = "no block stamps recorded"
+        print(json.dumps(out))
+        return
     rel, roll = rows[-1]
     out["blocks_rollout"] = int(roll.sum())
     out["blocks_rng"] = int((~roll).sum())

@@ -57,13 +57,15 @@ def main():
         t0 = st[st[:, 0] > 0, 0].min()
         us = lambda t: round((int(t) - t0) / 100.0, 2) if t else None  # noqa: E731
         lst = fs[64:].reshape(-1, 8)
-        fast = fs[32] == 0 and fs[32 + 5] != 0  # fast_tail: no merge_body stamps
+        fast = fs[32] == 0 and fs[13] != 0  # fast_tail: its own marks, no merge_body stamps
         row = {"last_leaf_sums": us(st[roll, 4].max()), "fm_block_leaf_sums": us(st[b, 4]),
                "fold_entry": us(lst[b, 0]), "fold_drained": us(lst[b, 1]), "fold_last": us(lst[b, 2]),
                "fold_staged": us(lst[b, 3]), "fold_headers": us(lst[b, 4]), "fold_sums": us(lst[b, 5])}
-        if fast:  # fast_tail's marks: own fold done, other nodes' headers in, root sums, outputs issued, published
-            for i, nm in ((1, "ft_own_fold"), (2, "ft_headers_in"), (3, "ft_root_sums"), (36, "ft_outputs"),
-                          (37, "ft_published")):
+        if fast:
+            for i, nm in ((1, "ft_own_fold"), (2, "ft_words_issued"), (3, "ft_headers_in"), (4, "ft_root_key"),
+                          (5, "ft_wsum"), (6, "ft_batch_a_in"), (7, "ft_batch_b_poll"), (8, "ft_batch_b_in"),
+                          (9, "ft_root_sums"), (10, "ft_best_stored"), (11, "ft_barrier"), (12, "ft_outputs"),
+                          (13, "ft_published")):
                 row[nm] = us(fs[i])
         else:
             row.update({"fm_entry": us(fs[1]), "fm_drained": us(fs[2]), "fm_last": us(fs[3]), "fm_staged": us(fs[4])})

@@ -24,6 +24,18 @@ def _controller(method, rng=None):
         mirror.mpc_params.pop("rng", None)
 
 
+def test_set_state_rejects_other_stream_key():
+    """A checkpoint's master_key must fit the controller's stream: uint64 (seed, counter) for Philox, a uint32 JAX
+    key otherwise -- never silently cast (a Philox counter is not a JAX key)."""
+    jx, ph = _controller("mppi", "jax"), _controller("mppi", "philox")
+    with pytest.raises(ValueError):
+        jx.set_state(ph.get_state())
+    with pytest.raises(ValueError):
+        ph.set_state(jx.get_state())
+    jx.set_state(jx.get_state())
+    ph.set_state(ph.get_state())
+
+
 def test_set_state_warns_when_device_part_dropped():
     """A fresh controller cannot take a checkpoint's device-resident part: it says so (RuntimeWarning)."""
     mpc = _controller("mppi")
