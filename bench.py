@@ -350,6 +350,42 @@ def tamols_latency(calls: int):
             "path": "srbd_tamols_run_terrain: 4 x 13 x 7 raycast patches + TAMOLS, stepping_stones_medium"}
 
 
+def c4_pipeline_latency(steps: int):
+    """C4 as one per-MPC-step sequence (BASELINE configs[3]; helpers/foothold_pipeline.py): the four heightmap
+    patches raycast on the GPU from the device-resident stepping_stones_medium scene and TAMOLS in one launch, the
+    adapted footholds into ref_state, SRBDControllerInterface.compute_control (prepare_state_and_reference + the
+    MPPI N = 10 000 H = 12 step on device draws) -- timed around the whole step from Python."""
+    import numpy as np
+
+    from quadruped_pympc_amd.helpers.foothold_pipeline import TamolsMpcStep
+    from quadruped_pympc_amd.helpers.legs_attr import LegsAttr
+    from quadruped_pympc_amd.helpers.terrain import GpuTerrain
+    from quadruped_pympc_amd.synthetic import CONFIGS, c4_config, c4_inputs
+
+    w = CONFIGS["c4"]
+    ter = GpuTerrain.stepping_stones()
+    pipe = TamolsMpcStep(ter, c4_config())
+    ins = [c4_inputs(k) for k in range(16)]
+    lat = []
+    for k in range(steps + 20):
+        state, seeds, hips, ref_base, cs = ins[k % len(ins)]
+        t0 = time.perf_counter()
+        out = pipe.step(state, LegsAttr(*seeds), LegsAttr(*hips), ref_base, cs, state["linear_velocity"],
+                        state["orientation"], state["angular_velocity"], np.zeros(4), 1.4)
+        lat.append(time.perf_counter() - t0)
+    assert np.isfinite(out[6]).all()
+    valid = sum(pipe.last_constraints[n] is not None for n in ("FL", "FR", "RL", "RR"))
+    pipe.close()
+    ter.close()
+    lat = np.array(lat[20:])
+    return {"value": round(w.num_samples / float(lat.mean()), 1), "unit": "rollouts/s",
+            "p50_ms": round(float(np.percentile(lat, 50)) * 1e3, 4),
+            "p99_ms": round(float(np.percentile(lat, 99)) * 1e3, 4), "steps": steps, "valid_legs": int(valid),
+            "workload": w.name, "path": "GpuHeightMap x4 (lazy) -> VisualFootholdAdaptation.compute_adaptation "
+                                        "(srbd_tamols_run_terrain: raycast + TAMOLS, one launch) -> ref_state -> "
+                                        "SRBDControllerInterface.compute_control (srbd_step, MPPI N=10000 H=12)"}
+
+
 # ---------------------------------------------------------------------------------------------- runs
 def run_steps(step_fn, ins, best, first_counter, count, lat=None):
     """`count` host-to-host steps, counters consecutive (the fused next-step draws are used)."""
@@ -624,13 +660,18 @@ def main(argv=None):
         line["c3"] = supplementary(_lib, "c3", args.targets, args.rng)
         # C5's 524 288 rows on one GPU: the denominator of the driver's C5 strong-scaling ratio
         line["c5_1gpu"] = supplementary(_lib, "c5", args.targets, args.rng)
-        # the headline shape on the other noise stream (Philox <-> the reference's jax.random stream)
+        # every shape on the other noise stream too (Philox <-> the reference's jax.random stream, which the
+        # drop-in Sampling_MPC draws by default)
         other = "jax" if args.rng == "philox" else "philox"
         line["c2_rng_" + other] = supplementary(_lib, "c2", args.targets, other)
+        line["north_star_65536_rng_" + other] = supplementary(_lib, "ns", args.targets, other)
+        line["c3_rng_" + other] = supplementary(_lib, "c3", args.targets, other)
+        line["c5_1gpu_rng_" + other] = supplementary(_lib, "c5", args.targets, other)
     if single and args.extras and args.config in ("c2", "c4"):  # the callers either side of the path
         line["interface_step"] = interface_latency(w, args.extras)
         line["interface_step_armed"] = interface_latency(w, args.extras, armed=True)
         line["tamols_c4"] = tamols_latency(args.extras)
+        line["c4"] = c4_pipeline_latency(args.extras)
     print(json.dumps(line), flush=True)
 
 

@@ -183,17 +183,20 @@ SRBD_HD double log1p_poly(double t) {
     return p * t;
 }
 SRBD_HD double log1p_tab(float t) {
-    if (t > -0.0078125f) return log1p_poly((double)t);
-    const double y = 1.0 + (double)t;  // exact: t's last bit is >= 2^-31 here
+    const bool small = t > -0.0078125f;  // |t| < 2^-7: the polynomial in t alone (no branch: selects below)
+    const double y = 1.0 + (double)t;    // exact when !small: t's last bit is >= 2^-31 there
     union { double d; uint64_t u; } b;
     b.d = y;
     const int e = (int)((b.u >> 52) & 0x7FF) - 1023;
     const int k = (int)((b.u >> 45) & 127);
     b.u = (b.u & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull;  // m in [1, 2)
-    const double r = fma(b.d, LOG1P_TAB[k].c, -1.0);
+    const Log1pEnt E = LOG1P_TAB[k];
+    // small: r = t, -log c = 0, e = 0, and the sum below is log1p_poly(t) itself (+0 + p == p for p != -0)
+    const double r = small ? (double)t : fma(b.d, E.c, -1.0);
+    const double nl = small ? 0.0 : E.nlogc;
+    const double ed = small ? 0.0 : (double)e;
     constexpr double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;  // hi: 32 bits
-    const double ed = (double)e;
-    return (ed * LN2_HI + LOG1P_TAB[k].nlogc) + (log1p_poly(r) + ed * LN2_LO);
+    return (ed * LN2_HI + nl) + (log1p_poly(r) + ed * LN2_LO);
 }
 // log1p_cr(t) for t in (-1, 0] -- jax_erf_inv's argument -x^2 -- at a fraction of float64 log1p's cost, the same
 // float: log1p_tab's value is rounded to float when it lies farther than 2^-40 relative (16 times its error bound)
@@ -224,9 +227,12 @@ SRBD_HD float log1p_fast(float t) {
     return f;
 }
 
+// correctly rounded float sqrt (np.sqrt's float32 result).  On the device __builtin_sqrtf is the correctly rounded
+// expansion (v_sqrt_f32 and a one-ulp fma correction); __fsqrt_rn lowers to the bare v_sqrt_f32 (within 1 ulp), which
+// made 3 of C1's 15 360 draws differ by an ulp once erf_inv's w >= 5 branch stood alone.
 SRBD_HD float sqrt_rn(float x) {
 #ifdef __HIP_DEVICE_COMPILE__
-    return __fsqrt_rn(x);
+    return __builtin_sqrtf(x);
 #else
     return sqrtf(x);
 #endif
@@ -239,11 +245,18 @@ SRBD_HD float jax_erf_inv(float x) {
     constexpr float B[9] = {-0.000200214257f, 0.000100950558f, 0.00134934322f, -0.00367342844f, 0.00573950773f,
                             -0.0076224613f,   0.00943887047f,  1.00167406f,    2.83297682f};
     float w = -log1p_fast(x * (-x));
-    const bool lt = w < 5.0f;
-    w = lt ? w - 2.5f : sqrt_rn(w) - 3.0f;
-    float p = lt ? A[0] : B[0];
+    float p;
+    if (w < 5.0f) {  // |x| < 0.9966: all but a few lanes of a wave (a branch, not 9 coefficient selects)
+        w = w - 2.5f;
+        p = A[0];
 #pragma unroll
-    for (int i = 1; i < 9; ++i) p = fmaf(p, w, lt ? A[i] : B[i]);
+        for (int i = 1; i < 9; ++i) p = fmaf(p, w, A[i]);
+    } else {
+        w = sqrt_rn(w) - 3.0f;
+        p = B[0];
+#pragma unroll
+        for (int i = 1; i < 9; ++i) p = fmaf(p, w, B[i]);
+    }
     return p * x;  // |x| == 1 (the +-inf edge) cannot occur: u lies in [nextafter(-1, 0), 1)
 }
 

@@ -151,20 +151,42 @@ class GpuTerrain:
 
 
 class GpuHeightMap:
-    """``HeightMap``-like object over a ``GpuTerrain``: ``update_height_map`` raycasts the patch on the GPU;
-    ``.data`` is (rows, cols, 1, 3); ``get_height`` is nearest-point height + 0.02, as ``PatchHeightMap``."""
+    """``HeightMap``-like object over a ``GpuTerrain``: ``update_height_map`` records the patch (centre, yaw) and the
+    raycast runs on the GPU when ``.data`` is first read; ``.data`` is (rows, cols, 1, 3); ``get_height`` is
+    nearest-point height + 0.02, as ``PatchHeightMap``.  Lazy, so ``VisualFootholdAdaptation.compute_adaptation``
+    can hand four pending patches over one terrain to the fused raycast + TAMOLS launch
+    (``TamolsSearch.run_terrain``) instead of four raycast launches and their copies (wb_interface.py:230-240
+    updates the four maps around the seeds and adapts at once)."""
 
     def __init__(self, terrain: GpuTerrain, num_rows=13, num_cols=7, dist_x=0.04, dist_y=0.04, ray_z=10.0):
         self.terrain = terrain
         self.num_rows, self.num_cols, self.dist_x, self.dist_y, self.ray_z = num_rows, num_cols, dist_x, dist_y, ray_z
-        self.data = None
+        self._data = None
+        self.pending = None  # (centre (3,), yaw) of a patch not raycast yet
 
     def update_height_map(self, center, yaw=0.0):
         c = np.asarray(center, dtype=np.float64).reshape(-1)[:3]
         if c.size < 3:
             c = np.concatenate([c, np.zeros(3 - c.size)])
-        p = self.terrain.patches(c[None], [yaw], self.num_rows, self.num_cols, self.dist_x, self.dist_y, self.ray_z)
-        self.data = p[0][:, :, None, :]
-        return self.data
+        self.pending = (c.copy(), float(yaw))
+        self._data = None
+
+    @property
+    def has_data(self) -> bool:
+        return self.pending is not None or self._data is not None
+
+    @property
+    def data(self):
+        if self.pending is not None:
+            c, yaw = self.pending
+            p = self.terrain.patches(c[None], [yaw], self.num_rows, self.num_cols, self.dist_x, self.dist_y,
+                                     self.ray_z)
+            self.set_data(p[0])
+        return self._data
+
+    def set_data(self, patch):
+        """The raycast patch (rows, cols, 3) of the pending update (the fused launch's output)."""
+        self._data = np.asarray(patch, dtype=np.float64)[:, :, None, :]
+        self.pending = None
 
     get_height = PatchHeightMap.get_height

@@ -167,6 +167,25 @@ class TamolsSearch:
         return self._result(rows, cols, want_heightmaps, want_scores)
 
 
+def _fused_patches(heightmaps, names, seeds):
+    """(terrain, yaw, first map) when the four maps are GpuHeightMaps of one terrain with one patch geometry, each
+    pending a patch around its seed at one yaw (what wb_interface.py:233-234 leaves before compute_adaptation);
+    else None."""
+    from .terrain import GpuHeightMap
+
+    maps = [heightmaps[n] for n in names]
+    if not all(isinstance(m, GpuHeightMap) and m.pending is not None for m in maps):
+        return None
+    g = maps[0]
+    geo = (g.terrain, g.num_rows, g.num_cols, g.dist_x, g.dist_y, g.ray_z, g.pending[1])
+    for m, sd in zip(maps, seeds):
+        if (m.terrain, m.num_rows, m.num_cols, m.dist_x, m.dist_y, m.ray_z, m.pending[1]) != geo:
+            return None
+        if not np.array_equal(m.pending[0], np.asarray(sd, dtype=np.float64).reshape(-1)[:3]):
+            return None
+    return g.terrain, g.pending[1], g
+
+
 class VisualFootholdAdaptation:
     def __init__(self, legs_order, adaptation_strategy="height", config_module=None, device_id=None):
         cfg = active_config(config_module)  # the reference's quadruped_pympc.config when installed
@@ -209,7 +228,8 @@ class VisualFootholdAdaptation:
                            base_orientation, base_orientation_rate, gait_phases=None, base_position=None,
                            current_contact=None, current_feet_pos=None, **_ignored):
         for leg_name in legs_order:
-            if heightmaps[leg_name].data is None:
+            hm = heightmaps[leg_name]
+            if not (hm.has_data if hasattr(hm, "has_data") else hm.data is not None):
                 return False
 
         if self.adaptation_strategy == "tamols" and tuple(legs_order) != LEGS:
@@ -223,16 +243,26 @@ class VisualFootholdAdaptation:
 
         elif self.adaptation_strategy == "tamols":
             names = list(legs_order)
-            data = np.stack([np.asarray(heightmaps[n].data, dtype=np.float64)[:, :, 0, :] for n in names])
             seeds = np.stack([np.asarray(reference_footholds[n], dtype=np.float64).copy() for n in names])
             hips = np.stack([np.asarray(hip_positions[n], dtype=np.float64) for n in names])
             contact = None if current_contact is None else np.asarray(current_contact).astype(np.int32)
             feet = None
             if current_feet_pos is not None and base_position is not None:
                 feet = np.stack([np.asarray(current_feet_pos[n], dtype=np.float64) for n in ("FL", "FR", "RL", "RR")])
-            out = self.search.run(data, seeds, hips, tamols_params_struct(self.tamols_params, self.robot_name),
-                                  forward_vel=forward_vel, base_position=base_position, current_contact=contact,
-                                  current_feet_pos=feet)
+            params = tamols_params_struct(self.tamols_params, self.robot_name)
+            fused = _fused_patches(heightmaps, names, seeds)
+            if fused is not None:  # GPU maps of one terrain, pending around the seeds: raycast + TAMOLS in one launch
+                ter, yaw, g = fused
+                out = self.search.run_terrain(ter, yaw, seeds, hips, params, rows=g.num_rows, cols=g.num_cols,
+                                              dist_x=g.dist_x, dist_y=g.dist_y, ray_z=g.ray_z,
+                                              forward_vel=forward_vel, base_position=base_position,
+                                              current_contact=contact, current_feet_pos=feet)
+                for i, n in enumerate(names):
+                    heightmaps[n].set_data(out["heightmaps"][i])
+            else:
+                data = np.stack([np.asarray(heightmaps[n].data, dtype=np.float64)[:, :, 0, :] for n in names])
+                out = self.search.run(data, seeds, hips, params, forward_vel=forward_vel, base_position=base_position,
+                                      current_contact=contact, current_feet_pos=feet)
             self.last_scores = out["scores"]
             for i, n in enumerate(names):
                 if out["valid"][i]:

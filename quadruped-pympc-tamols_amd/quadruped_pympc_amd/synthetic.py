@@ -99,3 +99,45 @@ def inputs(w: Workload, k: int = 0):
     """(state24, ref24, contact (4, H)) for MPC step k."""
     s = robot_state(w.robot, k)
     return s, reference(w.robot, s), contact_sequences(w.gait, w.horizon, k + 1)[-1]
+
+
+C4_LEGS = ("FL", "FR", "RL", "RR")
+
+
+def c4_inputs(k: int = 0, horizon: int = 12):
+    """C4 (Go2 trot on stepping_stones_medium) MPC step k: the state dict (base over the first stones, feet on
+    them), the reference footholds TAMOLS adapts (seeds, (4, 3): a stride ahead of the feet), the hips (4, 3),
+    the base reference dict and the trot contact sequence (4, H) -- the inputs of helpers/foothold_pipeline.py."""
+    feet = np.array([[1.22, 0.13, 0.05], [1.22, -0.13, 0.05], [0.84, 0.13, 0.05], [0.84, -0.13, 0.05]])
+    base = np.array([1.03 + 0.004 * k, 0.0, 0.35])
+    state = {"position": base, "linear_velocity": np.array([0.5, 0.02, 0.0]),
+             "orientation": np.array([0.01, -0.02, 0.05]), "angular_velocity": np.array([0.0, 0.1, -0.05])}
+    state.update({"foot_" + n: feet[i].copy() for i, n in enumerate(C4_LEGS)})
+    seeds = feet + np.array([0.12 + 0.002 * k, 0.01, 0.0])
+    hips = feet + np.array([0.0, 0.0, 0.3])
+    ref_base = {"ref_position": np.array([0.0, 0.0, 0.32]), "ref_linear_velocity": np.array([0.5, 0.0, 0.0]),
+                "ref_orientation": np.zeros(3), "ref_angular_velocity": np.zeros(3)}
+    cs = contact_sequences("trot", horizon, k + 3)[-1].astype(np.float64)
+    return state, seeds, hips, ref_base, cs
+
+
+def c4_config():
+    """A config module for C4 (the mirror's, switched to Go2, MPPI zero-order N = 10 000 H = 12, TAMOLS h_des at
+    the Go2 hip height, no solution shift)."""
+    import copy
+    import types
+
+    from . import config as base
+    from .config import HIP_HEIGHTS
+
+    w = CONFIGS["c4"]
+    cfg = types.SimpleNamespace(**{k: copy.deepcopy(getattr(base, k)) for k in
+                                   ("robot", "mass", "inertia", "hip_height", "gravity_constant", "mpc_params",
+                                    "simulation_params")})
+    cfg.robot, cfg.mass, cfg.inertia = w.robot, ROBOTS[w.robot][0], np.array(ROBOTS[w.robot][1])
+    cfg.hip_height = HIP_HEIGHTS[w.robot]
+    cfg.mpc_params.update(horizon=w.horizon, sampling_method=w.method, control_parametrization=w.parametrization,
+                          num_parallel_computations=w.num_samples, sigma_mppi=w.sigma, grf_max=cfg.mass * 9.81,
+                          device_id=0, shift_solution=False)
+    cfg.simulation_params["tamols_params"]["h_des"] = cfg.hip_height
+    return cfg
