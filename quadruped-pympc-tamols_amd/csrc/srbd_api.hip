@@ -1947,7 +1947,8 @@ extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, 
 // so a rocprofv3 pass over this call sees only that launch (a PMC A/B of two launches of one kernel name).
 //   SRBD_TL_STEP_ROLLOUT: the rollout launch exactly as srbd_step issues it -- the step input by value (KS), the
 //     in-launch final merge (FM, publishing into the host-mapped outputs) and the next step's draws (fused) where
-//     they apply; *form = 1 fused | 2 KS | 4 FM | 8 thread-per-sample rollout (else four lanes per sample).
+//     they apply; *form = 1 fused | 2 KS | 4 FM | 8 thread-per-sample rollout (else four lanes per sample) |
+//     16 fast_tail.
 //   SRBD_TL_STEP_MERGE: the merge launch srbd_step issues after it (0 us when the rollout launch merges).
 extern "C" int srbd_time_launch(srbd_ctx* c, int32_t which, int32_t iters, float* us, int32_t* form) {
     if (!c || iters < 1 || !us) return SRBD_E_INVALID;
@@ -1966,7 +1967,8 @@ extern "C" int srbd_time_launch(srbd_ctx* c, int32_t which, int32_t iters, float
     if (ks) fill_ksi(c, &ksi);
     if (form)
         *form = (which == SRBD_TL_STEP_ROLLOUT)
-                    ? ((fuse ? 1 : 0) | (ks ? 2 : 0) | (fm ? 4 : 0) | (c->mode == ROLLOUT_THREAD ? 8 : 0))
+                    ? ((fuse ? 1 : 0) | (ks ? 2 : 0) | (fm ? 4 : 0) | (c->mode == ROLLOUT_THREAD ? 8 : 0) |
+                       (fm && c->fast_tail ? 16 : 0))
                     : 0;
     const RngJob next{c->d_noise[1], 0, 0, 1, 1, nullptr};
     int nflags = 0;  // publish flags of the last launch (0: it publishes nothing)

@@ -1675,6 +1675,84 @@ constexpr int FT_TAIL0 = 192;  // the tail lanes: a quad of wave 3 (the P + 1 <=
 __host__ __device__ constexpr int ft_lds_floats(int P, int rec_stride) {
     return TREE_FAN * rec_stride + ((P + 3) & ~3) + ((P + 4) & ~3) + 4 * 40 + 2 * 4 * 64;
 }
+// ---- shared by fast_tail and direct_tail: the step input the outputs need (read while the sums are formed) and the
+// outputs themselves.
+// ft_prep: the tail lanes' merge_tail_lane rows into tsh (the predicted state's force-independent part), best_in[j]
+// (thread j < P) and the state's pass-through half (threads 12..23), through a global pointer: generic (flat) loads
+// count in lgkmcnt too, so every LDS read after them would wait for their memory round trip (the kernel argument
+// segment is global memory as well).
+__device__ __forceinline__ void ft_prep(const ModelConst& mc, const StepInput* in, float* tsh, float& b0,
+                                        float& state_hi) {
+    const int tid = threadIdx.x, P = mc.P;
+    const auto gin = (const __attribute__((address_space(1))) StepInput*)in;
+    if (tid >= FT_TAIL0 && tid < FT_TAIL0 + 4) {
+        const int qc = tid - FT_TAIL0 < 3 ? tid - FT_TAIL0 : 2;
+        float tail_pre[13];
+        merge_tail_load(gin, qc, tail_pre);
+        merge_tail_lane(mc, qc, tail_pre, tsh + 40 * (tid - FT_TAIL0));
+    }
+    if (tid < P) b0 = gin->best[tid];
+    if (tid >= 12 && tid < 24) state_hi = gin->state[tid];
+}
+// ft_outputs (merge_body's values), every thread of the block: vsh[0..P] holds the root sums (V[P] the weights' sum)
+// on entry (written before a barrier the caller passed); `late` != 0 on any thread publishes status -1.
+// best[j] = best_in[j] + V[j] / V[P] (random sampling: + the best row's noise), then the tail lanes' GRFs / prediction
+// (wave 3).  Host steps (GroupArgs::outt) write them as 8-byte words tagged with seq (tagged_outputs): the host takes
+// the step when every word carries it, so no wave waits for its stores and no flag follows them; else StepOutput +
+// the flag after every wave's stores have completed.
+__device__ __forceinline__ void ft_outputs(const ModelConst& mc, const GroupArgs& grp, const float* noise, bool rs,
+                                           int late, uint64_t bk, float beta, float btag, float b0, float state_hi,
+                                           float* nbv, const float* vsh, const float* tsh) {
+    const int tid = threadIdx.x, j = tid, P = mc.P;
+    const uint32_t seq = grp.seq;
+    late = __syncthreads_or(late);
+    StepOutput* out = grp.out;
+    uint64_t* ot = grp.outt;
+    auto put = [&](int w, float* dst, float v) {
+        if (ot)
+            __hip_atomic_store(ot + w, tag_word(seq, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else
+            st_sys(dst, v);
+    };
+    if (j < P) {
+        const float v = rs ? b0 + noise[(size_t)j * mc.ldn + ((int)(uint32_t)bk - mc.row0)] : b0 + vsh[j] / vsh[P];
+        nbv[j] = v;
+        put(j, &out->best[j], v);
+    }
+    if (tid >= 12 && tid < 24) put(P + 12 + tid, &out->pred[tid], state_hi);
+    if (tid == 0) {
+        put(P + 36, &out->best_cost, beta);
+        put(P + 37, reinterpret_cast<float*>(&out->best_index), __uint_as_float((uint32_t)bk));
+        put(P + 38, &out->best_freq, btag);
+        put(P + 39, reinterpret_cast<float*>(&out->status), __int_as_float(late ? -1 : 0));
+    }
+    __syncthreads();  // nb complete for the tail lanes
+    if (tid >= FT_TAIL0 && tid < FT_TAIL0 + 4) {
+        const int qc = tid - FT_TAIL0 < 3 ? tid - FT_TAIL0 : 2;
+        float ts[40];
+#pragma unroll
+        for (int i = 0; i < 40; ++i) ts[i] = tsh[40 * (tid - FT_TAIL0) + i];
+        float f[4], p, v, r, w;
+        merge_tail_grf(qc, ts, nbv, f, p, v, r, w);
+        if (tid - FT_TAIL0 < 3) {
+#pragma unroll
+            for (int l = 0; l < 4; ++l) put(P + 3 * l + qc, &out->grf[3 * l + qc], f[l]);
+            put(P + 12 + qc, &out->pred[qc], p);
+            put(P + 15 + qc, &out->pred[3 + qc], v);
+            put(P + 18 + qc, &out->pred[6 + qc], r);
+            put(P + 21 + qc, &out->pred[9 + qc], w);
+        }
+    }
+    if (!ot) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's output stores have completed
+        __syncthreads();
+    }
+    if (tid == 0) {
+        __hip_atomic_store(grp.gdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+        if (!ot) __hip_atomic_store(grp.flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float* noise, const float* recs,
                           int rec_stride, const GroupArgs& grp, int nroll, float* st) {
     __shared__ int last_sh, fin_sh;
@@ -1712,9 +1790,6 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
     __syncthreads();
     SRBD_LSTAMP(3);
     const bool fin = fin_sh;
-    // the step input through a global pointer: generic (flat) loads count in lgkmcnt too, so every LDS read after
-    // them would wait for their memory round trip (the kernel argument segment is global memory as well)
-    const auto gin = (const __attribute__((address_space(1))) StepInput*)in;
     float* nbv = st + TREE_FAN * rec_stride;  // the new parameters (the tail lanes read them)
     float* vsh = nbv + ((P + 3) & ~3);        // the root sums V[0..P]
     float* tsh = vsh + ((P + 4) & ~3);        // the tail lanes' merge_tail_lane rows, 4 x 40
@@ -1723,18 +1798,8 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
     const int j = tid;
     const bool col = !rs && j <= P;                  // column j (P: the weights' sum s)
     const int jw = j < P ? REC_HDR + j : 1;          // its word in a record
-    const bool tl = tid >= FT_TAIL0 && tid < FT_TAIL0 + 4;  // tail lanes, component tid - FT_TAIL0 (lane 3 = z)
-    const int qc = tid - FT_TAIL0 < 3 ? tid - FT_TAIL0 : 2;
     float b0 = 0.0f, state_hi = 0.0f;
-    if (fin) {  // step-input values the outputs need, in flight during the fold
-        if (tl) {  // the predicted state's force-independent part
-            float tail_pre[13];
-            merge_tail_load(gin, qc, tail_pre);
-            merge_tail_lane(mc, qc, tail_pre, tsh + 40 * (tid - FT_TAIL0));
-        }
-        if (j < P) b0 = gin->best[j];
-        if (tid >= 12 && tid < 24) state_hi = gin->state[tid];  // the prediction's pass-through half
-    }
+    if (fin) ft_prep(mc, in, tsh, b0, state_hi);  // in flight during the fold
     // ---- the node (fold_node_lds's arithmetic): key and child scales on every wave (lane c = child c)
     const float* R = st + (size_t)(lane < TREE_FAN ? lane : 0) * rec_stride;
     const bool have = lane < nb;
@@ -1871,57 +1936,8 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
         vsh[j] = V;
     }
     FT_MARK(9);  // root sums
-    late = __syncthreads_or(late);
     FT_MARK(10);
-    // ---- outputs (merge_body's values): best[j] = best_in[j] + V[j] / V[P], then the tail lanes' GRFs / prediction.
-    // Host steps (GroupArgs::outt) write them as 8-byte words tagged with seq (tagged_outputs): the host takes the step
-    // when every word carries it, so no wave waits for its stores and no flag follows them; else StepOutput + flag.
-    StepOutput* out = grp.out;
-    uint64_t* ot = grp.outt;
-    auto put = [&](int w, float* dst, float v) {
-        if (ot)
-            __hip_atomic_store(ot + w, tag_word(seq, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        else
-            st_sys(dst, v);
-    };
-    if (j < P) {
-        const float v = rs ? b0 + noise[(size_t)j * mc.ldn + ((int)(uint32_t)bk - mc.row0)] : b0 + vsh[j] / vsh[P];
-        nbv[j] = v;
-        put(j, &out->best[j], v);
-    }
-    if (tid >= 12 && tid < 24) put(P + 12 + tid, &out->pred[tid], state_hi);
-    if (tid == 0) {
-        put(P + 36, &out->best_cost, beta);
-        put(P + 37, reinterpret_cast<float*>(&out->best_index), __uint_as_float((uint32_t)bk));
-        put(P + 38, &out->best_freq, btag);
-        put(P + 39, reinterpret_cast<float*>(&out->status), __int_as_float(late ? -1 : 0));
-    }
-    FT_MARK(11);  // best stored
-    __syncthreads();  // nb complete for the tail lanes
-    if (tl) {
-        float ts[40];
-#pragma unroll
-        for (int i = 0; i < 40; ++i) ts[i] = tsh[40 * (tid - FT_TAIL0) + i];
-        float f[4], p, v, r, w;
-        merge_tail_grf(qc, ts, nbv, f, p, v, r, w);
-        if (tid - FT_TAIL0 < 3) {
-#pragma unroll
-            for (int l = 0; l < 4; ++l) put(P + 3 * l + qc, &out->grf[3 * l + qc], f[l]);
-            put(P + 12 + qc, &out->pred[qc], p);
-            put(P + 15 + qc, &out->pred[3 + qc], v);
-            put(P + 18 + qc, &out->pred[6 + qc], r);
-            put(P + 21 + qc, &out->pred[9 + qc], w);
-        }
-    }
-    FT_MARK(12);  // outputs issued (thread 0's)
-    if (!ot) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's output stores have completed
-        __syncthreads();
-    }
-    if (tid == 0) {
-        __hip_atomic_store(grp.gdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-        if (!ot) __hip_atomic_store(grp.flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    ft_outputs(mc, grp, noise, rs, late, bk, beta, btag, b0, state_hi, nbv, vsh, tsh);
     FT_MARK(13);  // published
 #undef FT_MARK
 }

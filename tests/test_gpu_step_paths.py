@@ -174,6 +174,7 @@ def test_fast_tail_equals_two_stage(lib, monkeypatch, method, N, H, noise):
             if k == 0:
                 np.testing.assert_array_equal(a[3], b[3])
             bf, bs = a[0], b[0]
+        assert fast.time_launch(3, 2)[1] & 16 and not slow.time_launch(3, 2)[1] & 16  # the tails the steps ran
     finally:
         fast.close()
         slow.close()
