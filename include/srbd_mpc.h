@@ -248,7 +248,8 @@ int srbd_time_kernels(srbd_ctx* ctx, int32_t iters, float* rollout_us, float* rn
 /* Measurement: average duration (us) of one kind of launch, `iters` back to back (one hipEvent pair), alone, so
  * a rocprofv3 pass over the call sees only it.  SRBD_TL_STEP_ROLLOUT is the rollout launch exactly as srbd_step
  * issues it (*form: 1 fused next-step draws | 2 step input by value | 4 in-launch final merge | 8 thread-per-sample
- * rollout kernel, else four lanes per sample | 16 fast_tail); SRBD_TL_STEP_MERGE
+ * rollout kernel, else four lanes per sample | 16 fast_tail | 32 the launch makes the step's
+ * draws itself: srbd_step then issues no RNG launch); SRBD_TL_STEP_MERGE
  * the merge launch srbd_step issues after it (0 when the rollout launch merges).  form may be NULL. */
 enum { SRBD_TL_RNG = 0, SRBD_TL_ROLLOUT = 1, SRBD_TL_ROLLOUT_FUSED = 2, SRBD_TL_STEP_ROLLOUT = 3,
        SRBD_TL_STEP_MERGE = 4, SRBD_TL_EMPTY = 5 };

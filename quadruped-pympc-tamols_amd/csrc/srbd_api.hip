@@ -113,6 +113,8 @@ struct srbd_ctx {
     uint32_t* d_gdone = nullptr;
     // fast_tail (fast_tail_ok, SRBD_FAST_TAIL=0 turns it off): the node records the folders hand over, tagged words
     bool fast_tail = false;
+    bool gen_env = true;  // SRBD_GEN != "0" at create (gen_now)
+    int gen_rg = GEN_REGEN_QUADS;  // quads the epilogue regenerates (SRBD_GEN_RG at create), the rest stored and read
     uint64_t* d_gtag = nullptr;
     // its host-step outputs as tagged words (GroupArgs::outt, tagged_outputs), host-mapped
     uint64_t* h_outt = nullptr;
@@ -429,6 +431,9 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     // every block writes lpb leaf records (the last block's past nleaf are never read)
     if ((e = hipMalloc((void**)&c->d_wrec, sizeof(float) * (size_t)c->nblocks * c->lpb * c->wrec_stride)) != hipSuccess)
         return cleanup_fail("hipMalloc", e);
+    const char* ge = getenv("SRBD_GEN");
+    c->gen_env = !(ge && !strcmp(ge, "0"));
+    if (const char* gr = getenv("SRBD_GEN_RG")) c->gen_rg = std::max(0, std::min(mc.P / 4, atoi(gr)));
     c->gsize = group_size(mc);
     c->ngroups = (c->nleaf + TREE_FAN - 1) / TREE_FAN;
     if (c->gsize > 1) {
@@ -528,6 +533,13 @@ extern "C" int srbd_set_stream(srbd_ctx* c, void* s) {
 constexpr int FUSE_MAX_ROWS = 65536;
 static bool fusable(const srbd_ctx* c) { return c->mc.n_local <= FUSE_MAX_ROWS; }
 
+// The step's draws made inside the rollout launch (gen_ok; SRBD_GEN=0 turns it off): host steps (the input by value)
+// at shapes whose draws do not fuse into the previous launch, device Philox stream.  The caller also checks that no
+// noise is injected.
+static bool gen_now(const srbd_ctx* c) {
+    return c->gen_env && c->ks && !fusable(c) && gen_ok(c->mc, c->mode);
+}
+
 // Device-chain steps draw on the device: CEM draws are then unscaled (StepInput::noise_scaled = 0)
 // whatever the last host step injected.
 static int reset_noise_scaled(srbd_ctx* c) {
@@ -553,9 +565,12 @@ static int upload_noise(srbd_ctx* c, const float* noise, int buf) {
 // Noise of a step: injected (noise != NULL), the draws the previous step's rollout launch made when
 // (seed, counter) match its prediction, else device draws generated now on the step's stream.
 // Returns in *buf the buffer holding them.  Everything is ordered on one stream.
-static int acquire_noise(srbd_ctx* c, const float* noise, uint64_t seed, uint64_t ctr, int* buf) {
+// gen: the rollout launch makes the step's draws itself (gen_now): nothing to draw here.
+static int acquire_noise(srbd_ctx* c, const float* noise, uint64_t seed, uint64_t ctr, int* buf, bool gen = false) {
     int rc = SRBD_OK;
-    if (!noise && c->pref_valid && c->pref_seed == seed && c->pref_ctr == ctr) {
+    if (gen && !noise) {
+        *buf = c->cur;
+    } else if (!noise && c->pref_valid && c->pref_seed == seed && c->pref_ctr == ctr) {
         *buf = c->pref_buf;
     } else {
         *buf = c->cur;
@@ -597,12 +612,13 @@ static int levels_up(const srbd_ctx* c) { return c->mc.t_xlevel - (c->gsize > 1 
 // Returns the number of merge blocks that publish (wait_published).
 static int enqueue_device_step(srbd_ctx* c, int buf, float* rank_out, StepOutput* out, int chain = 0,
                                int ctr_inc = 1, bool fuse_next = false, Publish pub = {nullptr, 0},
-                               float* costs = nullptr, const void* ksi = nullptr) {
+                               float* costs = nullptr, const void* ksi = nullptr, bool gen = false) {
     const ModelConst& mc = c->mc;
     const RngJob next{c->d_noise[1 - buf], 0, 0, 1, 1, pub.gate};
     GroupArgs grp = grp_of(c);
     grp.gate = pub.gate;
     grp.ksi = ksi;
+    grp.gen = gen && !fuse_next ? 1 + c->gen_rg : 0;
     // the rollout launch merges and publishes (not for the gait-adaptive rollout or the cost terms, which
     // srbd_set_gait / srbd_set_cost_terms can switch on after create: other kernels)
     if (c->final_merge && !mc.ga && !mc.cost_on && out && !rank_out && !chain && pub.flag) {
@@ -813,11 +829,13 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
         else if ((r = upload_input(c)))
             return r;
         int buf = 0;
-        if ((r = acquire_noise(c, noise, seed, counter, &buf))) return r;
+        const bool gen = !noise && gen_now(c);
+        if ((r = acquire_noise(c, noise, seed, counter, &buf, gen))) return r;
         const bool fuse = !noise && fusable(c);
         const Publish pub{c->d_flag, ++c->seq, nullptr};
         seq = pub.seq;
-        nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fuse, pub, nullptr, ks ? &ksi : nullptr);
+        nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fuse, pub, nullptr, ks ? &ksi : nullptr,
+                                     gen);
         HIP_TRY(c, hipGetLastError());
         if (fuse) {
             c->pref_valid = true;
@@ -1948,7 +1966,7 @@ extern "C" int srbd_time_kernels(srbd_ctx* c, int32_t iters, float* rollout_us, 
 //   SRBD_TL_STEP_ROLLOUT: the rollout launch exactly as srbd_step issues it -- the step input by value (KS), the
 //     in-launch final merge (FM, publishing into the host-mapped outputs) and the next step's draws (fused) where
 //     they apply; *form = 1 fused | 2 KS | 4 FM | 8 thread-per-sample rollout (else four lanes per sample) |
-//     16 fast_tail.
+//     16 fast_tail | 32 the step's draws made in the launch (gen_now: srbd_step issues no RNG launch).
 //   SRBD_TL_STEP_MERGE: the merge launch srbd_step issues after it (0 us when the rollout launch merges).
 extern "C" int srbd_time_launch(srbd_ctx* c, int32_t which, int32_t iters, float* us, int32_t* form) {
     if (!c || iters < 1 || !us) return SRBD_E_INVALID;
@@ -1963,12 +1981,13 @@ extern "C" int srbd_time_launch(srbd_ctx* c, int32_t which, int32_t iters, float
     const bool fuse = fusable(c);
     const bool ks = c->ks && !mc.ga && !mc.cost_on;
     const bool fm = c->final_merge && !mc.ga && !mc.cost_on;
+    const bool gen = gen_now(c) && ks;
     StepInputK ksi;
     if (ks) fill_ksi(c, &ksi);
     if (form)
         *form = (which == SRBD_TL_STEP_ROLLOUT)
                     ? ((fuse ? 1 : 0) | (ks ? 2 : 0) | (fm ? 4 : 0) | (c->mode == ROLLOUT_THREAD ? 8 : 0) |
-                       (fm && c->fast_tail ? 16 : 0))
+                       (fm && c->fast_tail ? 16 : 0) | (gen ? 32 : 0))
                     : 0;
     const RngJob next{c->d_noise[1], 0, 0, 1, 1, nullptr};
     int nflags = 0;  // publish flags of the last launch (0: it publishes nothing)
@@ -1983,6 +2002,7 @@ extern "C" int srbd_time_launch(srbd_ctx* c, int32_t which, int32_t iters, float
             case SRBD_TL_STEP_ROLLOUT: {
                 GroupArgs grp = grp_of(c);
                 grp.ksi = ks ? &ksi : nullptr;
+                grp.gen = gen ? 1 + c->gen_rg : 0;
                 if (fm) {
                     grp.out = c->d_out_host;
                     grp.flag = c->d_flag;

@@ -482,11 +482,13 @@ __device__ __forceinline__ float wave_sum_f32(float v) { return lane_tree_f32<6>
 // draws are regenerated here (the same Philox4x32-10 call and Box-Muller pairs rng_item made, so the same bits)
 // instead of re-read; the rest are re-read.  That trades VALU issue for HBM reads where the launch has both to
 // spare (C5 issue 71.6 of 104 us, 656 MB read).
+// RG = 2 (the in-launch draws, GroupArgs::gen: the rollout made the step's draws itself and stored only quads
+// [gen - 1, P / 4)): quads [0, gen - 1) are regenerated.
 constexpr int REGEN_QUADS = 16;  // C5 step launch 106.8 / 98.3 / 96.5 / 97.1 / 98.7 us at 0 / 12 / 16 / 20 / 24 of 36
-template <int SPL, bool RG>
+template <int SPL, int RG>
 __device__ __forceinline__ void leaf_wsum_lanes(const ModelConst& mc, const StepInput* __restrict__ in,
                                                 const float* __restrict__ base, bool zs, const float* e_sh,
-                                                float* rbuf, int rec_stride, int k0) {
+                                                float* rbuf, int rec_stride, int k0, int gen = 0) {
     constexpr int CB = SPL == 4 ? 8 : 12;
     constexpr int LPL = 64 / SPL;  // lanes per leaf
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, NW = blockDim.x >> 6;
@@ -499,9 +501,10 @@ __device__ __forceinline__ void leaf_wsum_lanes(const ModelConst& mc, const Step
     const bool writer = (lane % LPL) == LPL - 1;
     int jreg = 0;  // columns [0, jreg) regenerated
     if constexpr (RG && SPL == 4) {
-        if (mc.method == SRBD_MPPI && mc.rng == RNG_PHILOX && in->noise_scaled == 0 && 4 * REGEN_QUADS <= P) {
+        if (RG == 2 || (mc.method == SRBD_MPPI && mc.rng == RNG_PHILOX && in->noise_scaled == 0 && 4 * REGEN_QUADS <= P)) {
             const uint32_t key0 = in->seed_lo, key1 = in->seed_hi, c2 = in->ctr_lo, c3 = in->ctr_hi;
-            for (int q = w; q < REGEN_QUADS; q += NW) {
+            const int nq = RG == 2 ? gen - 1 : REGEN_QUADS;
+            for (int q = w; q < nq; q += NW) {
                 float zq[4][SPL];  // [column 4q + i][row u]
 #pragma unroll
                 for (int u = 0; u < SPL; ++u) {
@@ -526,7 +529,7 @@ __device__ __forceinline__ void leaf_wsum_lanes(const ModelConst& mc, const Step
                     if (writer) rec[REC_HDR + 4 * q + i] = a;
                 }
             }
-            jreg = 4 * REGEN_QUADS;
+            jreg = 4 * nq;
         }
     }
     for (int j0 = jreg + w; j0 <= P; j0 += CB * NW) {
@@ -628,7 +631,7 @@ __device__ __forceinline__ void leaf_wsum_cols(const ModelConst& mc, const StepI
 // Then the level-1 fold (grp.gsize > 1).  All threads call it; returns level1_fold's verdict (false without one).
 // TF: the thread form (2 / 4 leaves per block: records assembled in LDS); the four-lane kernels pass false and carry
 // none of that LDS, nor (CEM: no in-launch fold) the fold's stage -- static LDS a fused launch's draw blocks share.
-template <bool CEMT, bool ZS = false, bool TF = false, bool RG = false>
+template <bool CEMT, bool ZS = false, bool TF = false, int RG = 0>
 __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepInput* __restrict__ in, const int SPB,
                                                int sib, bool valid, float cost, const float* __restrict__ noise,
                                                float* __restrict__ recs, int rec_stride, float tag,
@@ -681,7 +684,7 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
             if (SPB == 128)
                 leaf_wsum_lanes<2, RG>(mc, in, noise + k0, zs, e_sh, rbuf, rec_stride, k0);
             else
-                leaf_wsum_lanes<4, RG>(mc, in, noise + k0, zs, e_sh, rbuf, rec_stride, k0);
+                leaf_wsum_lanes<4, RG>(mc, in, noise + k0, zs, e_sh, rbuf, rec_stride, k0, grp.gen);
         }
     }
     SRBD_RSTAMP(4);

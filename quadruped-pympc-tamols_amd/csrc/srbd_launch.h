@@ -54,8 +54,16 @@ struct GroupArgs {
     // fast_tail's outputs as tagged words (host-mapped, P + 40 of them: best[P] | grf 12 | pred 24 | best_cost,
     // best_index, best_freq, status, each (seq << 32 | bits)) instead of StepOutput + flag (tagged_outputs)
     uint64_t* outt = nullptr;
+    // the step's draws made inside the rollout launch (gen_ok: thread form, zero-order H 12, MPPI, device Philox
+    // stream): the horizon generates each step's values and stores the quads the epilogue does not regenerate; no
+    // RNG launch
+    int gen = 0;  // 0 off, else 1 + the quads the epilogue regenerates (the horizon stores the others)
 };
+// C5 host p50 (us) at 0 / 4 / 6 / 8 / 10 / 12 / 16 / 24 / 36 regenerated quads: 167.9 / 156.5 / 150.9 / 150.9 /
+// 149.4 / 152.6 / 153.7 / 156.5 / 164.7 (the RNG launch + read: 188.0)
+constexpr int GEN_REGEN_QUADS = 8;
 constexpr int TAGGED_OUT_EXTRA = 40;
+bool gen_ok(const ModelConst& mc, int mode);
 // words of the gtag buffer: header words [64][4] (a lane per node), then column words [64][P + 1] -- 64 node slots,
 // so every address fast_tail's unconditional loads form (nodes < TREE_FAN, columns < 256) lies in the allocation
 #define FT_GTAG_WORDS(P) (256 + 64 * ((P) + 1) + 256)

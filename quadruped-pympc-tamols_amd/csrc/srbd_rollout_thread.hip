@@ -13,8 +13,13 @@ namespace srbd {
 // is compiled for at least four waves per SIMD (a fifth measured slower: DESIGN.md section 4).
 // KS: the host step's input by value (the first kernel argument, read in place from the kernarg segment; block
 // 0 writes the device StepInput `in_dev`), as rollout_quad_kernel does.
-template <int KIND, int HT, int ST, bool CEMT, bool EXT, bool KS = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == SRBD_ZERO_ORDER ? 4 : 1))) rollout_kernel(
+// GEN (GroupArgs::gen, zero-order H 12, MPPI, device Philox draws): the launch makes the step's draws itself --
+// every fourth step the twelve column quads of the next four steps (rng_item's Philox call and Box-Muller pairs,
+// so the same bits); the epilogue regenerates the first gen - 1 quads (leaf_wsum_lanes, RG = 2) and reads the
+// rest back, which the horizon stores as it makes them -- in place of the RNG launch's write of N P floats and
+// the horizon's reads of them.
+template <int KIND, int HT, int ST, bool CEMT, bool EXT, bool KS = false, bool GEN = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND == SRBD_ZERO_ORDER ? (GEN ? 3 : 4) : 1))) rollout_kernel(
                                                       const std::conditional_t<KS, StepInputK, KsNone> ksi,
                                                       const ModelConst mc, const StepInput* __restrict__ in_dev,
                                                       const float* __restrict__ noise, float* __restrict__ costs,
@@ -65,7 +70,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
     // across the whole horizon.  (Hoisted, the 144 loads took 210 VGPRs plus SGPR spills to VGPR lanes:
     // 2 waves per SIMD and ~300 v_readlane per step at C5.)  P * ldn * 4 < 2^31: P <= 192 here and
     // n_local <= 8192 blocks x 256.
-    constexpr bool ZR = CT && KIND == SRBD_ZERO_ORDER && !EXT;
+    static_assert(!GEN || (KIND == SRBD_ZERO_ORDER && HT % 4 == 0 && !CEMT && !EXT), "GEN: zero-order H % 4 == 0");
+    constexpr bool ZR = CT && KIND == SRBD_ZERO_ORDER && !EXT && !GEN;
     constexpr int ZD = 2, ZRS = ZD + 1;
     float zr[ZR ? ZRS : 1][12];
     const auto nrs = __builtin_amdgcn_make_buffer_rsrc((void*)noise, (short)0, ZR ? mc.P * mc.ldn * 4 : 0, 0x00020000);
@@ -88,10 +94,44 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
         for (int m = 0; m < ZD && m < HT; ++m) zload(m, ldn4);
     }
     float dep = x[0];  // step_ptr dependency: set part-way through each step
+    // GEN: column quad l PL / 4 + q HT / 4 + s of this row holds steps 4 s .. 4 s + 3 of leg l's component q.  The
+    // epilogue regenerates quads [0, nrg) and reads the others back, which the horizon stores (GroupArgs::gen - 1)
+    float gz[GEN ? 12 : 1][4];
+    const int nrg = GEN ? grp.gen - 1 : 0;
+    // The twelve quads one after another: each quad's row word waits for the previous quad's last value (an empty
+    // asm), so the compiler does not interleave twelve Philox calls.
+    auto gen4 = [&](const int s, auto is) __attribute__((always_inline)) {
+        const int r = mc.row0 + k;
+        const bool live = r > 0 && valid;  // row 0 (the warm start) and the padding rows: zeros, as in the buffer
+        uint32_t d = (uint32_t)(r - 1);
+#pragma unroll
+        for (int l = 0; l < 4; ++l)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                uint32_t c[4] = {d, (uint32_t)(l * (PL / 4) + q * (HT / 4) + s), is->ctr_lo, is->ctr_hi};
+                philox4x32_10(c, is->seed_lo, is->seed_hi);
+                float v[4];
+                box_muller(c[0], c[1], v[0], v[1]);
+                box_muller(c[2], c[3], v[2], v[3]);
+                const int qq = l * (PL / 4) + q * (HT / 4) + s;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) gz[3 * l + q][i] = live ? mc.sigma_mppi * v[i] : 0.0f;
+                if (qq >= nrg) {  // a quad the epilogue reads back: stored (plain stores, kept in the XCD's L2)
+                    float* o = const_cast<float*>(noise) + (size_t)(4 * qq) * ldn + k;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) o[(size_t)i * ldn] = gz[3 * l + q][i];
+                }
+                asm volatile("" : "+v"(d) : "v"(gz[3 * l + q][3]));
+            }
+    };
     auto step = [&](const int n, auto EX) __attribute__((always_inline)) {
         const auto is = step_ptr(in, dep);
         if constexpr (ZR)
             if (n + ZD < HT) zload(n + ZD, step_int(mc.ldn * 4, dep));  // n: a compile-time constant (unrolled)
+        // the key read through a pointer tied to the last step's cost (its roll and angular-rate terms: the whole
+        // rotation update; tied to the forces or to a position, all 36 quads were made before the first step)
+        if constexpr (GEN)
+            if (n % 4 == 0) gen4(n / 4, step_ptr(in, cost3[0]));
         const float c[4] = {is->contact[0][n], is->contact[1][n], is->contact[2][n], is->contact[3][n]};
         const float fref = is->fzref[n];
         const float dt = mc.dts[n];
@@ -102,7 +142,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
             const int base = leg * PL;
             auto acc = [&](int j) {
                 float z;
-                if constexpr (ZR)
+                if constexpr (GEN)
+                    z = gz[3 * leg + (j - n) / HT][n % 4];
+                else if constexpr (ZR)
                     z = zr[n % ZRS][3 * leg + (j - n) / HT];  // ZO reads j = n + q H (decode_leg)
                 else
                     z = (step_gptr(noise, dep) + k)[(size_t)(base + j) * ldn];
@@ -154,8 +196,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KIND =
     return;
 #endif
     // RG: zero-order MPPI regenerates part of its draws in the epilogue (leaf_wsum_lanes, REGEN_QUADS)
-    block_epilogue<CEMT, false, true, KIND == SRBD_ZERO_ORDER && !CEMT && !EXT>(mc, in, T, tid, valid, cost, noise,
-                                                                               recs, rec_stride, 0.0f, grp, nroll);
+    block_epilogue<CEMT, false, true, GEN ? 2 : (KIND == SRBD_ZERO_ORDER && !CEMT && !EXT ? 1 : 0)>(
+        mc, in, T, tid, valid, cost, noise, recs, rec_stride, 0.0f, grp, nroll);
 }
 
 template <int KIND>
@@ -267,6 +309,16 @@ static void launch_thread_t(const ModelConst& mc, const StepInput* in, const flo
     const dim3 grid(blocks + extra * (256 / threads));
     // thread form with the cost terms: runtime shapes only (the four-lane kernel is the default)
     constexpr int HTT = EXT ? 0 : HT, STT = EXT ? 0 : ST;
+    if constexpr (KIND == SRBD_ZERO_ORDER && HT == 12 && !EXT) {
+        // gen_ok: the launch makes the step's draws (host steps, the input by value; no next-step draws).  Only the
+        // by-value form: with the input in global memory the same code spilled 368 B per lane.
+        if (grp.gen && grp.ksi) {
+            hipLaunchKernelGGL((rollout_kernel<KIND, HT, ST, false, false, true, true>), dim3(blocks), dim3(threads), 0,
+                               s, *static_cast<const StepInputK*>(grp.ksi), mc, in, noise, costs, recs, rec_stride,
+                               job, blocks, grp);
+            return;
+        }
+    }
     if constexpr (KIND == SRBD_ZERO_ORDER && (HT == 10 || HT == 12) && !EXT) {
         if (grp.ksi && mc.method != SRBD_CEM_MPPI) {  // ks_ok: the step input as the first kernel argument
             hipLaunchKernelGGL((rollout_kernel<KIND, HT, ST, false, false, true>), grid, dim3(threads), 0, s,
@@ -281,6 +333,13 @@ static void launch_thread_t(const ModelConst& mc, const StepInput* in, const flo
     else
         hipLaunchKernelGGL((rollout_kernel<KIND, HTT, STT, false, EXT>), grid, dim3(threads), 0, s, KsNone{}, mc, in,
                            noise, costs, recs, rec_stride, job, blocks, grp);
+}
+
+// The launch can make the step's draws itself (GroupArgs::gen); the caller also needs device draws (no injected
+// noise) and no next-step draws in the launch.
+bool gen_ok(const ModelConst& mc, int mode) {
+    return mode == ROLLOUT_THREAD && mc.kind == SRBD_ZERO_ORDER && mc.H == 12 && mc.method == SRBD_MPPI &&
+           mc.rng == RNG_PHILOX && !mc.ga && !mc.cost_on && mc.P % 4 == 0;
 }
 
 void launch_rollout_thread(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,

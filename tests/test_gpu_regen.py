@@ -44,3 +44,37 @@ def test_regenerated_draws_equal_read_draws(lib, wkey, N, H):
     np.testing.assert_array_equal(b_dev, b_inj)
     np.testing.assert_array_equal(np.array(r_dev.grf, f32), np.array(r_inj.grf, f32))
     np.testing.assert_array_equal(np.array(r_dev.predicted_state, f32), np.array(r_inj.predicted_state, f32))
+
+
+@pytest.mark.parametrize("wkey,N,rg", [("c5", 524288, None), ("c2", 300001, None), ("c5", 524288, "0"),
+                                       ("c5", 524288, "36")])
+def test_in_launch_draws_equal_rng_launch(lib, monkeypatch, wkey, N, rg):
+    """Host steps whose rollout launch makes the step's draws itself (gen_now: thread form, zero-order H 12, MPPI,
+    device Philox; the horizon stores the quads the epilogue reads back) against the same steps with the RNG launch
+    writing them first (SRBD_GEN=0; the rollout reads them, the epilogue regenerates REGEN_QUADS of them): bit for
+    bit over three warm-started steps, costs included.  rg: SRBD_GEN_RG, the quads the epilogue regenerates
+    (default GEN_REGEN_QUADS; 0: every quad stored and read back; 36: none stored).  N = 300 001: padding rows
+    past n_local in the last block (zeros in the buffer, zeros generated)."""
+    case = make_case(wkey, N=N, method="mppi", par="zero_order", H=12, seed=N % 83)
+    monkeypatch.setenv("SRBD_GEN", "0")
+    ref = lib.Context(product_cfg(case))
+    monkeypatch.delenv("SRBD_GEN")
+    if rg is not None:
+        monkeypatch.setenv("SRBD_GEN_RG", rg)
+    gen = lib.Context(product_cfg(case))
+    monkeypatch.delenv("SRBD_GEN_RG", raising=False)
+    try:
+        bg, br = case["best"].copy(), case["best"].copy()
+        for k in range(3):
+            a = gen.step(case["state"], case["ref"], case["contact"], bg, seed=77, counter=k, want_costs=True)
+            b = ref.step(case["state"], case["ref"], case["contact"], br, seed=77, counter=k, want_costs=True)
+            np.testing.assert_array_equal(a[3], b[3])
+            assert a[2].best_index == b[2].best_index
+            np.testing.assert_array_equal(a[0], b[0])
+            np.testing.assert_array_equal(np.array(a[2].grf, f32), np.array(b[2].grf, f32))
+            np.testing.assert_array_equal(np.array(a[2].predicted_state, f32), np.array(b[2].predicted_state, f32))
+            bg, br = a[0], b[0]
+        assert gen.time_launch(3, 2)[1] & 32 and not ref.time_launch(3, 2)[1] & 32  # the forms the steps ran
+    finally:
+        gen.close()
+        ref.close()
