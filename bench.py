@@ -170,7 +170,8 @@ def roofline(w, n_local: int, kern: dict, traffic):
     algo = n_local * (4 * P + 4)
     achieved = algo / (us * 1e-6) / 1e9
     tags = [t for b, t in ((2, "step input by value (KS)"), (4, "in-launch final merge (FM)"),
-                           (1, "+ next-step draw blocks")) if form & b]
+                           (1, "+ next-step draw blocks"), (16, "one-count fast tail"),
+                           (32, "the step's draws made in the launch, no RNG launch")) if form & b]
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "kernel": ("rollout_kernel" if form & 8 else "rollout_quad_kernel") + " as srbd_step launches it"
