@@ -168,14 +168,14 @@ constexpr Log1pEnt LOG1P_TAB[128] = {
     {0.5078125, 0.6776429940239801}, {0.50390625, 0.6853650401178903}, {0.50390625, 0.6853650401178903}, {0.5, 0.6931471805599453},
 };
 
-// The float64 evaluation: |t| < 2^-7 the Taylor polynomial to t^7 / 7 (truncation < 2^-59 relative; t is exact in
-// float64); else y = 1 + t (exact) = 2^e m, m in [1, 2), k = m's top 7 fraction bits, r = m c_k - 1 (one rounding:
-// the product has <= 62 bits), log y = e ln2 + (-log c_k) + log1p(r) (polynomial to r^7 / 7).  Error < 2^-44
-// relative (|log y| >= 2^-7 on this branch, so the absolute 2^-51 of the sum stays small).
+// The float64 evaluation: |t| < 2^-7 the Taylor polynomial to t^6 / 6 (truncation < t^6 / 7 <= 2^-44.8 relative; t
+// is exact in float64); else y = 1 + t (exact) = 2^e m, m in [1, 2), k = m's top 7 fraction bits, r = m c_k - 1 (one
+// rounding: the product has <= 62 bits), log y = e ln2 + (-log c_k) + log1p(r) (polynomial to r^6 / 6: truncation
+// < 2^-54.6 absolute).  Error < 2^-44 relative (|log y| >= 2^-7 on this branch, so the absolute 2^-51 of the sum
+// stays small).
 SRBD_HD double log1p_poly(double t) {
-    constexpr double C7 = 1.0 / 7, C6 = -1.0 / 6, C5 = 1.0 / 5, C4 = -1.0 / 4, C3 = 1.0 / 3, C2 = -1.0 / 2;
-    double p = fma(t, C7, C6);
-    p = fma(p, t, C5);
+    constexpr double C6 = -1.0 / 6, C5 = 1.0 / 5, C4 = -1.0 / 4, C3 = 1.0 / 3, C2 = -1.0 / 2;
+    double p = fma(t, C6, C5);
     p = fma(p, t, C4);
     p = fma(p, t, C3);
     p = fma(p, t, C2);
@@ -199,10 +199,11 @@ SRBD_HD double log1p_tab(float t) {
     return (ed * LN2_HI + nl) + (log1p_poly(r) + ed * LN2_LO);
 }
 // log1p_cr(t) for t in (-1, 0] -- jax_erf_inv's argument -x^2 -- at a fraction of float64 log1p's cost, the same
-// float: log1p_tab's value is rounded to float when it lies farther than 2^-40 relative (16 times its error bound)
-// from both rounding boundaries of the result (Ziv's test), so the float64 log1p rounds the same way; else (about one
-// draw in 2^15) the float64 log1p itself is evaluated.  |t| < 2^-29: log1p(t) lies within 2^-30 relative of t, so it
-// rounds to t.
+// float: log1p_tab's value L is rounded to float when it lies farther than 2^13 of its own ulps (>= 2^-40 |L|, 16
+// times its error bound) from the rounding midpoint (Ziv's test, on L's bits: float rounding drops the low 29 of the
+// 52 fraction bits, and the midpoint is 2^28 there -- L is a normal float's neighbour, |L| in [2^-30, 17)), so the
+// float64 log1p rounds the same way; else (about one draw in 2^15) the float64 log1p itself is evaluated.
+// |t| < 2^-29: log1p(t) lies within 2^-30 relative of t, so it rounds to t.
 // log1p_try: the float, or false where the float64 log1p must decide (srbd_selftest_log1p counts those).
 SRBD_HD bool log1p_try(float t, float* out) {
     bool ok = t > -1.0f && t <= 0.0f;
@@ -210,13 +211,11 @@ SRBD_HD bool log1p_try(float t, float* out) {
     if (ok && t <= -1.862645149230957e-09f) {  // 2^-29
         const double L = log1p_tab(t);
         f = (float)L;
-        union { float f; uint32_t u; } a, lo, hi;
-        a.f = f;  // f < 0: the next float toward zero has the bit pattern - 1, away from zero + 1
-        lo.u = a.u + 1u;
-        hi.u = a.u - 1u;
-        const double d_lo = 0.5 * ((double)f + (double)lo.f), d_hi = 0.5 * ((double)f + (double)hi.f);  // boundaries
-        const double tol = -L * 9.094947017729282e-13;  // 2^-40 |L|
-        ok = L - d_lo > tol && d_hi - L > tol;
+        union { double d; uint64_t u; } b;
+        b.d = L;
+        const uint32_t r = (uint32_t)b.u & 0x1FFFFFFFu;
+        const uint32_t dist = r > 0x10000000u ? r - 0x10000000u : 0x10000000u - r;
+        ok = dist > 0x2000u;
     }
     *out = f;
     return ok;

@@ -228,7 +228,7 @@ def _log1p_sample():
 
 def test_log1p_fast_equals_float64_log1p():
     """log1p_fast (the JAX normal's erf_inv argument, srbd_jaxrng.h): a short float64 evaluation rounded to float
-    unless it lies within 2^-40 relative of a rounding boundary, else the float64 log1p itself -- the same float32 as
+    unless it lies within 2^13 of its ulps (>= 2^-40 relative) of the rounding midpoint, else the float64 log1p -- the same float32 as
     float32(log1p(float64 t)) for every t in (-1, 0] sampled, with fallbacks rare (about 2^-15 of uniform draws)."""
     from quadruped_pympc_amd import _lib
 
