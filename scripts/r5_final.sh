@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-5 final evidence (GPU box): the full -m gpu suite, rocprofv3 kernel stats + PMC (FETCH / WRITE) + SQ for C2,
+# north-star and C3 (scripts/evidence_pass.sh; C5 in r5g), the per-rank C5 shape through the sharded step at world
+# 1, the default bench line.  Each step under its own limit; stops at the first failure.
+R=${GRAFT_REPO_ROOT:-/root/repo}; cd "$R" || exit 1
+O=$R/gpurun_out; T=${1:-r5z}; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -o addopts="" --timeout 240 --timeout-method thread -rf > $O/gpu_tests_$T.log 2>&1
+rc=$?; tail -3 $O/gpu_tests_$T.log; [ $rc -eq 0 ] || exit 3
+bash scripts/evidence_pass.sh $T c2 ns c3 || exit 4
+timeout -k 10 300 python bench.py --sharded --config c5 --num-samples 65536 --steps 1000 --no-cpu-baseline > $O/sharded_w1_c5rank_$T.json 2> $O/sharded_w1_c5rank_$T.err || { echo sharded failed; tail -5 $O/sharded_w1_c5rank_$T.err; exit 5; }
+tail -c 600 $O/sharded_w1_c5rank_$T.json; echo
+timeout -k 10 600 python bench.py > $O/bench_$T.json 2> $O/bench_$T.err || { echo bench failed; tail -5 $O/bench_$T.err; exit 6; }
+echo ALLDONE
