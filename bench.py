@@ -548,7 +548,14 @@ def bench_multi(_lib, w, args, rank, world, local_rank, scaling, steps=None, dev
     transport = mpc.transport
     mpc.close()
     return dict(n_total=n_total, n_local=n_local, wall=wall, lat=lat, kern=kern, dev=dev, transport=transport,
-                steps=steps)
+                steps=steps, world=world)
+
+
+def rows_per_rank(n_total: int, world: int):
+    """Every rank's row count under the fixed reduction tree's partition (srbd_shard_rows; ADVICE r4: balance)."""
+    from quadruped_pympc_amd import _lib
+
+    return [_lib.shard_rows(n_total, r, world)[1] for r in range(world)]
 
 
 def multi_line(w, out, scaling):
@@ -558,6 +565,7 @@ def multi_line(w, out, scaling):
     lat = np.array(out["lat"]) * 1e3
     return {"value": round(out["n_total"] * out["steps"] / out["wall"], 1), "unit": "rollouts/s",
             "scaling": scaling, "num_samples": out["n_total"], "rows_per_gpu": out["n_local"],
+            "rows_per_rank": rows_per_rank(out["n_total"], out.get("world", 1)),
             "ms_per_step": round(1e3 * out["wall"] / out["steps"], 5), "steps": out["steps"],
             "p50_step_ms": round(float(np.percentile(lat, 50)), 4), "transport": out["transport"],
             "kernels_us": {k: round(v, 3) for k, v in out["kern"].items()}}
@@ -631,6 +639,7 @@ def main(argv=None):
                 + ("Philox noise" if args.rng == "philox" else "jax.random (threefry) noise") + ")",
         "rng": args.rng,
         "config": {"workload": w.name, "num_samples": out["n_total"], "rows_per_gpu": out["n_local"],
+                   "rows_per_rank": rows_per_rank(out["n_total"], world),
                    "horizon": w.horizon, "method": w.method, "parametrization": w.parametrization,
                    "robot": w.robot, "gait": w.gait,
                    "parallelism": (f"rows sharded over {world} GPUs ({scaling} scaling), record exchange: "

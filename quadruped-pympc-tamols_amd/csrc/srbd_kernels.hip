@@ -221,7 +221,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     constexpr bool ZST = CT && KIND == SRBD_ZERO_ORDER && !EXT && HT <= 12;
     constexpr int PCT = ZST ? 12 * HT : 1;
     constexpr int ZSTR = PCT + 1;  // sample stride of the stage: odd, so the epilogue's row-per-lane reads hit 64 banks
-    __shared__ float zst[ZST ? (64 * ZSTR > GROUP_LDS_FLOATS ? 64 * ZSTR : GROUP_LDS_FLOATS) : 1];
+    __shared__ __attribute__((aligned(16))) float zst[ZST ? (64 * ZSTR > GROUP_LDS_FLOATS ? 64 * ZSTR : GROUP_LDS_FLOATS) : 1];
     __shared__ float bls[ZST ? PCT : 1];
     __shared__ float sls[ZST && CEMT ? PCT : 1];
     const int tid = threadIdx.x;
@@ -1612,7 +1612,7 @@ __device__ void final_merge(const ModelConst& mc, const StepInput* in, const flo
     if (threadIdx.x == 0) __hip_atomic_store(grp.gdone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     MergeShared<NT>& sh = *reinterpret_cast<MergeShared<NT>*>(lds);
     float* smem = lds + (sizeof(MergeShared<NT>) + 15) / 16 * 4;  // 16-byte aligned
-    stage_recs<10>(grp.grecs, smem, grp.ngroups * rec_stride);  // sc1 loads (other CUs wrote the records)
+    stage_recs16<5>(grp.grecs, smem, grp.ngroups * rec_stride);  // sc1 loads (other CUs wrote the records)
     __syncthreads();
 #ifdef SRBD_ROLLOUT_STAMPS
     if (threadIdx.x == 0) g_fstamp[4] = __builtin_amdgcn_s_memrealtime();
@@ -1785,7 +1785,7 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
         __hip_atomic_store(grp.cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
         gd = __hip_atomic_fetch_add(grp.gdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    stage_recs<10>(recs + (size_t)g * TREE_FAN * rec_stride, st, nb * rec_stride);  // sc1 loads (other CUs' records)
+    stage_recs16<5>(recs + (size_t)g * TREE_FAN * rec_stride, st, nb * rec_stride);  // sc1 loads (other CUs' records)
     if (tid == 0) fin_sh = gd == (uint32_t)(ng - 1);
     __syncthreads();
     SRBD_LSTAMP(3);
