@@ -678,7 +678,13 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
     const uint64_t key = (sib >= 0 && valid) ? cost_key(cost, (uint32_t)(mc.row0 + k0 + sib)) : KEY_NONE;
     if (sib >= 0) ks[sib] = key;
     __syncthreads();
-    if (w < lpb) {
+    // one leaf per block (the four-lane zero-order MPPI / random-sampling blocks): every wave forms the leaf minimum
+    // itself (the same keys, the same value), so the exponentials need no second barrier
+    constexpr bool ONE = ZS && !CEMT;
+    uint64_t m1 = KEY_NONE;
+    if constexpr (ONE) {
+        m1 = wave_min_u64(ks[lane]);
+    } else if (w < lpb) {
         const uint64_t m = wave_min_u64(ks[64 * w + lane]);
         if (lane == 0) lmin[w] = m;
     }
@@ -696,10 +702,11 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
             if (part == 0 && cnt < K) lel[b][cnt] = mine;
         }
     }
-    __syncthreads();
+    if constexpr (!ONE) __syncthreads();
     SRBD_RSTAMP(3);
     if (!rs) {
-        if (sib >= 0) e_sh[sib] = valid ? expf(-1.0f * (cost - u2f((uint32_t)(lmin[sib >> 6] >> 32)))) : 0.0f;
+        const uint64_t lm = ONE ? m1 : (sib >= 0 ? lmin[sib >> 6] : KEY_NONE);
+        if (sib >= 0) e_sh[sib] = valid ? expf(-1.0f * (cost - u2f((uint32_t)(lm >> 32)))) : 0.0f;
         __syncthreads();
         const bool zs = CEMT && zs_scaled(mc, in);
         if (SPB == 64)
@@ -720,16 +727,18 @@ __device__ __forceinline__ bool block_epilogue(const ModelConst& mc, const StepI
         else
             st_rec(&grec[(size_t)b * rec_stride + off], v);
     };
+    // ONE: every thread holds the leaf minimum (m1); random sampling passed no barrier since lmin was written
+    auto leafmin = [&](int b) { return ONE ? m1 : lmin[b]; };
     if (tid < lpb) {  // headers of leaf tid
-        const uint64_t m = lmin[tid];
+        const uint64_t m = leafmin(tid);
         put(tid, 0, u2f((uint32_t)(m >> 32)));
         put(tid, 2, u2f((uint32_t)m));
         if (rs) put(tid, 1, 1.0f);
     }
-    if (sib >= 0 && key == lmin[sib >> 6]) put(sib >> 6, 3, tag);
+    if (sib >= 0 && key == leafmin(sib >> 6)) put(sib >> 6, 3, tag);
     for (int i = tid; i < lpb * K; i += (int)blockDim.x) {  // keys
         const int b = i / K, q = i % K;
-        uint64_t kk = lmin[b];
+        uint64_t kk = leafmin(b);
         if constexpr (CEMT) kk = K > 1 ? lel[b][q] : kk;
         put(b, REC_HDR + P + 2 * q, u2f((uint32_t)kk));
         put(b, REC_HDR + P + 2 * q + 1, u2f((uint32_t)(kk >> 32)));
