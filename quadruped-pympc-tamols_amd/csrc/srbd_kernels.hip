@@ -1847,12 +1847,12 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
 #ifdef SRBD_ROLLOUT_STAMPS
     if (tid == 0) g_fstamp[0] = blockIdx.x + 1;
 #endif
-    // ---- the other nodes' words into registers, two batches of TREE_FAN / 2 nodes (all 32 at once spilled), through a
-    // buffer descriptor (h uniform: an SGPR offset, one VGPR of address per thread), sc1 as an agent-scope atomic load
+    // ---- the other nodes' words into registers, batches of 8 nodes issued while below ng (all 32 at once spilled;
+    // two batches of 16 issued 11 needless loads per thread at C2's 5 nodes), through a buffer descriptor (h uniform: an SGPR offset, one VGPR of address per thread), sc1 as an agent-scope atomic load
     // has it.  Every load unconditional and unmasked (a branch per load, or a select on its result right after it,
     // costs a wait per load); the words a thread does not need are skipped by the poll (`need`) and the sums.  The
     // gtag allocation covers every address formed here; the poll's re-reads are kept apart by an asm memory clobber.
-    constexpr int HB = TREE_FAN / 2;
+    constexpr int HB = TREE_FAN / 4;  // four batches of 8 nodes, only those below ng issued (C2's 5 nodes: one)
     const auto grs = __builtin_amdgcn_make_buffer_rsrc((void*)grp.gtag, (short)0, FT_GTAG_WORDS(P) * 8, 0x00020000);
     auto ldv = [&](int h) -> uint64_t {  // column word j of node h
         const auto v = __builtin_amdgcn_raw_buffer_load_b64(grs, 8 * (256 + j), 8 * h * TWV, 16);
@@ -1863,7 +1863,7 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
         return ((uint64_t)v[1] << 32) | v[0];
     };
     const bool hv = lane < ng && lane != g;
-    uint64_t xa[HB], xb[HB], hw[3];
+    uint64_t xq[4][HB], hw[3];
     auto issue = [&](uint64_t(&x)[HB], int h0) {
 #pragma unroll
         for (int u = 0; u < HB; ++u) x[u] = ldv(h0 + u);
@@ -1871,8 +1871,9 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
     hw[0] = ldh(0);
     hw[1] = ldh(2);
     hw[2] = ldh(3);
-    issue(xa, 0);
-    if (ng > HB) issue(xb, HB);
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        if (ng > b * HB) issue(xq[b], b * HB);
     FT_MARK(2);  // words issued
     int late = 0;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -1912,7 +1913,7 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
         float V = 0.0f;
         auto need = [&](int h) { return h < ng && h != g; };
         auto accum = [&](const uint64_t(&x)[HB], int h0) {
-            float w[HB];  // this batch's scales (registers: a whole row beside both batches spilled)
+            float w[HB];  // this batch's scales (registers: a whole row beside the batches spilled)
 #pragma unroll
             for (int q = 0; q < HB / 4; ++q) {
                 const float4 t = *reinterpret_cast<const float4*>(wnsc + h0 + 4 * q);
@@ -1925,13 +1926,14 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
                 V = h < ng ? V + t : V;
             }
         };
-        poll(xa, HB, [&](int u) { return need(u); }, [&](int u) { return ldv(u); });
-        FT_MARK(6);  // batch A in
-        accum(xa, 0);
-        if (ng > HB) {
-            poll(xb, HB, [&](int u) { return need(HB + u); }, [&](int u) { return ldv(HB + u); });
-            FT_MARK(8);  // batch B in
-            accum(xb, HB);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            if (ng > b * HB) {
+                poll(xq[b], HB, [&](int u) { return need(b * HB + u); }, [&](int u) { return ldv(b * HB + u); });
+                if (b == 0) FT_MARK(6);  // batch A in
+                if (b == 3) FT_MARK(8);  // the last batch in
+                accum(xq[b], b * HB);
+            }
         }
         vsh[j] = V;
     }
