@@ -3,7 +3,7 @@
 # north-star and C3 (scripts/evidence_pass.sh; C5 in r5g), the per-rank C5 shape through the sharded step at world
 # 1, the default bench line.  Each step under its own limit; stops at the first failure.
 R=${GRAFT_REPO_ROOT:-/root/repo}; cd "$R" || exit 1
-O=$R/gpurun_out; T=${1:-r5z}; mkdir -p $O
+O=$R/gpurun_out; T=${1:-r5f}; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -o addopts="" --timeout 240 --timeout-method thread -rf > $O/gpu_tests_$T.log 2>&1
 rc=$?; tail -3 $O/gpu_tests_$T.log; [ $rc -eq 0 ] || exit 3
