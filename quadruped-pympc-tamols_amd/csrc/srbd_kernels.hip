@@ -1770,6 +1770,9 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
 #define FT_MARK(i)
 #endif
     SRBD_LSTAMP(0);
+#ifdef SRBD_TAIL_PRIO
+    __builtin_amdgcn_s_setprio(SRBD_TAIL_PRIO);  // the tail's waves ahead of the draw blocks' in VALU arbitration
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's leaf record stores have completed
     __syncthreads();
     SRBD_LSTAMP(1);
@@ -1848,7 +1851,8 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
     if (tid == 0) g_fstamp[0] = blockIdx.x + 1;
 #endif
     // ---- the other nodes' words into registers, batches of 8 nodes issued while below ng (all 32 at once spilled;
-    // two batches of 16 issued 11 needless loads per thread at C2's 5 nodes), through a buffer descriptor (h uniform: an SGPR offset, one VGPR of address per thread), sc1 as an agent-scope atomic load
+    // two batches of 16 issued 11 needless loads per thread at C2's 5 nodes), through a buffer descriptor (h
+    // uniform: an SGPR offset, one VGPR of address per thread), sc1 as an agent-scope atomic load
     // has it.  Every load unconditional and unmasked (a branch per load, or a select on its result right after it,
     // costs a wait per load); the words a thread does not need are skipped by the poll (`need`) and the sums.  The
     // gtag allocation covers every address formed here; the poll's re-reads are kept apart by an asm memory clobber.
