@@ -1770,9 +1770,6 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
 #define FT_MARK(i)
 #endif
     SRBD_LSTAMP(0);
-#ifdef SRBD_TAIL_PRIO
-    __builtin_amdgcn_s_setprio(SRBD_TAIL_PRIO);  // the tail's waves ahead of the draw blocks' in VALU arbitration
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's leaf record stores have completed
     __syncthreads();
     SRBD_LSTAMP(1);
