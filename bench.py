@@ -224,6 +224,9 @@ def supplementary(_lib, key: str, steps: int, rng: str = "philox"):
             "device_chain": {"value": round(w.num_samples * steps / (ms * 1e-3), 1),
                              "ms_per_step": round(ms / steps, 5), "steps": steps},
             "kernels_us": {k: round(v, 3) for k, v in kern.items()},
+            # form bit 32: the step's draws are made inside its rollout launch (rng_us times the RNG launch the step
+            # no longer issues)
+            "step_draws": "in the rollout launch" if int(kern.get("step_rollout_form", 0)) & 32 else "RNG launch or fused",
             "roofline": roofline(w, w.num_samples, kern, pmc_traffic(w.name))}
 
 
