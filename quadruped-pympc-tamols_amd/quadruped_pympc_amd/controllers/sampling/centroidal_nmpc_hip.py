@@ -33,6 +33,7 @@ caller) is returned as a lazy array that copies from the device on first access.
 from __future__ import annotations
 
 import copy
+import ctypes as C
 import sys
 import warnings
 
@@ -70,6 +71,21 @@ class LazyCosts:
     @property
     def shape(self):
         return (self._ctx.n_local,)
+
+
+class _PrepBufs:
+    """srbd_prepare_state staging: state_in | ref_in | cur | prev (f64), best (f32), state | ref out (f64)."""
+
+    def __init__(self, num_params: int):
+        self.f64 = np.zeros(24 + 24 + 4 + 4, np.float64)
+        self.state_in, self.ref_in = self.f64[0:24], self.f64[24:48]
+        self.cur, self.prev = self.f64[48:52], self.f64[52:56]
+        self.best = np.zeros(num_params, f32)
+        self.out = np.zeros((2, 24), np.float64)
+        a, o = self.f64.ctypes.data, self.out.ctypes.data
+        self.addr = tuple(C.cast(a + 8 * k, _lib._DP) for k in (0, 24, 48, 52))
+        self.a_best = self.best.ctypes.data_as(_lib._FP)
+        self.addr_out = (C.cast(o, _lib._DP), C.cast(o + 24 * 8, _lib._DP))
 
 
 class Sampling_MPC:
@@ -294,24 +310,30 @@ class Sampling_MPC:
         if self._cfg.mpc_params["shift_solution"]:
             self.best_control_parameters = self.shift_solution(self.best_control_parameters, 1.0 / mpc_frequency)
         legs = ("FL", "FR", "RL", "RR")
-        state_in = np.concatenate(
-            (state_current["position"], state_current["linear_velocity"], state_current["orientation"],
-             state_current["angular_velocity"]) + tuple(state_current["foot_" + n] for n in legs),
-            dtype=np.float64).reshape((24,))
-        ref_in = np.concatenate(
-            (reference_state["ref_position"], reference_state["ref_linear_velocity"],
-             reference_state["ref_orientation"], reference_state["ref_angular_velocity"])
-            + tuple(reference_state["ref_foot_" + n].reshape((3,)) for n in legs), dtype=np.float64).reshape((24,))
+        ps = self._prep_bufs()
+        np.concatenate((state_current["position"], state_current["linear_velocity"], state_current["orientation"],
+                        state_current["angular_velocity"]) + tuple(state_current["foot_" + n] for n in legs),
+                       out=ps.state_in)
+        np.concatenate((reference_state["ref_position"], reference_state["ref_linear_velocity"],
+                        reference_state["ref_orientation"], reference_state["ref_angular_velocity"])
+                       + tuple(reference_state["ref_foot_" + n].reshape((3,)) for n in legs), out=ps.ref_in)
         # swing-foot substitution and lift-off zeroing in the C++ host producer (include/srbd_host.h)
-        self.best_control_parameters = np.array(self.best_control_parameters, dtype=f32)
-        cur = np.ascontiguousarray(current_contact, dtype=np.float64)
-        prev = np.ascontiguousarray(previous_contact, dtype=np.float64)
-        state, ref = np.empty(24), np.empty(24)
-        _lib.check(_lib.lib.srbd_prepare_state(_lib.dptr(state_in), _lib.dptr(ref_in), _lib.dptr(cur),
-                                               _lib.dptr(prev), self.num_control_parameters_single_leg,
-                                               _lib.fptr(self.best_control_parameters), _lib.dptr(state),
-                                               _lib.dptr(ref)), what="srbd_prepare_state")
+        ps.cur[...] = np.reshape(current_contact, 4)
+        ps.prev[...] = np.reshape(previous_contact, 4)
+        ps.best[...] = np.reshape(self.best_control_parameters, ps.best.shape)
+        _lib.check(_lib.lib.srbd_prepare_state(*ps.addr, self.num_control_parameters_single_leg, ps.a_best,
+                                               *ps.addr_out), what="srbd_prepare_state")
+        self.best_control_parameters = ps.best.copy()
+        state, ref = ps.out[0].copy(), ps.out[1].copy()
         return state, ref
+
+    def _prep_bufs(self):
+        """Persistent staging of srbd_prepare_state's arguments, addresses taken once (the call is on the
+        per-MPC-step path; a ctypes pointer conversion costs about as much as the C call)."""
+        ps = getattr(self, "_ps", None)
+        if ps is None:
+            ps = self._ps = _PrepBufs(self.num_control_parameters)
+        return ps
 
     def reset(self):
         print("Resetting the controller")

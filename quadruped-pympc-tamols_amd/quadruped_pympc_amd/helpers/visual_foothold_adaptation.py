@@ -19,6 +19,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+import copy
+
 import numpy as np
 
 from .. import _lib
@@ -203,6 +205,16 @@ class VisualFootholdAdaptation:
             self.tamols_params = cfg.simulation_params.get("tamols_params", {})
             self.robot_name = cfg.robot
         self.last_scores = None
+        self._params_src = self._params_struct = self._params_robot = None
+
+    def _params(self):
+        """tamols_params_struct of the current tamols_params, rebuilt only when they changed (a dict compare instead
+        of 17 attribute stores and a linspace per call)."""
+        if self._params_src is None or self._params_src != self.tamols_params or self._params_robot != self.robot_name:
+            self._params_struct = tamols_params_struct(self.tamols_params, self.robot_name)
+            self._params_src = copy.deepcopy(self.tamols_params)
+            self._params_robot = self.robot_name
+        return self._params_struct
 
     def update_footholds_adaptation(self, update_footholds_adaptation):
         self.footholds_adaptation = update_footholds_adaptation
@@ -249,7 +261,7 @@ class VisualFootholdAdaptation:
             feet = None
             if current_feet_pos is not None and base_position is not None:
                 feet = np.stack([np.asarray(current_feet_pos[n], dtype=np.float64) for n in ("FL", "FR", "RL", "RR")])
-            params = tamols_params_struct(self.tamols_params, self.robot_name)
+            params = self._params()
             fused = _fused_patches(heightmaps, names, seeds)
             if fused is not None:  # GPU maps of one terrain, pending around the seeds: raycast + TAMOLS in one launch
                 ter, yaw, g = fused
