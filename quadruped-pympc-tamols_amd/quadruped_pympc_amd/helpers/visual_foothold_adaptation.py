@@ -169,6 +169,14 @@ class TamolsSearch:
         return self._result(rows, cols, want_heightmaps, want_scores)
 
 
+def _rows(attr, names):
+    """(len(names), 3) float64 copy of the per-leg 3-vectors (one slice store per leg instead of np.stack)."""
+    out = np.empty((len(names), 3))
+    for i, n in enumerate(names):
+        out[i] = attr[n]
+    return out
+
+
 def _fused_patches(heightmaps, names, seeds):
     """(terrain, yaw, first map) when the four maps are GpuHeightMaps of one terrain with one patch geometry, each
     pending a patch around its seed at one yaw (what wb_interface.py:233-234 leaves before compute_adaptation);
@@ -183,7 +191,8 @@ def _fused_patches(heightmaps, names, seeds):
     for m, sd in zip(maps, seeds):
         if (m.terrain, m.num_rows, m.num_cols, m.dist_x, m.dist_y, m.ray_z, m.pending[1]) != geo:
             return None
-        if not np.array_equal(m.pending[0], np.asarray(sd, dtype=np.float64).reshape(-1)[:3]):
+        # bitwise (a -0.0 / 0.0 mismatch only costs the unfused path); ~10x cheaper than np.array_equal
+        if m.pending[0].tobytes() != np.asarray(sd, dtype=np.float64).reshape(-1)[:3].tobytes():
             return None
     return g.terrain, g.pending[1], g
 
@@ -255,12 +264,12 @@ class VisualFootholdAdaptation:
 
         elif self.adaptation_strategy == "tamols":
             names = list(legs_order)
-            seeds = np.stack([np.asarray(reference_footholds[n], dtype=np.float64).copy() for n in names])
-            hips = np.stack([np.asarray(hip_positions[n], dtype=np.float64) for n in names])
+            seeds = _rows(reference_footholds, names)
+            hips = _rows(hip_positions, names)
             contact = None if current_contact is None else np.asarray(current_contact).astype(np.int32)
             feet = None
             if current_feet_pos is not None and base_position is not None:
-                feet = np.stack([np.asarray(current_feet_pos[n], dtype=np.float64) for n in ("FL", "FR", "RL", "RR")])
+                feet = _rows(current_feet_pos, LEGS)
             params = self._params()
             fused = _fused_patches(heightmaps, names, seeds)
             if fused is not None:  # GPU maps of one terrain, pending around the seeds: raycast + TAMOLS in one launch
