@@ -389,6 +389,39 @@ int srbd_tamols_run_terrain(srbd_tamols_ctx* ctx, srbd_terrain* terrain, double 
                             const double* feet, const srbd_tamols_params* params, double* out_footholds,
                             double* out_boxes, int32_t* out_valid, double* out_scores, double* out_seed_heights,
                             double* out_heightmaps);
+/* ------------------------------------------------------------------ one C4 MPC step in one call
+ * The per-MPC-step chain of helpers/foothold_pipeline.py TamolsMpcStep.step (wb_interface.py:230-291 +
+ * srbd_controller_interface.py:113-180, MPPI / random sampling, one sampling iteration) behind one host call:
+ * srbd_tamols_run_terrain on the patches around the seeds -> the adapted footholds (an infeasible leg: the seed at
+ * its terrain height, VFA:223-228) as ref_foot_* after ref_base -> srbd_prepare_state -> srbd_step (device draws).
+ * The same calls in the same order as the Python chain, so the same results bit for bit; the host work between
+ * them is C instead of ~60 us of Python. */
+typedef struct srbd_foothold_io {
+    /* inputs */
+    double state_in[24];        /* position, linear_velocity, orientation, angular_velocity, foot_FL..RR */
+    double ref_base[12];        /* ref_position, ref_linear_velocity, ref_orientation, ref_angular_velocity */
+    double seeds[12], hips[12]; /* reference footholds and hips, legs FL FR RL RR */
+    double forward_vel[3];      /* TAMOLS forward velocity (the base linear velocity) */
+    double current_contact[4], previous_contact[4];
+    double yaw, dist_x, dist_y, ray_z;
+    int32_t rows, cols;
+    /* outputs */
+    double footholds[12];       /* adapted ref_foot_* */
+    double boxes[24];           /* constraint boxes (valid legs) */
+    double seed_heights[4];
+    int32_t valid[4];
+    double state_out[24], ref_out[24]; /* prepare_state_and_reference's outputs */
+    double* scores;             /* 4 x rows*cols, or NULL */
+    double* heightmaps;         /* 4 x rows x cols x 3, or NULL */
+} srbd_foothold_io;
+
+/* best_params (in/out, 4 x params_per_leg floats): the warm start; lift-off legs are zeroed before the step and the
+ * step's result replaces it.  contact: 4 x contact_stride floats (the first `horizon` columns are used). */
+int srbd_foothold_mpc_step(srbd_tamols_ctx* tamols, srbd_terrain* terrain, const srbd_tamols_params* params,
+                           srbd_ctx* ctx, srbd_foothold_io* io, const float* contact, int32_t contact_stride,
+                           float* best_params, int32_t params_per_leg, uint64_t seed, uint64_t counter,
+                           srbd_result* out);
+
 /* Diagnostic: enable != 0 stamps the phases of the following TAMOLS calls; out_us[5] (may be NULL)
  * receives the last call's mean per-block durations of (patch, queries, scores, slice argmin + count)
  * and the span from the first block's start to the last leg's end, in us.  enable == 0 turns it off. */

@@ -142,6 +142,36 @@ extern "C" int srbd_prepare_state(const double state_in[24], const double ref_in
     return SRBD_OK;
 }
 
+// helpers/foothold_pipeline.py TamolsMpcStep.step in one host call (include/srbd_mpc.h).  The base position and
+// the current feet TAMOLS reads are the state's own (state_in[0:3], state_in[12:24]); its contact flags are the
+// current contact truncated to int32 (VFA's astype).
+extern "C" int srbd_foothold_mpc_step(srbd_tamols_ctx* tamols, srbd_terrain* terrain, const srbd_tamols_params* params,
+                                      srbd_ctx* ctx, srbd_foothold_io* io, const float* contact,
+                                      int32_t contact_stride, float* best_params, int32_t params_per_leg,
+                                      uint64_t seed, uint64_t counter, srbd_result* out) {
+    if (!tamols || !terrain || !params || !ctx || !io || !contact || !best_params || !out || params_per_leg < 1)
+        return SRBD_E_INVALID;
+    int32_t cint[4];
+    for (int l = 0; l < 4; ++l) cint[l] = (int32_t)io->current_contact[l];
+    int rc = srbd_tamols_run_terrain(tamols, terrain, io->yaw, io->rows, io->cols, io->dist_x, io->dist_y, io->ray_z,
+                                     io->seeds, io->hips, io->forward_vel, io->state_in, cint, io->state_in + 12,
+                                     params, io->footholds, io->boxes, io->valid, io->scores, io->seed_heights,
+                                     io->heightmaps);
+    if (rc != SRBD_OK) return rc;
+    double ref_in[24];
+    memcpy(ref_in, io->ref_base, sizeof(double) * 12);
+    memcpy(ref_in + 12, io->footholds, sizeof(double) * 12);  // wb_interface.py:268-285
+    rc = srbd_prepare_state(io->state_in, ref_in, io->current_contact, io->previous_contact, params_per_leg,
+                            best_params, io->state_out, io->ref_out);
+    if (rc != SRBD_OK) return rc;
+    float st[24], rf[24];
+    for (int i = 0; i < 24; ++i) {
+        st[i] = (float)io->state_out[i];
+        rf[i] = (float)io->ref_out[i];
+    }
+    return srbd_step(ctx, st, rf, contact, contact_stride, best_params, nullptr, nullptr, seed, counter, out, nullptr);
+}
+
 // ROS:343-358.  The payload words are written with relaxed atomic stores between the odd and even
 // sequence stores, so a reader that sees the same even sequence before and after its copy holds one
 // message (release on the closing store; acquire/fence on the reader side).

@@ -62,6 +62,17 @@ class TamolsParams(C.Structure):
     ]
 
 
+class FootholdIO(C.Structure):
+    """srbd_foothold_io (include/srbd_mpc.h): the C4 step's inputs and outputs."""
+    _fields_ = [
+        ("state_in", _D * 24), ("ref_base", _D * 12), ("seeds", _D * 12), ("hips", _D * 12), ("forward_vel", _D * 3),
+        ("current_contact", _D * 4), ("previous_contact", _D * 4), ("yaw", _D), ("dist_x", _D), ("dist_y", _D),
+        ("ray_z", _D), ("rows", _I), ("cols", _I),
+        ("footholds", _D * 12), ("boxes", _D * 24), ("seed_heights", _D * 4), ("valid", _I * 4),
+        ("state_out", _D * 24), ("ref_out", _D * 24), ("scores", _P), ("heightmaps", _P),
+    ]
+
+
 SIGNATURES = {
     "srbd_num_params": (_I, [C.POINTER(SrbdConfig)]),
     "srbd_device_count": (_I, [_IP]),
@@ -153,6 +164,8 @@ SIGNATURES.update({
     "srbd_terrain_patches": (_I, [_P, _DP, _DP, _I, _I, _I, _D, _D, _D, _DP]),
     "srbd_tamols_run_terrain": (_I, [_P, _P, _D, _I, _I, _D, _D, _D, _P, _P, _P, _P, _P, _P,
                                      C.POINTER(TamolsParams), _P, _P, _P, _P, _P, _P]),
+    "srbd_foothold_mpc_step": (_I, [_P, _P, C.POINTER(TamolsParams), _P, C.POINTER(FootholdIO), _P, _I, _P, _I,
+                                    C.c_uint64, C.c_uint64, C.POINTER(SrbdResult)]),
     "srbd_tamols_phases": (_I, [_P, _I, _FP]),
     "srbd_tamols_phases_raw": (_I, [_P, _P]),
     "srbd_set_rng": (_I, [_P, _I]),

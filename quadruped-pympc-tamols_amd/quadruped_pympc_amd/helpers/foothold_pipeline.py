@@ -18,8 +18,12 @@ call (the per-step cost C4 names).
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 
+from .. import _lib
+from ..controllers.sampling import centroidal_nmpc_hip
 from ..interfaces.srbd_controller_interface import SRBDControllerInterface
 from ..runtime import active_config
 from .legs_attr import LegsAttr
@@ -38,18 +42,129 @@ class TamolsMpcStep:
         self.heightmaps = LegsAttr(*[GpuHeightMap(terrain, num_rows, num_cols, dist_x, dist_y) for _ in LEGS])
         self.vfa = VisualFootholdAdaptation(LEGS, "tamols", cfg)
         self.iface = SRBDControllerInterface(cfg)
-        self.last_ref_state = None
+        self._ref_state = None
+        self._ref_src = None  # (ref_base, footholds (4, 3), constraints) of a fused step, made into a dict on demand
         self.last_constraints = None
+        self.fused = True  # srbd_foothold_mpc_step when the configuration allows (see _fusable)
+        self._io = None
 
     @property
     def controller(self):
         return self.iface.controller
+
+    @property
+    def last_ref_state(self):
+        """The ref_state the last step gave compute_control (wb_interface.py:268-285)."""
+        if self._ref_src is not None:
+            ref_base, fh, constraints = self._ref_src
+            ref_state = dict(ref_base)
+            for i, n in enumerate(LEGS):
+                ref_state["ref_foot_" + n] = fh[i:i + 1]
+                ref_state["ref_foot_constraints_" + n] = constraints[n]
+            self._ref_state, self._ref_src = ref_state, None
+        return self._ref_state
+
+    def _fusable(self):
+        """One host call (srbd_foothold_mpc_step) makes exactly the Python chain's calls when: the plain sampling
+        controller (not the gait-adaptive one), MPPI or random sampling (no sigma), one sampling iteration, no
+        solution shift, TAMOLS adaptation, and the four maps over one terrain with one patch geometry."""
+        ctrl = self.iface.controller
+        if not self.fused or type(ctrl) is not centroidal_nmpc_hip.Sampling_MPC:
+            return False
+        if ctrl.sampling_method == "cem_mppi" or ctrl.num_sampling_iterations != 1:
+            return False
+        if self.cfg.mpc_params["shift_solution"] or self.vfa.adaptation_strategy != "tamols":
+            return False
+        g = self.heightmaps.FL
+        geo = (g.terrain, g.num_rows, g.num_cols, g.dist_x, g.dist_y, g.ray_z)
+        return all(isinstance(m, GpuHeightMap) and (m.terrain, m.num_rows, m.num_cols, m.dist_x, m.dist_y, m.ray_z)
+                   == geo for m in self.heightmaps)
+
+    def _fused_io(self):
+        io = self._io
+        if io is None:
+            g = self.heightmaps.FL
+            io = self._io = _lib.FootholdIO()
+            io.rows, io.cols, io.dist_x, io.dist_y, io.ray_z = g.num_rows, g.num_cols, g.dist_x, g.dist_y, g.ray_z
+            self._io_np = {k: np.ctypeslib.as_array(getattr(io, k)) for k in
+                           ("state_in", "ref_base", "seeds", "hips", "forward_vel", "current_contact",
+                            "previous_contact", "footholds", "boxes", "seed_heights", "valid")}
+            self._io_scores = np.zeros((4, g.num_rows * g.num_cols))
+            self._io_hm = np.zeros((4, g.num_rows, g.num_cols, 3))
+            io.scores, io.heightmaps = self._io_scores.ctypes.data, self._io_hm.ctypes.data
+            self._io_ref = C.byref(io)
+        return io
+
+    def _step_fused(self, state_current, ref_feet_pos, hip_pos, ref_base, contact_sequence, base_lin_vel,
+                    base_ori_euler_xyz):
+        """step() through srbd_foothold_mpc_step; the Python objects it would have updated are updated the same
+        way (the heightmaps' patches, VFA's footholds / constraints / scores, the interface's previous contact,
+        the controller's warm start, key and last result)."""
+        iface, ctrl, vfa = self.iface, self.iface.controller, self.vfa
+        io = self._fused_io()
+        a = self._io_np
+        np.concatenate([state_current[k] for k in ("position", "linear_velocity", "orientation", "angular_velocity",
+                                                   "foot_FL", "foot_FR", "foot_RL", "foot_RR")], out=a["state_in"])
+        np.concatenate([ref_base[k] for k in ("ref_position", "ref_linear_velocity", "ref_orientation",
+                                              "ref_angular_velocity")], out=a["ref_base"])
+        seeds, hips = a["seeds"], a["hips"]
+        seeds[0:3], seeds[3:6], seeds[6:9], seeds[9:12] = ref_feet_pos.FL, ref_feet_pos.FR, ref_feet_pos.RL, \
+            ref_feet_pos.RR
+        hips[0:3], hips[3:6], hips[6:9], hips[9:12] = hip_pos.FL, hip_pos.FR, hip_pos.RL, hip_pos.RR
+        a["forward_vel"][:] = np.asarray(base_lin_vel, dtype=np.float64).reshape(-1)[:3]
+        current_contact = np.array([contact_sequence[0][0], contact_sequence[1][0], contact_sequence[2][0],
+                                    contact_sequence[3][0]])
+        a["current_contact"][:] = current_contact
+        a["previous_contact"][:] = iface.previous_contact_mpc
+        io.yaw = float(base_ori_euler_xyz[2])
+        ctx = ctrl.context
+        H = ctx.cfg.horizon
+        cs = np.asarray(contact_sequence)
+        if cs.ndim != 2 or cs.shape[0] != 4 or cs.shape[1] < H:
+            raise ValueError("contact_sequence must be (4, >=H)")
+        ctx._contact[...] = cs[:, :H]
+        ctx._best[...] = np.reshape(ctrl.best_control_parameters, ctx.P)
+        ctrl = ctrl.with_newkey()
+        seed, counter = ctrl._key_args(ctrl.master_key)
+        res = _lib.SrbdResult()
+        rc = _lib.lib.srbd_foothold_mpc_step(vfa.search.h, self.heightmaps.FL.terrain.h, C.byref(vfa._params()),
+                                             ctx.h, self._io_ref, ctx._a_contact, H, ctx._a_best,
+                                             ctrl.num_control_parameters_single_leg, seed, counter, C.byref(res))
+        if rc != _lib.OK:
+            raise RuntimeError(f"srbd_foothold_mpc_step failed ({rc}): {_lib.last_error(ctx.h)} "
+                               f"{vfa.search.h and _lib.lib.srbd_tamols_last_error(vfa.search.h)}")
+        ctx.step_id += 1
+        # the objects' state, as the Python chain leaves it
+        hm = self._io_hm.copy()
+        for i, m in enumerate(self.heightmaps):
+            m._data, m.pending = hm[i][:, :, None, :], None
+        fh = a["footholds"].reshape(4, 3).copy()
+        boxes, valid = a["boxes"].reshape(4, 2, 3), a["valid"]
+        constraints = vfa.footholds_constraints
+        for i, n in enumerate(LEGS):
+            if valid[i]:
+                constraints[n] = [boxes[i, 0].copy(), boxes[i, 1].copy()]
+        vfa.last_scores = self._io_scores.copy()
+        vfa.update_footholds_adaptation(LegsAttr(fh[0], fh[1], fh[2], fh[3]))
+        self._ref_state, self._ref_src = None, (ref_base, fh, LegsAttr(*constraints))
+        self.last_constraints = constraints
+        iface.previous_contact_mpc = current_contact
+        ctrl.best_control_parameters = ctx._best.copy()
+        ctrl.last_result = res
+        g = np.array(res.grf, dtype=np.float32)
+        grfs = LegsAttr(FL=g[0:3] * current_contact[0], FR=g[3:6] * current_contact[1],
+                        RL=g[6:9] * current_contact[2], RR=g[9:12] * current_contact[3])
+        footholds = LegsAttr(FL=fh[0], FR=fh[1], RL=fh[2], RR=fh[3])
+        return grfs, footholds, None, None, None, 1.4, np.array(res.predicted_state, dtype=np.float32)
 
     def step(self, state_current: dict, ref_feet_pos: LegsAttr, hip_pos: LegsAttr, ref_base: dict,
              contact_sequence: np.ndarray, base_lin_vel: np.ndarray, base_ori_euler_xyz: np.ndarray,
              base_ang_vel: np.ndarray, pgg_phase_signal: np.ndarray, pgg_step_freq: float, optimize_swing: int = 0):
         """ref_base: ``ref_position``, ``ref_linear_velocity``, ``ref_orientation``, ``ref_angular_velocity``.
         Returns ``compute_control``'s 7-tuple; the ref_state it was given is kept in ``last_ref_state``."""
+        if self._fusable():
+            return self._step_fused(state_current, ref_feet_pos, hip_pos, ref_base, contact_sequence, base_lin_vel,
+                                    base_ori_euler_xyz)
         feet = LegsAttr(*[np.asarray(state_current["foot_" + n], dtype=np.float64) for n in LEGS])
         current_contact = np.array([contact_sequence[i][0] for i in range(4)])
         seeds = LegsAttr(*[np.array(ref_feet_pos[n], dtype=np.float64) for n in LEGS])
@@ -64,7 +179,7 @@ class TamolsMpcStep:
         for n in LEGS:
             ref_state["ref_foot_" + n] = np.asarray(adapted[n], dtype=np.float64).reshape((1, 3))
             ref_state["ref_foot_constraints_" + n] = constraints[n]
-        self.last_ref_state = ref_state
+        self._ref_state, self._ref_src = ref_state, None
         self.last_constraints = constraints
         return self.iface.compute_control(state_current, ref_state, contact_sequence, self.cfg.inertia,
                                           pgg_phase_signal, pgg_step_freq, optimize_swing)

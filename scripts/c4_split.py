@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Wall-clock split of the C4 per-MPC-step pipeline on the GPU box (no profiler): the raycast + TAMOLS launch
-(srbd_tamols_run_terrain) and the MPPI step (srbd_step) timed inside the step by wrapping the two C entry points,
+(srbd_tamols_run_terrain) and the MPPI step (srbd_step) -- or the one-call srbd_foothold_mpc_step -- timed inside the
+step by wrapping the C entry points;
 the rest is host Python.  Usage: c4_split.py [steps]"""
 import json
 import os
@@ -35,7 +36,7 @@ class Timed:
         return r
 
 
-for name in ("srbd_tamols_run_terrain", "srbd_step", "srbd_prepare_state"):
+for name in ("srbd_tamols_run_terrain", "srbd_step", "srbd_prepare_state", "srbd_foothold_mpc_step"):
     setattr(_lib.lib, name, Timed(name, getattr(_lib.lib, name)))
 
 ter = GpuTerrain.stepping_stones()

@@ -120,3 +120,67 @@ def test_c4_pipeline_steps(pipe):
         np.testing.assert_allclose(got, fh_o, rtol=0, atol=1e-12)
         np.testing.assert_array_equal(np.stack([out[1][n] for n in LEGS]), got)
         assert np.isfinite(np.concatenate([out[0][n] for n in LEGS] + [out[6]])).all()
+
+
+def test_c4_fused_step_equals_python_chain():
+    """srbd_foothold_mpc_step (TamolsMpcStep's one-call path) against the same pipeline run through the Python
+    chain (fused off), step by step from the same start: every returned array, the ref_state, the constraints, the
+    heightmap patches, the scores, the warm start, the key and the step result bit for bit -- over trot contacts
+    (swing feet, lift-offs) and seeds out of reach (infeasible legs: the seed at its terrain height)."""
+    from quadruped_pympc_amd import _lib
+    from quadruped_pympc_amd.helpers.foothold_pipeline import TamolsMpcStep
+    from quadruped_pympc_amd.helpers.legs_attr import LegsAttr
+    from quadruped_pympc_amd.helpers.terrain import GpuTerrain
+    from quadruped_pympc_amd.synthetic import c4_config, c4_inputs
+
+    if _lib.device_count() < 1:
+        pytest.fail("no HIP device visible")
+    ter = GpuTerrain.stepping_stones()
+    pf, pu = TamolsMpcStep(ter, c4_config()), TamolsMpcStep(ter, c4_config())
+    pu.fused = False
+    assert pf._fusable() and not pu._fusable()
+    invalid_seen = 0
+    try:
+        for k in range(12):
+            state, seeds, hips, ref_base, cs = c4_inputs(k)
+            if k % 4 == 3:
+                seeds = seeds + np.array([1.5, 0.0, 0.0])  # beyond the legs' reach
+            outs = []
+            for p in (pf, pu):
+                outs.append(p.step(state, LegsAttr(*seeds.copy()), LegsAttr(*hips), ref_base, cs.copy(),
+                                   state["linear_velocity"], state["orientation"], state["angular_velocity"],
+                                   np.zeros(4), 1.4))
+            of, ou = outs
+            for i in (0, 1):
+                for n in LEGS:
+                    np.testing.assert_array_equal(of[i][n], ou[i][n])
+                    assert of[i][n].dtype == ou[i][n].dtype
+            assert of[2:6] == ou[2:6]
+            np.testing.assert_array_equal(of[6], ou[6])
+            rf, ru = pf.last_ref_state, pu.last_ref_state
+            assert rf.keys() == ru.keys()
+            for key in ru:
+                if key.startswith("ref_foot_constraints_"):
+                    assert (rf[key] is None) == (ru[key] is None)
+                    if ru[key] is not None:
+                        for a, b in zip(rf[key], ru[key]):
+                            np.testing.assert_array_equal(a, b)
+                else:
+                    np.testing.assert_array_equal(rf[key], ru[key])
+                    assert np.asarray(rf[key]).shape == np.asarray(ru[key]).shape
+            for n in LEGS:
+                np.testing.assert_array_equal(pf.heightmaps[n].data, pu.heightmaps[n].data)
+                np.testing.assert_array_equal(pf.vfa.footholds_adaptation[n], pu.vfa.footholds_adaptation[n])
+            np.testing.assert_array_equal(pf.vfa.last_scores, pu.vfa.last_scores)
+            np.testing.assert_array_equal(pf.controller.best_control_parameters, pu.controller.best_control_parameters)
+            np.testing.assert_array_equal(pf.controller.master_key, pu.controller.master_key)
+            np.testing.assert_array_equal(pf.iface.previous_contact_mpc, pu.iface.previous_contact_mpc)
+            a, b = pf.controller.last_result, pu.controller.last_result
+            assert (a.best_index, a.best_cost, a.status) == (b.best_index, b.best_cost, b.status)
+            invalid_seen += int((pf._io_np["valid"] == 0).sum())  # infeasible legs keep their old constraints
+            assert pf.controller.context.step_id == pu.controller.context.step_id
+    finally:
+        pf.close()
+        pu.close()
+        ter.close()
+    assert invalid_seen > 0
