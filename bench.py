@@ -358,7 +358,8 @@ def c4_pipeline_latency(steps: int):
     """C4 as one per-MPC-step sequence (BASELINE configs[3]; helpers/foothold_pipeline.py): the four heightmap
     patches raycast on the GPU from the device-resident stepping_stones_medium scene and TAMOLS in one launch, the
     adapted footholds into ref_state, SRBDControllerInterface.compute_control (prepare_state_and_reference + the
-    MPPI N = 10 000 H = 12 step on device draws) -- timed around the whole step from Python."""
+    MPPI N = 10 000 H = 12 step on device draws; one host call, srbd_foothold_mpc_step, when the config allows) --
+    timed around the whole step from Python."""
     import numpy as np
 
     from quadruped_pympc_amd.helpers.foothold_pipeline import TamolsMpcStep
@@ -379,15 +380,18 @@ def c4_pipeline_latency(steps: int):
         lat.append(time.perf_counter() - t0)
     assert np.isfinite(out[6]).all()
     valid = sum(pipe.last_constraints[n] is not None for n in ("FL", "FR", "RL", "RR"))
+    fused = pipe._fusable()
     pipe.close()
     ter.close()
     lat = np.array(lat[20:])
     return {"value": round(w.num_samples / float(lat.mean()), 1), "unit": "rollouts/s",
             "p50_ms": round(float(np.percentile(lat, 50)) * 1e3, 4),
             "p99_ms": round(float(np.percentile(lat, 99)) * 1e3, 4), "steps": steps, "valid_legs": int(valid),
-            "workload": w.name, "path": "GpuHeightMap x4 (lazy) -> VisualFootholdAdaptation.compute_adaptation "
-                                        "(srbd_tamols_run_terrain: raycast + TAMOLS, one launch) -> ref_state -> "
-                                        "SRBDControllerInterface.compute_control (srbd_step, MPPI N=10000 H=12)"}
+            "workload": w.name, "fused": bool(fused),
+            "path": "TamolsMpcStep.step: GpuHeightMap x4 (lazy) -> VisualFootholdAdaptation.compute_adaptation "
+                    "(srbd_tamols_run_terrain: raycast + TAMOLS, one launch) -> ref_state -> "
+                    "SRBDControllerInterface.compute_control (srbd_prepare_state, srbd_step MPPI N=10000 H=12); "
+                    "fused: the same calls chained in C by srbd_foothold_mpc_step"}
 
 
 # ---------------------------------------------------------------------------------------------- runs
