@@ -217,7 +217,10 @@ int terrain_enqueue(srbd_terrain* t, const double* centers, const double* yaws, 
 // One TAMOLS call as one launch (tamols_kernel.hip): TAMOLS_BPL blocks per leg, each raycasting (or
 // reading) the leg's patch and scoring its slice of the candidates; the leg's last block merges the
 // slices, the last leg publishes `seq` into `flag`.  Outputs are host-mapped pointers.
-constexpr int TAMOLS_BPL = 16;
+#ifndef SRBD_TAMOLS_BPL
+#define SRBD_TAMOLS_BPL 16  // blocks per leg (a build-time knob for scripts/build_variants.sh sweeps)
+#endif
+constexpr int TAMOLS_BPL = SRBD_TAMOLS_BPL;
 constexpr int TAMOLS_THREADS = 1024;
 constexpr int TAMOLS_LDS_PRIMS = 1024;  // scenes up to this many primitives are staged in LDS (80 KB)
 struct TamolsJob {
