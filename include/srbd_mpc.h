@@ -413,6 +413,9 @@ typedef struct srbd_foothold_io {
     double state_out[24], ref_out[24]; /* prepare_state_and_reference's outputs */
     double* scores;             /* 4 x rows*cols, or NULL */
     double* heightmaps;         /* 4 x rows x cols x 3, or NULL */
+    int32_t stage;              /* out: the calls that completed (0 none, 1 TAMOLS, 2 + prepare_state, 3 + step),
+                                   so a caller can leave its objects as the chain would on an error */
+    int32_t pad;
 } srbd_foothold_io;
 
 /* best_params (in/out, 4 x params_per_leg floats): the warm start; lift-off legs are zeroed before the step and the

@@ -151,6 +151,7 @@ extern "C" int srbd_foothold_mpc_step(srbd_tamols_ctx* tamols, srbd_terrain* ter
                                       uint64_t seed, uint64_t counter, srbd_result* out) {
     if (!tamols || !terrain || !params || !ctx || !io || !contact || !best_params || !out || params_per_leg < 1)
         return SRBD_E_INVALID;
+    io->stage = 0;
     int32_t cint[4];
     for (int l = 0; l < 4; ++l) cint[l] = (int32_t)io->current_contact[l];
     int rc = srbd_tamols_run_terrain(tamols, terrain, io->yaw, io->rows, io->cols, io->dist_x, io->dist_y, io->ray_z,
@@ -158,18 +159,22 @@ extern "C" int srbd_foothold_mpc_step(srbd_tamols_ctx* tamols, srbd_terrain* ter
                                      params, io->footholds, io->boxes, io->valid, io->scores, io->seed_heights,
                                      io->heightmaps);
     if (rc != SRBD_OK) return rc;
+    io->stage = 1;
     double ref_in[24];
     memcpy(ref_in, io->ref_base, sizeof(double) * 12);
     memcpy(ref_in + 12, io->footholds, sizeof(double) * 12);  // wb_interface.py:268-285
     rc = srbd_prepare_state(io->state_in, ref_in, io->current_contact, io->previous_contact, params_per_leg,
                             best_params, io->state_out, io->ref_out);
     if (rc != SRBD_OK) return rc;
+    io->stage = 2;
     float st[24], rf[24];
     for (int i = 0; i < 24; ++i) {
         st[i] = (float)io->state_out[i];
         rf[i] = (float)io->ref_out[i];
     }
-    return srbd_step(ctx, st, rf, contact, contact_stride, best_params, nullptr, nullptr, seed, counter, out, nullptr);
+    rc = srbd_step(ctx, st, rf, contact, contact_stride, best_params, nullptr, nullptr, seed, counter, out, nullptr);
+    if (rc == SRBD_OK) io->stage = 3;
+    return rc;
 }
 
 // ROS:343-358.  The payload words are written with relaxed atomic stores between the odd and even

@@ -69,7 +69,7 @@ class FootholdIO(C.Structure):
         ("current_contact", _D * 4), ("previous_contact", _D * 4), ("yaw", _D), ("dist_x", _D), ("dist_y", _D),
         ("ray_z", _D), ("rows", _I), ("cols", _I),
         ("footholds", _D * 12), ("boxes", _D * 24), ("seed_heights", _D * 4), ("valid", _I * 4),
-        ("state_out", _D * 24), ("ref_out", _D * 24), ("scores", _P), ("heightmaps", _P),
+        ("state_out", _D * 24), ("ref_out", _D * 24), ("scores", _P), ("heightmaps", _P), ("stage", _I), ("pad", _I),
     ]
 
 

@@ -119,37 +119,46 @@ class TamolsMpcStep:
         io.yaw = float(base_ori_euler_xyz[2])
         ctx = ctrl.context
         H = ctx.cfg.horizon
-        cs = np.asarray(contact_sequence)
-        if cs.ndim != 2 or cs.shape[0] != 4 or cs.shape[1] < H:
-            raise ValueError("contact_sequence must be (4, >=H)")
-        ctx._contact[...] = cs[:, :H]
+        ctx._contact[...] = np.asarray(contact_sequence)[:, :H]
         ctx._best[...] = np.reshape(ctrl.best_control_parameters, ctx.P)
+        key0 = (ctrl.master_key, ctrl._calls)
         ctrl = ctrl.with_newkey()
         seed, counter = ctrl._key_args(ctrl.master_key)
         res = _lib.SrbdResult()
         rc = _lib.lib.srbd_foothold_mpc_step(vfa.search.h, self.heightmaps.FL.terrain.h, C.byref(vfa._params()),
                                              ctx.h, self._io_ref, ctx._a_contact, H, ctx._a_best,
                                              ctrl.num_control_parameters_single_leg, seed, counter, C.byref(res))
+        # the objects' state, as the Python chain leaves it -- also when a call of the chain failed (io.stage:
+        # the calls that completed), so an error leaves them as compute_adaptation / compute_control would
+        vfa.reset()
+        if io.stage >= 1:
+            hm = self._io_hm.copy()
+            for i, m in enumerate(self.heightmaps):
+                m._data, m.pending = hm[i][:, :, None, :], None
+            fh = a["footholds"].reshape(4, 3).copy()
+            boxes, valid = a["boxes"].reshape(4, 2, 3), a["valid"]
+            constraints = vfa.footholds_constraints
+            for i, n in enumerate(LEGS):
+                if valid[i]:
+                    constraints[n] = [boxes[i, 0].copy(), boxes[i, 1].copy()]
+            vfa.last_scores = self._io_scores.copy()
+            vfa.update_footholds_adaptation(LegsAttr(fh[0], fh[1], fh[2], fh[3]))
+            self._ref_state, self._ref_src = None, (ref_base, fh, LegsAttr(*constraints))
+            self.last_constraints = constraints
+        else:  # the patches stay pending around the seeds (update_height_map ran, the search did not)
+            for i, m in enumerate(self.heightmaps):
+                m._data, m.pending = None, (seeds[3 * i:3 * i + 3].copy(), io.yaw)
+        if io.stage >= 2:
+            iface.previous_contact_mpc = current_contact
+            ctrl.best_control_parameters = ctx._best.copy()
+        else:  # compute_control's with_newkey had not run
+            ctrl.master_key, ctrl._calls = key0
         if rc != _lib.OK:
-            raise RuntimeError(f"srbd_foothold_mpc_step failed ({rc}): {_lib.last_error(ctx.h)} "
-                               f"{vfa.search.h and _lib.lib.srbd_tamols_last_error(vfa.search.h)}")
+            what = "srbd_tamols_run_terrain" if io.stage == 0 else "srbd_prepare_state" if io.stage == 1 else "srbd_step"
+            msg = _lib.lib.srbd_tamols_last_error(vfa.search.h) if io.stage == 0 else _lib.last_error(ctx.h)
+            raise RuntimeError(f"srbd_foothold_mpc_step: {what} failed ({rc}): "
+                               f"{msg.decode() if isinstance(msg, bytes) else msg}")
         ctx.step_id += 1
-        # the objects' state, as the Python chain leaves it
-        hm = self._io_hm.copy()
-        for i, m in enumerate(self.heightmaps):
-            m._data, m.pending = hm[i][:, :, None, :], None
-        fh = a["footholds"].reshape(4, 3).copy()
-        boxes, valid = a["boxes"].reshape(4, 2, 3), a["valid"]
-        constraints = vfa.footholds_constraints
-        for i, n in enumerate(LEGS):
-            if valid[i]:
-                constraints[n] = [boxes[i, 0].copy(), boxes[i, 1].copy()]
-        vfa.last_scores = self._io_scores.copy()
-        vfa.update_footholds_adaptation(LegsAttr(fh[0], fh[1], fh[2], fh[3]))
-        self._ref_state, self._ref_src = None, (ref_base, fh, LegsAttr(*constraints))
-        self.last_constraints = constraints
-        iface.previous_contact_mpc = current_contact
-        ctrl.best_control_parameters = ctx._best.copy()
         ctrl.last_result = res
         g = np.array(res.grf, dtype=np.float32)
         grfs = LegsAttr(FL=g[0:3] * current_contact[0], FR=g[3:6] * current_contact[1],
@@ -162,7 +171,8 @@ class TamolsMpcStep:
              base_ang_vel: np.ndarray, pgg_phase_signal: np.ndarray, pgg_step_freq: float, optimize_swing: int = 0):
         """ref_base: ``ref_position``, ``ref_linear_velocity``, ``ref_orientation``, ``ref_angular_velocity``.
         Returns ``compute_control``'s 7-tuple; the ref_state it was given is kept in ``last_ref_state``."""
-        if self._fusable():
+        cs = np.asarray(contact_sequence)
+        if self._fusable() and cs.ndim == 2 and cs.shape[0] == 4 and cs.shape[1] >= self.controller.horizon:
             return self._step_fused(state_current, ref_feet_pos, hip_pos, ref_base, contact_sequence, base_lin_vel,
                                     base_ori_euler_xyz)
         feet = LegsAttr(*[np.asarray(state_current["foot_" + n], dtype=np.float64) for n in LEGS])
