@@ -160,9 +160,8 @@ class TamolsMpcStep:
                                f"{msg.decode() if isinstance(msg, bytes) else msg}")
         ctx.step_id += 1
         ctrl.last_result = res
-        g = np.array(res.grf, dtype=np.float32)
-        grfs = LegsAttr(FL=g[0:3] * current_contact[0], FR=g[3:6] * current_contact[1],
-                        RL=g[6:9] * current_contact[2], RR=g[9:12] * current_contact[3])
+        g = np.array(res.grf, dtype=np.float32).reshape(4, 3) * current_contact[:, None]  # as compute_control
+        grfs = LegsAttr(FL=g[0], FR=g[1], RL=g[2], RR=g[3])
         footholds = LegsAttr(FL=fh[0], FR=fh[1], RL=fh[2], RR=fh[3])
         return grfs, footholds, None, None, None, 1.4, np.array(res.predicted_state, dtype=np.float32)
 

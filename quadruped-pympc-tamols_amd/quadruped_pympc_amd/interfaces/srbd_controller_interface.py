@@ -64,7 +64,8 @@ class SRBDControllerInterface:
 
         nmpc_footholds = LegsAttr(FL=ref_state["ref_foot_FL"][0], FR=ref_state["ref_foot_FR"][0],
                                   RL=ref_state["ref_foot_RL"][0], RR=ref_state["ref_foot_RR"][0])
-        nmpc_GRFs = np.array(nmpc_GRFs)
-        nmpc_GRFs = LegsAttr(FL=nmpc_GRFs[0:3] * current_contact[0], FR=nmpc_GRFs[3:6] * current_contact[1],
-                             RL=nmpc_GRFs[6:9] * current_contact[2], RR=nmpc_GRFs[9:12] * current_contact[3])
+        # leg l's GRFs times current_contact[l] (SCI:175-178), the four products in one array operation (the same
+        # dtype promotion and values as four array x scalar products)
+        g = np.asarray(nmpc_GRFs).reshape(4, 3) * current_contact[:, None]
+        nmpc_GRFs = LegsAttr(FL=g[0], FR=g[1], RL=g[2], RR=g[3])
         return nmpc_GRFs, nmpc_footholds, None, None, None, best_sample_freq, nmpc_predicted_state
