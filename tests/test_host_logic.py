@@ -173,6 +173,55 @@ def test_prepare_state_and_reference_matches_oracle(cur, prev):
     np.testing.assert_array_equal(m.best_control_parameters, b_ref)
 
 
+def test_prepare_state_staging_shapes_and_copies():
+    """prepare_state_and_reference stages into persistent buffers: contacts as lists or (4, 1) columns, the warm start
+    as (1, P) give the oracle's arrays; the returned arrays are copies (a second call does not change the first
+    call's), and a size mismatch raises as np.reshape does.  float32 state arrays: the reference's array is float32
+    (NMPC:575-596 concatenates without a dtype, so the swing feet it substitutes are rounded to float32); here it is
+    float64 with the feet exact -- the same float32 values once srbd_step stages the state (checked below)."""
+    rng = np.random.default_rng(5)
+    m = Sampling_MPC(cfg_module(sampling_method="mppi", control_parametrization="zero_order"))
+    PL = m.num_control_parameters_single_leg
+    outs = []
+    for k, (cur, prev) in enumerate([([0, 1, 1, 0], [1, 1, 1, 1]), ([1, 0, 0, 1], [0, 1, 1, 0])]):
+        best = rng.standard_normal(m.num_control_parameters).astype(f32)
+        sc, rs = dicts(rng)
+        if k == 1:
+            sc = {n: v.astype(f32) for n, v in sc.items()}
+        s_ref, r_ref, b_ref = prepare_state_and_reference(sc, rs, np.array(cur), np.array(prev), best.copy(), PL)
+        m.best_control_parameters = best.reshape(1, -1) if k == 0 else best
+        c_in = list(cur) if k == 0 else np.array(cur, np.float64).reshape(4, 1)
+        s, r = m.prepare_state_and_reference(sc, rs, c_in, prev)
+        if k == 1:
+            assert s_ref.dtype == f32 and s.dtype == np.float64
+            np.testing.assert_array_equal(s.astype(f32), s_ref)
+            s_ref = s_ref.astype(np.float64)
+            s_ref[12:] = np.where(np.repeat(np.array(cur) == 0, 3), np.concatenate(
+                [rs["ref_foot_" + n].reshape(3) for n in ("FL", "FR", "RL", "RR")]), s_ref[12:])
+        np.testing.assert_array_equal(s, s_ref)
+        np.testing.assert_array_equal(r, r_ref)
+        np.testing.assert_array_equal(m.best_control_parameters, b_ref)
+        outs.append((s, s.copy(), r, r.copy()))
+    for s, s0, r, r0 in outs:
+        np.testing.assert_array_equal(s, s0)
+        np.testing.assert_array_equal(r, r0)
+    with pytest.raises(ValueError):
+        m.prepare_state_and_reference(sc, rs, [1, 1, 1], [1, 1, 1, 1])
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.int64, np.float32, bool])
+def test_grf_contact_masking_matches_per_leg_products(dtype):
+    """compute_control's GRF masking as one (4, 3) x (4, 1) product: the dtype and values of the reference's four
+    array x scalar products (SCI:175-178) for every contact dtype."""
+    g = (np.arange(12, dtype=np.float32) - 5.5) * np.float32(1.37)
+    cc = np.array([1, 0, 1, 1]).astype(dtype)
+    per_leg = [g[0:3] * cc[0], g[3:6] * cc[1], g[6:9] * cc[2], g[9:12] * cc[3]]
+    one = g.reshape(4, 3) * cc[:, None]
+    for a, b in zip(per_leg, one):
+        np.testing.assert_array_equal(a, b)
+        assert a.dtype == b.dtype
+
+
 @pytest.mark.parametrize("par,H", [("zero_order", 12), ("linear_spline", 12), ("cubic_spline", 16)])
 def test_spline_host_matches_oracle(par, H):
     m = Sampling_MPC(cfg_module(sampling_method="mppi", control_parametrization=par, horizon=H))
