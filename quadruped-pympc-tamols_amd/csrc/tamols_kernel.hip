@@ -176,6 +176,7 @@ __device__ __forceinline__ double tamols_score(const TamolsArgs& a, int leg, dou
 }
 
 constexpr int TAMOLS_SLICE = (TAMOLS_MAXCAND + TAMOLS_BPL - 1) / TAMOLS_BPL;  // candidates per block, max
+static_assert(TAMOLS_BPL <= 64, "the merge loads one slice partial per lane of one wave");
 
 __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const TamolsJob j) {
     __shared__ double px[TAMOLS_MAXCAND], py[TAMOLS_MAXCAND], pz[TAMOLS_MAXCAND];
@@ -324,20 +325,30 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
     }
     __syncthreads();
     TAM_STAMP(4);
-    if (!last || tid != 0) return;
+    if (!last || tid >= 64) return;
+    // wave 0 of the leg's last block: lane q loads slice q's partial (all NB in one round trip -- the loads go past
+    // the L2s, ~0.3 us each, and one lane loading them in turn took ~4 us), then every lane folds them in block
+    // order through lane shuffles (strict <, the first minimum wins, as the sequential fold)
+    double ps = INFINITY, pi = -1.0, ph = 0.0, pseed = 0.0;
+    if (tid < NB) {
+        const double* P = j.part + 4 * ((size_t)leg * NB + tid);
+        ps = __hip_atomic_load(P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pi = __hip_atomic_load(P + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ph = __hip_atomic_load(P + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pseed = __hip_atomic_load(P + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     int bi = -1;
     double bs = INFINITY, bh = 0.0;
     for (int q = 0; q < NB; ++q) {
-        const double* P = j.part + 4 * ((size_t)leg * NB + q);
-        const double s = __hip_atomic_load(P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double s = __shfl(ps, q), i = __shfl(pi, q), h = __shfl(ph, q);
         if (s < bs) {
             bs = s;
-            bi = (int)__hip_atomic_load(P + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            bh = __hip_atomic_load(P + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bi = (int)i;
+            bh = h;
         }
     }
-    const double seedh = __hip_atomic_load(j.part + 4 * ((size_t)leg * NB) + 3, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+    const double seedh = __shfl(pseed, 0);
+    if (tid != 0) return;
     const srbd_tamols_params& p = a.p;
     double* F = j.out + 3 * leg;  // [fh 12 | box 24 | seedh 4 | valid 4 x int32]
     double* B = j.out + 12 + 6 * leg;

@@ -28,6 +28,7 @@ kw = dict(forward_vel=np.array([0.5, 0.0, 0.0]), base_position=np.array([1.03, 0
 _lib.lib.srbd_tamols_phases(srch.h, 1, None)
 acc = np.zeros(5)
 sub = np.zeros(3)
+skew = np.zeros(4)  # block starts: last, median; last slice counted; last leg's end (us from the first start)
 n = 200
 for k in range(n + 10):
     srch.run_terrain(ter, 0.0, feet + np.array([0.12, 0.01, 0.0]), hips, ps, **kw)
@@ -37,6 +38,10 @@ for k in range(n + 10):
         acc += out
         raw = np.zeros(4 * 64 * 8, np.uint64)  # block 0 of leg 0: start, staged, walked, patch done
         _lib.lib.srbd_tamols_phases_raw(srch.h, raw.ctypes.data)
+        st = raw.reshape(4 * 64, 8)[: 4 * 16].astype(np.float64)  # 4 legs x TAMOLS_BPL (16) blocks
+        t0b = st[:, 0].min()
+        skew += np.array([st[:, 0].max() - t0b, np.median(st[:, 0]) - t0b, st[:, 4].max() - t0b,
+                          st[:, 5].max() - t0b]) * 0.01
         s0 = raw[:8].astype(np.float64)
         if s0[6] and s0[7]:
             sub += np.array([s0[6] - s0[0], s0[7] - s0[6], s0[1] - s0[7]]) * 0.01
@@ -50,4 +55,6 @@ lat = np.array(lat[10:]) * 1e6
 print(json.dumps({"phases_us": dict(zip(("patch", "queries", "scores", "argmin_count", "span"),
                                         np.round(acc / n, 3).tolist())),
                   "patch_split_us": dict(zip(("stage_scene", "walk", "combine"), np.round(sub / n, 3).tolist())),
+                  "starts_us": dict(zip(("last_start", "median_start", "last_counted", "last_leg_end"),
+                                        np.round(skew / n, 3).tolist())),
                   "p50_us": round(float(np.percentile(lat, 50)), 2), "p99_us": round(float(np.percentile(lat, 99)), 2)}))
