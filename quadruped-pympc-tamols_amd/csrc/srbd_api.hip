@@ -2171,7 +2171,7 @@ extern "C" int srbd_tamols_create(int32_t device_id, srbd_tamols_ctx** out) {
     t->device = device_id;
     bool ok = hipSetDevice(device_id) == hipSuccess &&
               hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) == hipSuccess &&
-              hipHostMalloc((void**)&t->h_flag, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) ==
+              hipHostMalloc((void**)&t->h_flag, sizeof(uint32_t) * 4, hipHostMallocMapped | hipHostMallocCoherent) ==
                   hipSuccess &&
               hipHostGetDevicePointer((void**)&t->d_flag, t->h_flag, 0) == hipSuccess &&
               hipMalloc((void**)&t->d_part, sizeof(double) * 4 * TAMOLS_BPL * 4) == hipSuccess &&
@@ -2182,7 +2182,7 @@ extern "C" int srbd_tamols_create(int32_t device_id, srbd_tamols_ctx** out) {
         srbd_tamols_destroy(t);
         return fail(nullptr, SRBD_E_HIP, "TAMOLS context allocation failed");
     }
-    __atomic_store_n(t->h_flag, 0u, __ATOMIC_RELEASE);
+    for (int l = 0; l < 4; ++l) __atomic_store_n(t->h_flag + l, 0u, __ATOMIC_RELEASE);  // one word per leg
     *out = t;
     return SRBD_OK;
 }
@@ -2270,12 +2270,17 @@ static int tamols_launch_wait(srbd_tamols_ctx* t, TamolsJob& j, const double* se
     j.dbg = t->d_dbg;
     launch_tamols_fused(j, t->stream);
     TAM_TRY(t, hipGetLastError());
+    const auto published = [&] {  // every leg's word holds this call's sequence number
+        for (int l = 0; l < 4; ++l)
+            if (__atomic_load_n(t->h_flag + l, __ATOMIC_ACQUIRE) != j.seq) return false;
+        return true;
+    };
     for (uint64_t it = 1;; ++it) {
-        if (__atomic_load_n(t->h_flag, __ATOMIC_ACQUIRE) == j.seq) break;
+        if (published()) break;
         if ((it & 4095) == 0) {
             const hipError_t e = hipStreamQuery(t->stream);
             if (e == hipSuccess) {
-                if (__atomic_load_n(t->h_flag, __ATOMIC_ACQUIRE) == j.seq) break;
+                if (published()) break;
                 t->err = "TAMOLS launch completed without publishing its outputs";
                 return SRBD_E_HIP;
             }

@@ -234,8 +234,8 @@ struct TamolsJob {
     double* scores;      // 4 x nc or NULL
     double* out;         // fh 12 | boxes 24 | seed heights 4 | valid 4 x int32 (2 doubles)
     double* part;        // 4 x TAMOLS_BPL x 4 partials (device)
-    unsigned* cnt;       // 4 per-leg block counters + 1 leg counter (device, zero between calls)
-    uint32_t* flag;      // host-mapped publish word
+    unsigned* cnt;       // 4 per-leg block counters (device, zero between calls)
+    uint32_t* flag;      // host-mapped publish words, one per leg
     uint32_t seq;
     uint64_t* dbg;       // diagnostic phase stamps (4 x TAMOLS_BPL x 8) or NULL
 };

@@ -14,7 +14,7 @@
 //   phase C: strict-< argmin over the slice in candidate order -> (score, index, height) partial.
 // The last block of a leg to finish (per-leg counter; partials stored write-through) merges them in block
 // order (strict <, so the first minimum over all candidates wins, VFA:185-190) and writes the leg's
-// foothold, box and validity; the last leg to finish publishes the call's sequence number to the host.
+// foothold, box and validity and publishes the call's sequence number in its own host word.
 // Outputs go straight to host-mapped memory; the host spins on the flag (no copy, no stream sync).
 // float64 keeps the host oracle's decisions (reach bounds, argmin) bit-for-bit comparable.
 #include "terrain_ray.h"
@@ -374,13 +374,10 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
     }
     j.out[36 + leg] = seedh;
     __hip_atomic_store(j.cnt + leg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next call
-    __threadfence_system();  // this leg's host-mapped outputs
-    const unsigned done = __hip_atomic_fetch_add(j.cnt + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence_system();  // this leg's host-mapped outputs (and, fenced before the count, its blocks' scores)
+    // the leg publishes on its own word: the host waits for all four (no cross-leg counter round trip)
+    __hip_atomic_store(j.flag + leg, j.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     TAM_STAMP(5);
-    if (done == 3u) {  // the last leg: every leg's outputs have reached the system -> publish
-        __hip_atomic_store(j.cnt + 4, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(j.flag, j.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
 #undef TAM_STAMP
 }
 
