@@ -133,6 +133,10 @@ int srbd_armed_stats(const srbd_ctx* ctx, int64_t* served, int64_t* cancelled);
 int srbd_armed_refired(const srbd_ctx* ctx, int64_t* refired);
 /* Test hook: the host sleeps delay_us between claiming an armed chain and storing its go word. */
 int srbd_debug_arm_delay(srbd_ctx* ctx, uint32_t delay_us);
+/* Test hook: the next column-split merge (CEM, or > 256 records) has one slice withhold its hand-off word, so
+ * the tail block's bounded wait (2 s) times out and the step fails with SRBD_E_HIP; the call resets the
+ * hand-off state, and the following step is exact again. */
+int srbd_debug_split_drop(srbd_ctx* ctx);
 
 /*
  * Gait-adaptive sampling (centroidal_nmpc_jax_gait_adaptive.py; replaces
@@ -424,6 +428,40 @@ int srbd_foothold_mpc_step(srbd_tamols_ctx* tamols, srbd_terrain* terrain, const
                            srbd_ctx* ctx, srbd_foothold_io* io, const float* contact, int32_t contact_stride,
                            float* best_params, int32_t params_per_leg, uint64_t seed, uint64_t counter,
                            srbd_result* out);
+
+/* ------------------------------------------------------------------ one plugin-API MPC step in one call
+ * SRBDControllerInterface.compute_control's sampling branch (srbd_controller_interface.py:113-180) over the plain
+ * Sampling_MPC, behind one host call: prepare_state_and_reference (centroidal_nmpc_jax.py:563-627, no solution
+ * shift: the caller keeps that case) -> per sampling iteration: with_newkey (:498-501) -> CEM's
+ * with_newsigma(sigma_cem_mppi) at iteration 0 -> jitted_compute_control (srbd_step on device draws) -> the GRFs
+ * times current_contact (SCI:175-178).  The same calls in the same order as the Python chain, so the same bits.
+ * Key (in/out, advanced once per iteration as with_newkey + the step's key arguments do):
+ *   SRBD_RNG_PHILOX   : key = (seed, counter); with_newkey: counter + 1; the step runs (seed, counter)
+ *   SRBD_RNG_JAX[_LEGACY]: key[0] = the packed JAX key (key[0] << 32 | key[1]), key[1] = the controller's call
+ *                       count; with_newkey: key = split(key)[0]; the step runs (packed key, call count + 1). */
+typedef struct srbd_interface_io {
+    /* inputs */
+    double state_in[24];        /* position, linear_velocity, orientation, angular_velocity, foot_FL..RR */
+    double ref_in[24];          /* ref_position .. ref_angular_velocity, ref_foot_FL..RR */
+    double current_contact[4];  /* contact_sequence[:, 0] */
+    double previous_contact[4]; /* the interface's previous_contact_mpc */
+    double sigma_reset;         /* CEM: mpc_params['sigma_cem_mppi'] */
+    uint64_t key[2];            /* in/out, see above */
+    int32_t horizon, iterations, rng, cem; /* H, num_sampling_iterations, SRBD_RNG_*, method == CEM */
+    /* outputs */
+    double state_out[24], ref_out[24]; /* prepare_state_and_reference's outputs */
+    double grf[12];             /* the last iteration's GRFs times current_contact (float64) */
+    int32_t stage;              /* the calls that completed: 0 none, 1 prepare_state, 2 + i: iteration i's step */
+    int32_t pad;
+} srbd_interface_io;
+
+/* contact / contact64: 4 x contact_stride float32 or float64 values (exactly one non-NULL; the first `horizon`
+ * columns are used, float64 rounded to float32 as the step stages them).  best_params (in/out, 4 x params_per_leg):
+ * the warm start (lift-off legs zeroed, then each iteration's result); sigma (in/out, CEM only, P floats).  `out`:
+ * the last iteration's srbd_result. */
+int srbd_interface_step(srbd_ctx* ctx, srbd_interface_io* io, const float* contact, const double* contact64,
+                        int32_t contact_stride, float* best_params, int32_t params_per_leg, float* sigma,
+                        srbd_result* out);
 
 /* Diagnostic: enable != 0 stamps the phases of the following TAMOLS calls; out_us[5] (may be NULL)
  * receives the last call's mean per-block durations of (patch, queries, scores, slice argmin + count)

@@ -424,6 +424,8 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     const size_t noise_bytes = sizeof(float) * (size_t)mc.P * mc.ldn;
     if ((e = hipMalloc((void**)&c->d_in, STEP_INPUT_ALLOC)) != hipSuccess) return cleanup_fail("hipMalloc", e);
     if ((e = hipMalloc((void**)&c->d_out, sizeof(StepOutput))) != hipSuccess) return cleanup_fail("hipMalloc", e);
+    // a column-split merge only ORs late bits into status, so the device output starts zeroed (srbd_sync_result)
+    if ((e = hipMemset(c->d_out, 0, sizeof(StepOutput))) != hipSuccess) return cleanup_fail("hipMemset", e);
     for (int b = 0; b < 2; ++b)
         if ((e = hipMalloc((void**)&c->d_noise[b], noise_bytes)) != hipSuccess) return cleanup_fail("hipMalloc", e);
     if ((e = hipMalloc((void**)&c->d_costs, sizeof(float) * mc.ldn)) != hipSuccess)
@@ -687,15 +689,21 @@ static int wait_published(srbd_ctx* c, uint32_t seq, int nflags = 1, int* cancel
 
 // A step whose merge reported a timed-out in-launch hand-off (StepOutput::status != 0: fast_tail -1, the column
 // split's tail block / a slice 1 / 2): drain the stream, so no block of that launch is still writing, reset the
-// hand-off state (the split's epoch and tagged words, the arrival counts) and fail the call.  The host zeroes
-// status before each launch (the column split only ORs its late bits in).
-static int check_handoff(srbd_ctx* c) {
-    if (__atomic_load_n(&c->h_out->status, __ATOMIC_ACQUIRE) == 0) return SRBD_OK;
-    const int st = c->h_out->status;
+// hand-off state (the split's epoch and tagged words -- zeroed, so the next launch cannot accept a late word of
+// the timed-out one --, the arrival counts, the device output's status) and fail the call.  Every path that
+// launches a merge zeroes the status it reads before the launch (the column split only ORs its late bits in):
+// srbd_step and srbd_step_finish the host-mapped one; device chains the device one, zeroed at create and here.
+// An armed chain queued behind the timed-out step is cancelled first, so the drain does not wait out its copy
+// kernel's deadline and the next call does not claim a chain that has given up.
+static int check_handoff(srbd_ctx* c, int st = 0) {
+    if (!st) st = __atomic_load_n(&c->h_out->status, __ATOMIC_ACQUIRE);
+    if (st == 0) return SRBD_OK;
+    arm_cancel(c);
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     HIP_TRY(c, hipMemset(reinterpret_cast<char*>(c->d_in) + sizeof(StepInput), 0, sizeof(SplitXchg)));
     if (c->d_gcnt) HIP_TRY(c, hipMemset(c->d_gcnt, 0, sizeof(uint32_t) * (size_t)c->ngroups));
     if (c->d_gdone) HIP_TRY(c, hipMemset(c->d_gdone, 0, sizeof(uint32_t)));
+    HIP_TRY(c, hipMemset(&c->d_out->status, 0, sizeof(int32_t)));
     c->h_out->status = 0;
     return fail(c, SRBD_E_HIP, "merge hand-off timed out (status " + std::to_string(st) + ")");
 }
@@ -941,6 +949,17 @@ extern "C" int srbd_debug_arm_delay(srbd_ctx* c, uint32_t delay_us) {
     return SRBD_OK;
 }
 
+extern "C" int srbd_debug_split_drop(srbd_ctx* c) {
+    if (!c) return SRBD_E_INVALID;
+    arm_cancel(c);
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    const uint32_t one = 1;
+    HIP_TRY(c, hipMemcpyAsync(reinterpret_cast<char*>(c->d_in) + sizeof(StepInput) + offsetof(SplitXchg, drop), &one,
+                              sizeof(one), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return SRBD_OK;
+}
+
 extern "C" int srbd_armed_stats(const srbd_ctx* c, int64_t* served, int64_t* cancelled) {
     if (!c) return SRBD_E_INVALID;
     std::lock_guard<std::mutex> lk(g_arm_mu);
@@ -988,6 +1007,7 @@ extern "C" int srbd_step_finish(srbd_ctx* c, const void* d_records, int32_t nrec
     if (nrec != c->mc.t_world) return fail(c, SRBD_E_INVALID, "srbd_step_finish takes world_size rank records");
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     const Publish pub{c->d_flag, ++c->seq};
+    c->h_out->status = 0;  // check_handoff (a column split ORs late bits in)
     // the gathered rank buffers are the exchange level's node list in order (ceil partition, tree_shape)
     const int nflags = launch_merge(c->mc, c->d_in, (const float*)d_records, c->mc.t_xnodes,
                                     rec_floats_rank(c->mc.P, c->mc.K), 1, nullptr, nullptr, c->d_out_host, 0,
@@ -995,6 +1015,7 @@ extern "C" int srbd_step_finish(srbd_ctx* c, const void* d_records, int32_t nrec
     HIP_TRY(c, hipGetLastError());
     int rc = wait_published(c, pub.seq, nflags);
     if (rc) return rc;
+    if ((rc = check_handoff(c))) return rc;
     if (out_costs_local) {
         HIP_TRY(c, hipMemcpyAsync(out_costs_local, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,
                                   c->stream));
@@ -1045,6 +1066,11 @@ extern "C" int srbd_sync_result(srbd_ctx* c, float* best, float* sigma, srbd_res
     HIP_TRY(c, hipSetDevice(c->cfg.device_id));
     HIP_TRY(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(StepOutput), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    // a device chain's merges OR a timed-out hand-off into d_out's status (sticky over the chain): report it
+    // and reset the hand-off state, as a host step does
+    const int st = c->h_out->status;
+    int rc;
+    if (st && (rc = check_handoff(c, st))) return rc;
     return copy_out(c, best, sigma, out);
 }
 
@@ -1709,6 +1735,7 @@ static int xg_step(srbd_ctx* c, const float* state, const float* ref, const floa
     if ((rc = acquire_noise(c, noise_local, seed, counter, &buf))) return rc;
     const bool fuse = !noise_local && fusable(c);
     const Publish pub{c->d_flag, ++c->seq};
+    c->h_out->status = 0;  // check_handoff / the exchange's -1
     enqueue_xchg_step(c, buf, c->d_out_host, 0, fuse, pub, ks ? &ksi : nullptr);
     HIP_TRY(c, hipGetLastError());
     if (fuse) {
@@ -1720,7 +1747,7 @@ static int xg_step(srbd_ctx* c, const float* state, const float* ref, const floa
     c->chain_started = false;
     c->input_ready = true;
     if ((rc = wait_published(c, pub.seq))) return rc;
-    if (c->h_out->status != 0) return xg_check_err(c) ? SRBD_E_HIP : fail(c, SRBD_E_HIP, "exchange step failed");
+    if (c->h_out->status != 0) return xg_check_err(c) ? SRBD_E_HIP : check_handoff(c);
     if (out_costs_local) {
         HIP_TRY(c, hipMemcpyAsync(out_costs_local, c->d_costs, sizeof(float) * c->mc.n_local, hipMemcpyDeviceToHost,
                                   c->stream));

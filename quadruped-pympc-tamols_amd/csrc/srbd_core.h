@@ -97,7 +97,8 @@ static_assert(sizeof(StepInput) % 16 == 0 && offsetof(StepInput, best) % 16 == 0
 // slice read the epoch before storing them).
 struct SplitXchg {
     uint32_t epoch;
-    uint32_t pad[3];
+    uint32_t drop;  // tests (srbd_debug_split_drop): != 0 makes slice 1 withhold a word; cleared by the reset
+    uint32_t pad[2];
     uint64_t elite[2 * MAXK];  // the top-K keys' low and high halves
     uint64_t sums[MAXP + 1];   // column j: sum_r scale_r v_r[j]; [P]: sum_r scale_r s_r (float bits)
 };

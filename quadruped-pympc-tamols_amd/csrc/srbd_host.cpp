@@ -252,3 +252,64 @@ extern "C" int srbd_jax_split(const uint32_t key[2], int32_t num, int32_t partit
     }
     return SRBD_OK;
 }
+
+// ------------------------------------------------------------------ one plugin-API MPC step in one call
+// SRBDControllerInterface.compute_control's sampling branch (srbd_controller_interface.py:113-180) over the plain
+// Sampling_MPC (include/srbd_mpc.h srbd_interface_step): prepare_state_and_reference (NMPC:563-627, no solution
+// shift), then per sampling iteration with_newkey (NMPC:498-501), CEM's with_newsigma(sigma_cem_mppi) at iteration 0,
+// jitted_compute_control (srbd_step on device draws, NMPC:629-1094), and the GRFs times current_contact (SCI:175-178).
+// The same calls in the same order as the Python chain, so the same bits.
+extern "C" int srbd_interface_step(srbd_ctx* ctx, srbd_interface_io* io, const float* contact,
+                                   const double* contact64, int32_t contact_stride, float* best_params,
+                                   int32_t params_per_leg, float* sigma, srbd_result* out) {
+    if (!ctx || !io || (!contact == !contact64) || !best_params || !out || params_per_leg < 1 ||
+        io->iterations < 1 || contact_stride < io->horizon || io->horizon < 1 || io->horizon > SRBD_MAX_HORIZON)
+        return SRBD_E_INVALID;
+    if (io->cem && !sigma) return SRBD_E_INVALID;
+    io->stage = 0;
+    int rc = srbd_prepare_state(io->state_in, io->ref_in, io->current_contact, io->previous_contact, params_per_leg,
+                                best_params, io->state_out, io->ref_out);
+    if (rc != SRBD_OK) return rc;
+    io->stage = 1;
+    float st[24], rf[24];
+    for (int i = 0; i < 24; ++i) {  // the step's float32 staging (Context._stage: numpy's round-to-nearest cast)
+        st[i] = (float)io->state_out[i];
+        rf[i] = (float)io->ref_out[i];
+    }
+    float cf[4 * SRBD_MAX_HORIZON];
+    const float* cs = contact;
+    int32_t stride = contact_stride;
+    if (contact64) {
+        const int H = io->horizon;
+        for (int l = 0; l < 4; ++l)
+            for (int k = 0; k < H; ++k) cf[l * H + k] = (float)contact64[(size_t)l * contact_stride + k];
+        cs = cf;
+        stride = H;
+    }
+    const int P = 4 * params_per_leg;
+    for (int it = 0; it < io->iterations; ++it) {
+        uint64_t seed, counter;
+        if (io->rng == SRBD_RNG_PHILOX) {  // master_key = (seed, counter + 1)
+            io->key[1] += 1;
+            seed = io->key[0];
+            counter = io->key[1];
+        } else {  // master_key = split(master_key)[0]; the call count numbers the device step
+            const uint32_t k[2] = {(uint32_t)(io->key[0] >> 32), (uint32_t)io->key[0]};
+            uint32_t o[4];
+            if ((rc = srbd_jax_split(k, 2, io->rng == SRBD_RNG_JAX ? 1 : 0, o)) != SRBD_OK) return rc;
+            io->key[0] = ((uint64_t)o[0] << 32) | o[1];
+            io->key[1] += 1;
+            seed = io->key[0];
+            counter = io->key[1];
+        }
+        if (io->cem && it == 0)
+            for (int j = 0; j < P; ++j) sigma[j] = (float)io->sigma_reset;
+        rc = srbd_step(ctx, st, rf, cs, stride, best_params, io->cem ? sigma : nullptr, nullptr, seed, counter, out,
+                       nullptr);
+        if (rc != SRBD_OK) return rc;
+        io->stage = 2 + it;
+    }
+    for (int l = 0; l < 4; ++l)
+        for (int c = 0; c < 3; ++c) io->grf[3 * l + c] = (double)out->grf[3 * l + c] * io->current_contact[l];
+    return SRBD_OK;
+}

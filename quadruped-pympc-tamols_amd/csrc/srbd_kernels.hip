@@ -1231,8 +1231,10 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     }
     if (SPLITX && hand && !tailblk) {  // a slice publishes its columns' sums (block 1 also the weights' sum)
         __syncthreads();
+        // srbd_debug_split_drop (tests): block 1 withholds the weights' sum, so the tail block's wait times out
+        const bool drop = blockIdx.x == 1 && __hip_atomic_load(&xg->drop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (int i = tid; i <= ncol; i += T)
-            if (i < ncol || blockIdx.x == 1)
+            if (i < ncol || (blockIdx.x == 1 && !drop))
                 __hip_atomic_store(&xg->sums[i < ncol ? jc(i) : P], tagged(f2u(Vs[i])), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
     }

@@ -73,6 +73,15 @@ class FootholdIO(C.Structure):
     ]
 
 
+class InterfaceIO(C.Structure):
+    """srbd_interface_io (include/srbd_mpc.h): one SRBDControllerInterface.compute_control step's inputs / outputs."""
+    _fields_ = [
+        ("state_in", _D * 24), ("ref_in", _D * 24), ("current_contact", _D * 4), ("previous_contact", _D * 4),
+        ("sigma_reset", _D), ("key", C.c_uint64 * 2), ("horizon", _I), ("iterations", _I), ("rng", _I), ("cem", _I),
+        ("state_out", _D * 24), ("ref_out", _D * 24), ("grf", _D * 12), ("stage", _I), ("pad", _I),
+    ]
+
+
 SIGNATURES = {
     "srbd_num_params": (_I, [C.POINTER(SrbdConfig)]),
     "srbd_device_count": (_I, [_IP]),
@@ -90,6 +99,7 @@ SIGNATURES = {
     "srbd_armed_stats": (_I, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "srbd_armed_refired": (_I, [_P, C.POINTER(C.c_int64)]),
     "srbd_debug_arm_delay": (_I, [_P, C.c_uint32]),
+    "srbd_debug_split_drop": (_I, [_P]),
     "srbd_record_floats": (_I, [_P]),
     "srbd_record_floats_host": (_I, [C.POINTER(SrbdConfig)]),
     "srbd_shard_rows": (_I, [C.c_int64, _I, _I, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
@@ -166,6 +176,7 @@ SIGNATURES.update({
                                      C.POINTER(TamolsParams), _P, _P, _P, _P, _P, _P]),
     "srbd_foothold_mpc_step": (_I, [_P, _P, C.POINTER(TamolsParams), _P, C.POINTER(FootholdIO), _P, _I, _P, _I,
                                     C.c_uint64, C.c_uint64, C.POINTER(SrbdResult)]),
+    "srbd_interface_step": (_I, [_P, _P, _P, _P, _I, _P, _I, _P, C.POINTER(SrbdResult)]),
     "srbd_tamols_phases": (_I, [_P, _I, _FP]),
     "srbd_tamols_phases_raw": (_I, [_P, _P]),
     "srbd_set_rng": (_I, [_P, _I]),
@@ -197,7 +208,11 @@ def _load():
         )
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:  # e.g. a measurement build (probe / ASan variant) made before the ABI grew
+            raise ImportError(f"{LIB_PATH} does not export {name}: it is older than include/srbd_mpc.h -- rebuild it "
+                              "(make -C quadruped-pympc-tamols_amd [probe|asan], or __graft_entry__.build())") from None
         fn.restype = res
         fn.argtypes = args
     if lib.srbd_abi_version() != 1:
@@ -206,6 +221,23 @@ def _load():
 
 
 lib = _load()
+
+
+def _load_fast():
+    """The CPython glue of the per-MPC-step host path (csrc/srbd_pyfast.c), bound to this library instance; None
+    when it is not built (the Python chain then makes the same library calls)."""
+    if os.environ.get("SRBD_PYFAST", "1") == "0":
+        return None
+    try:
+        from . import _srbd_fast
+    except ImportError:
+        return None
+    _srbd_fast.bind(C.cast(lib.srbd_interface_step, C.c_void_p).value,
+                    C.cast(lib.srbd_pgg_contact_sequence, C.c_void_p).value)
+    return _srbd_fast
+
+
+fast = _load_fast()
 
 
 def fptr(a: np.ndarray | None):
@@ -587,6 +619,10 @@ class Context:
     def debug_arm_delay(self, delay_us: int):
         """srbd_debug_arm_delay (tests): host sleep between an armed claim and its go word."""
         self.check(lib.srbd_debug_arm_delay(self.h, int(delay_us)), "srbd_debug_arm_delay")
+
+    def debug_split_drop(self):
+        """srbd_debug_split_drop (tests): the next column-split merge's hand-off times out (the step fails)."""
+        self.check(lib.srbd_debug_split_drop(self.h), "srbd_debug_split_drop")
 
     def set_stream(self, stream_handle: int | None):
         """Launch on a caller-owned hipStream_t; None (or 0, the legacy null stream) -> the context's own."""

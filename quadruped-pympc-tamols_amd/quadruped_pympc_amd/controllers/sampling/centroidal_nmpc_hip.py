@@ -189,6 +189,19 @@ class Sampling_MPC:
         self._calls = 0  # numbers the device steps (the draws made ahead are keyed by the next key and call)
         self._ctx = None
 
+    # ------------------------------------------------------------------ copies
+    # host staging whose raw addresses are cached (with_newkey's key buffer, prepare_state's arguments) and the
+    # device context: a copy (copy.deepcopy, pickle) makes its own on first use instead of sharing the original's
+    _TRANSIENT = ("_ctx", "_split_buf", "_split_addr", "_ps")
+
+    def __getstate__(self):
+        d = {k: v for k, v in self.__dict__.items() if k not in self._TRANSIENT}
+        d["_ctx"] = None
+        return d
+
+    def __setstate__(self, d):
+        self.__dict__.update(d)
+
     # ------------------------------------------------------------------ device
     def _srbd_config(self) -> "_lib.SrbdConfig":
         mp = self._cfg.mpc_params

@@ -35,6 +35,7 @@ class PeriodicGaitGenerator:
         self._seq_key = None  # (dts, lens) bytes of the cached sequence-call arguments
         self._out = np.empty(8 * _lib.MAX_HORIZON)
         self._out_p = _lib.dptr(self._out)
+        self._addr = C.addressof(self._g)
 
     # plain attributes of the reference, backed by the C struct
     duty_factor = property(lambda s: s._g.duty_factor, lambda s, v: setattr(s._g, "duty_factor", float(v)))
@@ -73,6 +74,8 @@ class PeriodicGaitGenerator:
         return np.array(self._g.phase_signal)
 
     def compute_contact_sequence(self, contact_sequence_dts, contact_sequence_lenghts):
+        if _lib.fast is not None:  # the same C call, its arguments and result array handled in C (_srbd_fast)
+            return _lib.fast.pgg_contact_sequence(self._addr, contact_sequence_dts, contact_sequence_lenghts)
         key = (np.asarray(contact_sequence_dts, dtype=np.float64).tobytes(),
                np.asarray(contact_sequence_lenghts, dtype=np.int32).tobytes())
         if key != self._seq_key:  # the 100 Hz caller passes the same arrays every step

@@ -7,6 +7,7 @@ parameter packing and the TAMOLS oracle's known answers.  Compute calls must fai
 (no HIP device, no CPU fallback).
 """
 import copy
+import ctypes as C
 import types
 
 import numpy as np
@@ -354,3 +355,71 @@ def test_tamols_oracle_unreachable_falls_back_to_seed_height():
     fh, boxes, valid, scores = orc.compute(hms, seeds, hips, None)
     assert not valid.any() and np.isinf(scores).all()
     np.testing.assert_allclose(fh[:, 2], 0.02)
+
+
+# ---------------------------------------------------------------- the per-step CPython glue (_srbd_fast)
+def test_fast_glue_is_built_and_bound():
+    assert _lib.fast is not None, "_srbd_fast is not built (make -C quadruped-pympc-tamols_amd)"
+
+
+@pytest.mark.parametrize("gait", [0, 1, 7])
+def test_pgg_fast_glue_equals_python_path(monkeypatch, gait):
+    """compute_contact_sequence through _srbd_fast equals the ctypes path (same C call) for every dts / lens form
+    the caller may pass (lists, int64 lengths), and keeps the same error."""
+    a, b = PeriodicGaitGenerator(0.65, 1.4, gait, 12), PeriodicGaitGenerator(0.65, 1.4, gait, 12)
+    for k in range(50):
+        dts, lens = ([0.02], [12]) if k % 2 else (np.array([0.01, 0.02]), np.array([3, 12], np.int64))
+        x = a.compute_contact_sequence(dts, lens)
+        monkeypatch.setattr(_lib, "fast", None)
+        y = b.compute_contact_sequence(dts, lens)
+        monkeypatch.undo()
+        assert x.dtype == y.dtype and x.shape == y.shape and x.flags["C_CONTIGUOUS"]
+        np.testing.assert_array_equal(x, y)
+        a.run(0.002 * (k % 5), 1.4)
+        b.run(0.002 * (k % 5), 1.4)
+    if gait != 7:
+        with pytest.raises(ValueError, match="compute_contact_sequence failed"):
+            a.compute_contact_sequence([0.02], [3])  # runs past the last dts entry (the reference: IndexError)
+
+
+def test_interface_glue_declines_other_inputs():
+    """interface_step returns None (the Python sequence then runs) for inputs it does not take, before it touches
+    the context, the staging or the library -- so no device is needed to check it."""
+    from quadruped_pympc_amd._lib import InterfaceIO
+
+    io = InterfaceIO()
+    io.horizon = 12
+    rng = np.random.default_rng(0)
+    sc, rs = dicts(rng)
+    best = np.zeros(48, f32)
+    cs = np.ones((4, 12))
+    args = lambda s, r, c: (0, C.addressof(io), s, r, c, best, np.ones(4), np.array([42, 0], np.uint64), 0, 1, None,
+                            np.zeros(48, f32), None, 0)
+    assert _lib.fast.interface_step(*args({k: list(v) for k, v in sc.items()}, rs, cs)) is None
+    assert _lib.fast.interface_step(*args({k: v.astype(f32) for k, v in sc.items()}, rs, cs)) is None
+    assert _lib.fast.interface_step(*args(sc, rs, cs[:, :8])) is None       # shorter than the horizon
+    assert _lib.fast.interface_step(*args(sc, rs, cs.astype(np.int64))) is None
+    del sc["foot_RR"]
+    assert _lib.fast.interface_step(*args(sc, rs, cs)) is None
+    assert io.stage == 0 and not any(io.state_in)
+
+
+def test_controller_copies_own_their_staging():
+    """with_newkey / prepare_state cache raw addresses of per-controller staging; a deepcopy (or a pickle
+    round trip) must make its own instead of writing into the original's (or freed) memory."""
+    import pickle
+
+    m = Sampling_MPC(cfg_module(sampling_method="mppi", control_parametrization="zero_order"))
+    m.with_newkey()
+    rng = np.random.default_rng(1)
+    sc, rs = dicts(rng)
+    m.prepare_state_and_reference(sc, rs, np.ones(4), np.ones(4))
+    k_orig = m.master_key.copy()
+    for c in (copy.deepcopy(m), pickle.loads(pickle.dumps(m))):
+        assert c._ctx is None and "_split_buf" not in c.__dict__ and "_ps" not in c.__dict__
+        c.with_newkey()
+        c.prepare_state_and_reference(sc, rs, np.array([0, 1, 1, 0]), np.ones(4))
+        np.testing.assert_array_equal(m.master_key, k_orig)
+        np.testing.assert_array_equal(c.master_key, _lib.jax_split(k_orig, 2)[0])
+    m.with_newkey()
+    np.testing.assert_array_equal(m.master_key, _lib.jax_split(k_orig, 2)[0])
