@@ -71,16 +71,22 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
-def spawn_ranks(args, argv) -> int:
-    """torchrun as a child process (never exec): one rank per GPU on this node."""
+def torchrun_cmd(gpus: int, argv, port: int, script: str | None = None) -> list:
+    """The launcher command of `bench.py --gpus N` without a torchrun environment: one rank per GPU of this node,
+    rendezvous on 127.0.0.1, every rank running this script with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), script or os.path.abspath(__file__)] + list(argv)
+
+
+def spawn_ranks(args, argv, script: str | None = None) -> int:
+    """torchrun as a child process (never exec): rank 0's JSON line reaches this process's stdout (the ranks
+    inherit it; the others print none) and the child's exit status is returned."""
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (xGMI mailboxes, RCCL)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
-    return subprocess.call(cmd, env=env)
+    return subprocess.call(torchrun_cmd(args.gpus, argv, port, script), env=env)
 
 
 # ---------------------------------------------------------------------------------------------- helpers
@@ -553,9 +559,11 @@ def bench_multi(_lib, w, args, rank, world, local_rank, scaling, steps=None, dev
     n_local = mpc.ctx.n_local
     kern = mpc.ctx.time_kernels(100)
     transport = mpc.transport
+    transports = [None] * world  # the exchange every rank set up (xgmi, or rccl after a failed probe)
+    dist.all_gather_object(transports, transport)
     mpc.close()
     return dict(n_total=n_total, n_local=n_local, wall=wall, lat=lat, kern=kern, dev=dev, transport=transport,
-                steps=steps, world=world)
+                transports=transports, steps=steps, world=world)
 
 
 def rows_per_rank(n_total: int, world: int):
@@ -575,6 +583,7 @@ def multi_line(w, out, scaling):
             "rows_per_rank": rows_per_rank(out["n_total"], out.get("world", 1)),
             "ms_per_step": round(1e3 * out["wall"] / out["steps"], 5), "steps": out["steps"],
             "p50_step_ms": round(float(np.percentile(lat, 50)), 4), "transport": out["transport"],
+            "transport_per_rank": out.get("transports"),
             "kernels_us": {k: round(v, 3) for k, v in out["kern"].items()}}
 
 
@@ -647,6 +656,7 @@ def main(argv=None):
         "rng": args.rng,
         "config": {"workload": w.name, "num_samples": out["n_total"], "rows_per_gpu": out["n_local"],
                    "rows_per_rank": rows_per_rank(out["n_total"], world),
+                   **({"transport_per_rank": out["transports"]} if out.get("transports") else {}),
                    "horizon": w.horizon, "method": w.method, "parametrization": w.parametrization,
                    "robot": w.robot, "gait": w.gait,
                    "parallelism": (f"rows sharded over {world} GPUs ({scaling} scaling), record exchange: "

@@ -63,7 +63,10 @@ def worker(rank, world, port, method, N, outdir):
 
 
 @pytest.mark.parametrize("world,method,N", [(2, "mppi", 1001), (2, "cem_mppi", 600), (2, "random_sampling", 450),
-                                            (3, "mppi", 1000)])
+                                            (3, "mppi", 1000),
+                                            # the driver's 8-GPU node: eight ranks, the exchange level and the
+                                            # host tree at the widest world bench.py --gpus runs
+                                            (8, "mppi", 4160), (8, "cem_mppi", 2048)])
 def test_sharded_merge_gloo(tmp_path, world, method, N):
     mp.start_processes(worker, args=(world, free_port(), method, N, str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
