@@ -115,6 +115,7 @@ struct srbd_ctx {
     bool fast_tail = false;
     bool gen_env = true;  // SRBD_GEN != "0" at create (gen_now)
     int gen_rg = GEN_REGEN_QUADS;  // quads the epilogue regenerates (SRBD_GEN_RG at create), the rest stored and read
+    int gen_quad_min = 0;  // four-lane form: rows from which the launch makes its draws (gen_now); 0 off
     uint64_t* d_gtag = nullptr;
     // its host-step outputs as tagged words (GroupArgs::outt, tagged_outputs), host-mapped
     uint64_t* h_outt = nullptr;
@@ -436,6 +437,7 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     const char* ge = getenv("SRBD_GEN");
     c->gen_env = !(ge && !strcmp(ge, "0"));
     if (const char* gr = getenv("SRBD_GEN_RG")) c->gen_rg = std::max(0, std::min(mc.P / 4, atoi(gr)));
+    if (const char* gq = getenv("SRBD_GEN_QUAD_MIN")) c->gen_quad_min = atoi(gq);
     c->gsize = group_size(mc);
     c->ngroups = (c->nleaf + TREE_FAN - 1) / TREE_FAN;
     if (c->gsize > 1) {
@@ -538,8 +540,14 @@ static bool fusable(const srbd_ctx* c) { return c->mc.n_local <= FUSE_MAX_ROWS; 
 // The step's draws made inside the rollout launch (gen_ok; SRBD_GEN=0 turns it off): host steps (the input by value)
 // at shapes whose draws do not fuse into the previous launch, device Philox stream.  The caller also checks that no
 // noise is injected.
+// The four-lane form (GEN: rollout_quad_kernel) is opt-in (SRBD_GEN_QUAD_MIN=rows at create; measured slower at the
+// north-star shape: step launch 33.1 vs 30.3 us -- the same VALU work moved onto the rollout waves),
+// with the in-launch final merge and unarmed (armed chains carry the next step's draws).
 static bool gen_now(const srbd_ctx* c) {
-    return c->gen_env && c->ks && !fusable(c) && gen_ok(c->mc, c->mode);
+    if (!c->gen_env || !c->ks || !gen_ok(c->mc, c->mode)) return false;
+    if (c->mode == ROLLOUT_QUAD)
+        return c->gen_quad_min > 0 && !c->arm_mode && c->final_merge && c->mc.n_local >= c->gen_quad_min;
+    return !fusable(c);
 }
 
 // Device-chain steps draw on the device: CEM draws are then unscaled (StepInput::noise_scaled = 0)
@@ -839,7 +847,7 @@ extern "C" int srbd_step(srbd_ctx* c, const float* state, const float* ref, cons
         int buf = 0;
         const bool gen = !noise && gen_now(c);
         if ((r = acquire_noise(c, noise, seed, counter, &buf, gen))) return r;
-        const bool fuse = !noise && fusable(c);
+        const bool fuse = !noise && !gen && fusable(c);
         const Publish pub{c->d_flag, ++c->seq, nullptr};
         seq = pub.seq;
         nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fuse, pub, nullptr, ks ? &ksi : nullptr,
@@ -2005,10 +2013,10 @@ extern "C" int srbd_time_launch(srbd_ctx* c, int32_t which, int32_t iters, float
     c->cur = 0;
     if (int rc = reset_noise_scaled(c)) return rc;
     const ModelConst& mc = c->mc;
-    const bool fuse = fusable(c);
     const bool ks = c->ks && !mc.ga && !mc.cost_on;
     const bool fm = c->final_merge && !mc.ga && !mc.cost_on;
     const bool gen = gen_now(c) && ks;
+    const bool fuse = fusable(c) && !gen;
     StepInputK ksi;
     if (ks) fill_ksi(c, &ksi);
     if (form)
@@ -2374,7 +2382,15 @@ extern "C" int srbd_tamols_run_terrain(srbd_tamols_ctx* t, srbd_terrain* ter, do
     j.yaw_s = sin(yaw);
     j.dist_x = dist_x;
     j.dist_y = dist_y;
+    j.inv_dx = 1.0 / dist_x;
+    j.inv_dy = 1.0 / dist_y;
     j.ray_z = ray_z;
+    // the raycast patch is ray_xy's lattice: nine points per nearest-neighbour query, one block per leg
+    // (SRBD_TAMOLS_LATTICE=0: every point scanned, 16 blocks per leg -- the same results)
+    const char* le = getenv("SRBD_TAMOLS_LATTICE");
+    const bool lattice_env = !(le && le[0] == '0');
+    j.lattice = lattice_env && std::isfinite(dist_x) && std::isfinite(dist_y) && dist_x > 0.0 && dist_y > 0.0 &&
+                std::isfinite(j.yaw_c) && std::isfinite(j.yaw_s);
     j.hm_out = out_hm ? t->d_hm_host : nullptr;
     const int rc = tamols_launch_wait(t, j, seeds, hips, vel, base, contact, feet, p, rows, cols, out_fh, out_box,
                                       out_valid, out_scores, out_seedh);

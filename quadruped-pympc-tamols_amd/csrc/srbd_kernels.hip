@@ -170,7 +170,11 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
 // KS: the host step's input arrives by value (StepInputK, GroupArgs::ksi); block 0 writes it to the device
 // StepInput `in_dev` for the merge and later readers, so the step needs no upload kernel (one dependent launch
 // and a PCIe read fewer).
-template <int KIND, int HT, int ST, bool CEMT, bool EXT, int FM = 0, bool KS = false>
+// GEN (GroupArgs::gen, zero-order H 12 host steps, MPPI, device Philox draws): the launch makes the step's draws
+// itself -- every fourth step each lane the three column quads (its leg's three components) of the next four
+// steps: rng_item's Philox4x32-10 call and Box-Muller pairs, so the same bits.  No noise is read or written: the
+// values stay raw in `pre` as the ZST loads leave them, and the LDS stage feeds the epilogue as before.
+template <int KIND, int HT, int ST, bool CEMT, bool EXT, int FM = 0, bool KS = false, bool GEN = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) rollout_quad_kernel(
                                                            const std::conditional_t<KS, StepInputK, KsNone> ksi,
                                                            const ModelConst mc, const StepInput* __restrict__ in_dev,
@@ -219,6 +223,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     // per block (the launcher's quad block for zero-order).  The group reduction reuses the buffer.  H <= 12:
     // 38.5 KB of LDS per block keeps four blocks per CU (H = 16 would need 51 KB: three).
     constexpr bool ZST = CT && KIND == SRBD_ZERO_ORDER && !EXT && HT <= 12;
+    static_assert(!GEN || (ZST && HT % 4 == 0 && !CEMT), "GEN: the zero-order LDS-staged form, H % 4 == 0");
     constexpr int PCT = ZST ? 12 * HT : 1;
     constexpr int ZSTR = PCT + 1;  // sample stride of the stage: odd, so the epilogue's row-per-lane reads hit 64 banks
     __shared__ __attribute__((aligned(16))) float zst[ZST ? (64 * ZSTR > GROUP_LDS_FLOATS ? 64 * ZSTR : GROUP_LDS_FLOATS) : 1];
@@ -267,6 +272,15 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     float footL[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) footL[q] = st[12 + 3 * lq + q];
+    // ZST: this lane's leg's contact value of every step in registers, loaded once (lane-varying row: one vector
+    // load per step, issued before the horizon), instead of four scalar loads and a 10-instruction lane select
+    // per step
+    constexpr int NCL = ZST ? HT : 1;
+    float clreg[NCL];
+    if constexpr (ZST) {
+#pragma unroll
+        for (int n = 0; n < HT; ++n) clreg[n] = in->contact[lq][n];
+    }
 
     // Specialised shapes: every parameter this lane reads over the horizon (its component's block
     // of each leg) is loaded before the first step, so the horizon chain pays one memory round trip
@@ -323,7 +337,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     // more with the window (H16: 48 -> 144 B at lead 2), so they keep the up-front loads.
     constexpr int CLEAD = 2;
     constexpr bool CWIN = CT && CEMT && KIND == SRBD_CUBIC_SPLINE && ST > 1;
-    if constexpr (CWIN) {
+    if constexpr (GEN) {
+        // nothing to load: the horizon makes the values (gen4)
+    } else if constexpr (CWIN) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) load_slot(i);
     } else if constexpr (CT) {
@@ -338,7 +354,27 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
     }
 
     float dep = p;  // step_ptr dependency: set part-way through each step
+    // GEN: steps 4 s .. 4 s + 3 of component q of this lane's leg are column quad lq PL / 4 + q HT / 4 + s of the row
+    auto gen4 = [&](const int s, auto is) __attribute__((always_inline)) {
+        const int r = mc.row0 + k;
+        const bool live = r > 0 && valid;  // row 0 (the warm start) and the padding rows: zeros, as in the buffer
+        const uint32_t d = (uint32_t)(r - 1);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            uint32_t cc[4] = {d, (uint32_t)(lq * (PL / 4) + q * (HT / 4) + s), is->ctr_lo, is->ctr_hi};
+            philox4x32_10(cc, is->seed_lo, is->seed_hi);
+            float v[4];
+            box_muller(cc[0], cc[1], v[0], v[1]);
+            box_muller(cc[2], cc[3], v[2], v[3]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pre[q][(4 * s + i) % NPRE] = live ? mc.sigma_mppi * v[i] : 0.0f;
+        }
+    };
     auto step = [&](const int n, auto EX) __attribute__((always_inline)) {  // EX: as rollout_kernel
+        // GEN: the key read through a pointer tied to the last step's cost, so the quads are made four steps at a
+        // time, not hoisted to the start (as rollout_kernel's GEN)
+        if constexpr (GEN)
+            if (n % 4 == 0) gen4(n / 4, step_ptr(in, cost));
         if constexpr (CT && PW < NPRE)
             if (n + PW < NPRE) load_slot(n + PW);  // n is a compile-time constant here (unrolled horizon)
         if constexpr (CWIN) {
@@ -353,7 +389,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
         // this step's scalars through step_ptr: loaded per step, not hoisted across the unrolled horizon
         // (hoisted: SGPR spills to VGPR lanes, ~150 v_readlane per step in the cubic CEM kernel)
         const auto is = step_ptr(in, dep);
-        const float cl[4] = {is->contact[0][n], is->contact[1][n], is->contact[2][n], is->contact[3][n]};
+        float cl[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        if constexpr (!ZST)
+#pragma unroll
+            for (int l = 0; l < 4; ++l) cl[l] = is->contact[l][n];
         const float fref = is->fzref[n];
         const float dt = mc.dts[n];
         const float sq = mc.sq[n], somq = mc.somq[n], sa = mc.sa[n], sb = mc.sb[n], scc = mc.sc[n], sd = mc.sd[n];
@@ -365,8 +404,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) r
         if constexpr (LEGP) {
             // this lane's leg's contact value as bit masks (lmask[l] = ~0 on the lanes of leg l): a select chain
             // here became three nested divergent branches, each with its own scalar load and lgkmcnt(0) wait
-            const float clq = __uint_as_float((__float_as_uint(cl[0]) & lmask[0]) | (__float_as_uint(cl[1]) & lmask[1]) |
-                                              (__float_as_uint(cl[2]) & lmask[2]) | (__float_as_uint(cl[3]) & lmask[3]));
+            const float clq = ZST ? clreg[ZST ? n : 0]
+                                  : __uint_as_float((__float_as_uint(cl[0]) & lmask[0]) | (__float_as_uint(cl[1]) & lmask[1]) |
+                                                    (__float_as_uint(cl[2]) & lmask[2]) | (__float_as_uint(cl[3]) & lmask[3]));
             const int lbase = lq * PL;
             // component q of this leg's decoded force (slot i, parameter j of the leg when not prefetched)
             auto PQ = [&](int q, int i, int j) {
@@ -2008,6 +2048,14 @@ static void launch_rollout_t(const ModelConst& mc, const StepInput* in, const fl
         const dim3 grid(blocks + extra * 256 / threads);
         if constexpr (KIND == SRBD_ZERO_ORDER && (HT == 10 || HT == 12) && !EXT) {
             if (!cem && grp.ksi) {  // ks_ok: the step input as a kernel argument
+                if constexpr (HT == 12) {
+                    if (grp.gen && grp.out && !grp.xa && !next) {  // gen_ok: the launch makes the step's draws
+                        hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, 1, true, true>), grid,
+                                           dim3(threads), 0, s, *static_cast<const StepInputK*>(grp.ksi), mc, in,
+                                           noise, costs, recs, rec_stride, job, blocks, grp);
+                        return;
+                    }
+                }
                 if (grp.out && grp.xa)
                     hipLaunchKernelGGL((rollout_quad_kernel<KIND, HT, ST, false, false, 2, true>), grid, dim3(threads),
                                        0, s, *static_cast<const StepInputK*>(grp.ksi), mc, in, noise, costs, recs, rec_stride, job, blocks, grp);

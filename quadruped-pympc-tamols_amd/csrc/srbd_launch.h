@@ -226,8 +226,10 @@ constexpr int TAMOLS_LDS_PRIMS = 1024;  // scenes up to this many primitives are
 struct TamolsJob {
     TamolsArgs a;
     int use_terrain;     // 1: raycast the patches from `t` (centres = the seeds), 0: read `hm`
+    int lattice;         // use_terrain with dist_x, dist_y > 0: the patch is a lattice (one block per leg)
     TerrainDev t;
     double yaw_c, yaw_s, dist_x, dist_y, ray_z;
+    double inv_dx, inv_dy;  // 1 / dist_x, 1 / dist_y (the lattice queries)
     int rows, cols;
     const double* hm;    // 4 x nc x 3 (device-visible) when !use_terrain
     double* hm_out;      // 4 x nc x 3 raycast patches or NULL

@@ -339,8 +339,8 @@ static void launch_thread_t(const ModelConst& mc, const StepInput* in, const flo
 // The launch can make the step's draws itself (GroupArgs::gen); the caller also needs device draws (no injected
 // noise) and no next-step draws in the launch.
 bool gen_ok(const ModelConst& mc, int mode) {
-    return mode == ROLLOUT_THREAD && mc.kind == SRBD_ZERO_ORDER && mc.H == 12 && mc.method == SRBD_MPPI &&
-           mc.rng == RNG_PHILOX && !mc.ga && !mc.cost_on && mc.P % 4 == 0;
+    return (mode == ROLLOUT_THREAD || mode == ROLLOUT_QUAD) && mc.kind == SRBD_ZERO_ORDER && mc.H == 12 &&
+           mc.method == SRBD_MPPI && mc.rng == RNG_PHILOX && !mc.ga && !mc.cost_on && mc.P % 4 == 0;
 }
 
 void launch_rollout_thread(const ModelConst& mc, const StepInput* in, const float* noise, float* costs, float* recs,

@@ -77,6 +77,44 @@ __device__ __forceinline__ void tamols_query_part(const TamolsArgs& a, int leg, 
     }
 }
 
+// The same query on a raycast patch (TamolsJob::lattice): the patch points are ray_xy's rows x cols lattice about
+// the seed (spacing dist_x, dist_y, rotated by the yaw), so the nearest point is the per-axis nearest lattice row
+// and column (the squared distance separates in the lattice frame; clamped for a query off the patch).  Only the
+// 3 x 3 points about that one are scanned, in index order with strict < as the whole scan does: every point
+// outside them is farther by >= 2 spacings^2, so the first nearest point -- ties included -- is among them and the
+// height is the full scan's bit for bit.
+__device__ __forceinline__ double tamols_query_lattice(const TamolsJob& j, int leg, int t, const double* px,
+                                                       const double* py, const double* pz) {
+    const TamolsArgs& a = j.a;
+    double qx, qy;
+    tamols_query_point(a, leg, t, px, py, qx, qy);
+    const double ex = qx - a.seeds[3 * leg], ey = qy - a.seeds[3 * leg + 1];
+    // the window's centre needs no exact rounding (the 3 x 3 window absorbs an off-by-one): reciprocals, not divides
+    const double u = (j.yaw_c * ex + j.yaw_s * ey) * j.inv_dx + (double)(j.rows - 1) * 0.5;
+    const double v = (j.yaw_c * ey - j.yaw_s * ex) * j.inv_dy + (double)(j.cols - 1) * 0.5;
+    // fmax / fmin return the number when the other operand is NaN (a NaN query: no point is nearer, as in the scan)
+    const int i0 = (int)fmin(fmax(floor(u + 0.5), 0.0), (double)(j.rows - 1));
+    const int k0 = (int)fmin(fmax(floor(v + 0.5), 0.0), (double)(j.cols - 1));
+    double bd = INFINITY, bh = 0.0;
+#pragma unroll
+    for (int di = -1; di <= 1; ++di) {
+        const int i = i0 + di;
+#pragma unroll
+        for (int dk = -1; dk <= 1; ++dk) {
+            const int k = k0 + dk;
+            if (i < 0 || i >= j.rows || k < 0 || k >= j.cols) continue;
+            const int idx = i * j.cols + k;
+            const double dx = qx - px[idx], dy = qy - py[idx];
+            const double d2 = dx * dx + dy * dy;
+            if (d2 < bd) {
+                bd = d2;
+                bh = pz[idx];
+            }
+        }
+    }
+    return bh;
+}
+
 // Score of candidate (cx, cy) with its query heights h[0..NQ) (VFA:192-222): INFINITY when a hard
 // constraint fails.
 __device__ __forceinline__ double tamols_score(const TamolsArgs& a, int leg, double cx, double cy,
@@ -175,8 +213,12 @@ __device__ __forceinline__ double tamols_score(const TamolsArgs& a, int leg, dou
            stab * p.w_stability;
 }
 
-constexpr int TAMOLS_SLICE = (TAMOLS_MAXCAND + TAMOLS_BPL - 1) / TAMOLS_BPL;  // candidates per block, max
+// candidates per block, max: every candidate when a leg runs in one block (TamolsJob::lattice)
+constexpr int TAMOLS_SLICE = TAMOLS_MAXCAND;
 static_assert(TAMOLS_BPL <= 64, "the merge loads one slice partial per lane of one wave");
+
+__device__ void tamols_leg_out(const TamolsJob& j, int leg, int bi, const double* px, const double* py, double bh,
+                               double seedh);
 
 __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const TamolsJob j) {
     __shared__ double px[TAMOLS_MAXCAND], py[TAMOLS_MAXCAND], pz[TAMOLS_MAXCAND];
@@ -265,7 +307,10 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
     // ---- phase A: this block's candidates [c0, c1), their queries (+ the seed on block 0)
     const int c0 = (int)((long)b * nc / NB), c1 = (int)((long)(b + 1) * nc / NB);
     const int nown = (c1 - c0) * TAMOLS_NQ, nloc = nown + (b == 0 ? 1 : 0);
-    {
+    if (j.lattice) {  // a raycast lattice patch: nine points per query
+        for (int t = tid; t < nloc; t += T)
+            nn[t] = tamols_query_lattice(j, leg, t < nown ? c0 * TAMOLS_NQ + t : nc * TAMOLS_NQ, px, py, pz) + 0.02;
+    } else {
         // Q lanes per query (aligned groups of Q consecutive lanes), each scanning a contiguous quarter of the
         // patch; the groups' (d2, first index) minima combine lowest-part-first, so the first nearest point of
         // the whole patch wins exactly as in one serial scan
@@ -303,6 +348,40 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
     TAM_STAMP(3);
 
     // ---- phase C: the slice's strict-< argmin, then the leg's last block merges the slices in order
+    if (NB == 1) {  // the leg in one block: a parallel argmin -- (score, index) of the scores < INFINITY, the lower
+                    // index on equal scores, so the first minimum wins as in the sequential strict-< scan (NaN and
+                    // INFINITY never do: bi stays -1)
+        double bs = INFINITY;
+        int bi = 0x7fffffff;
+        for (int c = tid; c < nc; c += T)
+            if (sc[c] < bs) {  // strided and increasing: a later equal score never replaces
+                bs = sc[c];
+                bi = c;
+            }
+        for (int m = 32; m >= 1; m >>= 1) {
+            const double os = __shfl_xor(bs, m, 64);
+            const int oi = __shfl_xor(bi, m, 64);
+            if (os < bs || (os == bs && oi < bi)) {
+                bs = os;
+                bi = oi;
+            }
+        }
+        if ((tid & 63) == 0) {
+            rbest[tid >> 6] = bs;
+            rhit[tid >> 6] = bi;
+        }
+        __syncthreads();
+        if (tid != 0) return;
+        TAM_STAMP(4);
+        for (int w = 1; w < (T + 63) / 64; ++w)
+            if (rbest[w] < bs || (rbest[w] == bs && rhit[w] < bi)) {
+                bs = rbest[w];
+                bi = rhit[w];
+            }
+        tamols_leg_out(j, leg, bs < INFINITY ? bi : -1, px, py, bs < INFINITY ? nn[bi * TAMOLS_NQ] : 0.0, nn[nloc - 1]);
+        TAM_STAMP(5);
+        return;
+    }
     if (tid == 0) {
         int bi = -1;
         double bs = INFINITY;
@@ -349,6 +428,17 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
     }
     const double seedh = __shfl(pseed, 0);
     if (tid != 0) return;
+    __hip_atomic_store(j.cnt + leg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next call
+    tamols_leg_out(j, leg, bi, px, py, bh, seedh);
+    TAM_STAMP(5);
+#undef TAM_STAMP
+}
+
+// The leg's outputs (one lane): foothold, box and validity of candidate bi (-1: none feasible), its query height bh,
+// the seed height; then the leg publishes the call's sequence number on its own host word.
+__device__ void tamols_leg_out(const TamolsJob& j, int leg, int bi, const double* px, const double* py, double bh,
+                               double seedh) {
+    const TamolsArgs& a = j.a;
     const srbd_tamols_params& p = a.p;
     double* F = j.out + 3 * leg;  // [fh 12 | box 24 | seedh 4 | valid 4 x int32]
     double* B = j.out + 12 + 6 * leg;
@@ -373,12 +463,9 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
         valid[leg] = 0;
     }
     j.out[36 + leg] = seedh;
-    __hip_atomic_store(j.cnt + leg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next call
-    __threadfence_system();  // this leg's host-mapped outputs (and, fenced before the count, its blocks' scores)
+    __threadfence_system();  // this leg's host-mapped outputs and its blocks' scores / patch (drained before)
     // the leg publishes on its own word: the host waits for all four (no cross-leg counter round trip)
     __hip_atomic_store(j.flag + leg, j.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    TAM_STAMP(5);
-#undef TAM_STAMP
 }
 
 // Once per TAMOLS context (srbd_tamols_create, on its device): the staged scene needs up to
@@ -392,7 +479,8 @@ int tamols_prepare() {
 }
 
 void launch_tamols_fused(const TamolsJob& j, hipStream_t s) {
-    const int nb = j.a.ncand < TAMOLS_BPL ? j.a.ncand : TAMOLS_BPL;
+    // a raycast lattice patch: one block per leg (nine points per query, no cross-block merge)
+    const int nb = j.lattice ? 1 : (j.a.ncand < TAMOLS_BPL ? j.a.ncand : TAMOLS_BPL);
     const int np = j.use_terrain ? j.t.nprims : 0;
     const size_t smem = (np > 0 && np <= TAMOLS_LDS_PRIMS) ? (sizeof(srbd_terrain_prim) + 2 * sizeof(double)) * np : 0;
     hipLaunchKernelGGL(tamols_fused_kernel, dim3(nb, 4), dim3(TAMOLS_THREADS), smem, s, j);

@@ -38,7 +38,8 @@ for k in range(n + 10):
         acc += out
         raw = np.zeros(4 * 64 * 8, np.uint64)  # block 0 of leg 0: start, staged, walked, patch done
         _lib.lib.srbd_tamols_phases_raw(srch.h, raw.ctypes.data)
-        st = raw.reshape(4 * 64, 8)[: 4 * 16].astype(np.float64)  # 4 legs x TAMOLS_BPL (16) blocks
+        st = raw.reshape(4 * 64, 8).astype(np.float64)
+        st = st[st[:, 0] > 0]  # the blocks of this call's legs (16 per leg, or one on a lattice patch)
         t0b = st[:, 0].min()
         skew += np.array([st[:, 0].max() - t0b, np.median(st[:, 0]) - t0b, st[:, 4].max() - t0b,
                           st[:, 5].max() - t0b]) * 0.01

@@ -47,15 +47,22 @@ def test_regenerated_draws_equal_read_draws(lib, wkey, N, H):
 
 
 @pytest.mark.parametrize("wkey,N,rg", [("c5", 524288, None), ("c2", 300001, None), ("c5", 524288, "0"),
-                                       ("c5", 524288, "36")])
+                                       ("c5", 524288, "36"),
+                                       # the four-lane form (rollout_quad_kernel GEN): the north-star shape and a
+                                       # ragged last block; its draws stay in registers and the LDS stage
+                                       ("c2", 65536, None), ("c2", 40001, None)])
 def test_in_launch_draws_equal_rng_launch(lib, monkeypatch, wkey, N, rg):
     """Host steps whose rollout launch makes the step's draws itself (gen_now: thread form, zero-order H 12, MPPI,
     device Philox; the horizon stores the quads the epilogue reads back) against the same steps with the RNG launch
-    writing them first (SRBD_GEN=0; the rollout reads them, the epilogue regenerates REGEN_QUADS of them): bit for
+    writing them first (SRBD_GEN=0; the rollout reads them, the epilogue regenerates REGEN_QUADS of them), and the
+    opt-in four-lane form (SRBD_GEN_QUAD_MIN; each lane makes its leg's three quads every fourth step; no noise
+    stored): bit for
     bit over three warm-started steps, costs included.  rg: SRBD_GEN_RG, the quads the epilogue regenerates
     (default GEN_REGEN_QUADS; 0: every quad stored and read back; 36: none stored).  N = 300 001: padding rows
     past n_local in the last block (zeros in the buffer, zeros generated)."""
     case = make_case(wkey, N=N, method="mppi", par="zero_order", H=12, seed=N % 83)
+    if N <= 65536:  # the four-lane GEN form is opt-in
+        monkeypatch.setenv("SRBD_GEN_QUAD_MIN", "1")
     monkeypatch.setenv("SRBD_GEN", "0")
     ref = lib.Context(product_cfg(case))
     monkeypatch.delenv("SRBD_GEN")
@@ -63,6 +70,7 @@ def test_in_launch_draws_equal_rng_launch(lib, monkeypatch, wkey, N, rg):
         monkeypatch.setenv("SRBD_GEN_RG", rg)
     gen = lib.Context(product_cfg(case))
     monkeypatch.delenv("SRBD_GEN_RG", raising=False)
+    monkeypatch.delenv("SRBD_GEN_QUAD_MIN", raising=False)
     try:
         bg, br = case["best"].copy(), case["best"].copy()
         for k in range(3):

@@ -151,3 +151,46 @@ def test_large_scene_fused_tamols(lib, n_box, n_cyl):
     finally:
         s.close()
         ter.close()
+
+
+@pytest.mark.parametrize("yaw", [0.0, 0.4, math.pi / 2, -2.3])
+def test_lattice_queries_equal_full_scan(lib, monkeypatch, yaw):
+    """The raycast patch's nearest-neighbour queries on the lattice (nine points per query, one block per leg)
+    against every point scanned (SRBD_TAMOLS_LATTICE=0, 16 blocks per leg): every output bit-equal, with hips on
+    half-lattice points (exact ties between two patch points: the first index wins both ways) and hips off the
+    patch (queries clamped to its edge)."""
+    from quadruped_pympc_amd import config
+    from quadruped_pympc_amd.helpers.terrain import GpuTerrain
+    from quadruped_pympc_amd.helpers.visual_foothold_adaptation import TamolsSearch, tamols_params_struct
+
+    ter = GpuTerrain.stepping_stones()
+    s = TamolsSearch(0)
+    rng = np.random.default_rng(int(1000 * abs(yaw)) + 3)
+    params = dict(config.simulation_params["tamols_params"])
+    params["h_des"] = 0.25
+    ps = tamols_params_struct(params, "go2")
+    c, sn = math.cos(yaw), math.sin(yaw)
+    try:
+        for trial in range(6):
+            feet = np.array([[1.22, 0.13, 0.05], [1.22, -0.13, 0.05], [0.84, 0.13, 0.05], [0.84, -0.13, 0.05]])
+            feet[:, :2] += rng.uniform(-0.3, 0.3, 2)
+            seeds = feet + np.array([0.12, 0.02, 0.0])
+            # hips at (half-)lattice offsets from the seed in the patch frame, or far off the patch
+            du, dv = rng.integers(-8, 9, 4) * 0.02, rng.integers(-8, 9, 4) * 0.02
+            if trial % 3 == 2:
+                du = du * 10.0
+            hips = seeds.copy()
+            hips[:, 0] += c * du - sn * dv
+            hips[:, 1] += sn * du + c * dv
+            hips[:, 2] += 0.3
+            kw = dict(forward_vel=np.array([0.5, 0.1, 0.0]), base_position=feet.mean(0) + [0, 0, 0.3],
+                      current_contact=np.array([0, 1, 1, 0], np.int32), current_feet_pos=feet)
+            a = s.run_terrain(ter, yaw, seeds, hips, ps, **kw)
+            monkeypatch.setenv("SRBD_TAMOLS_LATTICE", "0")
+            b = s.run_terrain(ter, yaw, seeds, hips, ps, **kw)
+            monkeypatch.delenv("SRBD_TAMOLS_LATTICE")
+            for k in ("footholds", "boxes", "valid", "scores", "seed_heights", "heightmaps"):
+                np.testing.assert_array_equal(a[k], b[k], err_msg=f"{k} trial {trial}")
+    finally:
+        s.close()
+        ter.close()
