@@ -2385,7 +2385,7 @@ extern "C" int srbd_tamols_run_terrain(srbd_tamols_ctx* t, srbd_terrain* ter, do
     j.inv_dx = 1.0 / dist_x;
     j.inv_dy = 1.0 / dist_y;
     j.ray_z = ray_z;
-    // the raycast patch is ray_xy's lattice: nine points per nearest-neighbour query, one block per leg
+    // the raycast patch is ray_xy's lattice: four points per nearest-neighbour query, one block per leg
     // (SRBD_TAMOLS_LATTICE=0: every point scanned, 16 blocks per leg -- the same results)
     const char* le = getenv("SRBD_TAMOLS_LATTICE");
     const bool lattice_env = !(le && le[0] == '0');

@@ -27,9 +27,14 @@
 typedef int (*iface_fn_t)(srbd_ctx*, srbd_interface_io*, const float*, const double*, int32_t, float*, int32_t,
                           float*, srbd_result*);
 typedef int (*pgg_seq_fn_t)(srbd_pgg*, const double*, const int32_t*, int32_t, double*, int32_t);
+typedef int (*foothold_fn_t)(srbd_tamols_ctx*, srbd_terrain*, const srbd_tamols_params*, srbd_ctx*, srbd_foothold_io*,
+                             const float*, int32_t, float*, int32_t, uint64_t, uint64_t, srbd_result*);
+typedef int (*split_fn_t)(const uint32_t*, int32_t, int32_t, uint32_t*);
 
 static iface_fn_t g_iface;
 static pgg_seq_fn_t g_pgg_seq;
+static foothold_fn_t g_foothold;
+static split_fn_t g_split;
 
 static const char* const STATE_KEYS[8] = {"position", "linear_velocity", "orientation", "angular_velocity",
                                           "foot_FL",  "foot_FR",         "foot_RL",     "foot_RR"};
@@ -40,13 +45,15 @@ static PyObject* k_state[8];
 static PyObject* k_ref[8];
 static PyObject* k_zero;  /* the int 0 (ref_foot_*[0]) */
 
-/* bind(interface_step_address, pgg_contact_sequence_address) */
+/* bind(srbd_interface_step, srbd_pgg_contact_sequence, srbd_foothold_mpc_step, srbd_jax_split addresses) */
 static PyObject* bind(PyObject* self, PyObject* args) {
-    unsigned long long a, b;
+    unsigned long long a, b, c, d;
     (void)self;
-    if (!PyArg_ParseTuple(args, "KK", &a, &b)) return NULL;
+    if (!PyArg_ParseTuple(args, "KKKK", &a, &b, &c, &d)) return NULL;
     g_iface = (iface_fn_t)(uintptr_t)a;
     g_pgg_seq = (pgg_seq_fn_t)(uintptr_t)b;
+    g_foothold = (foothold_fn_t)(uintptr_t)c;
+    g_split = (split_fn_t)(uintptr_t)d;
     Py_RETURN_NONE;
 }
 
@@ -261,8 +268,192 @@ fail:
     return NULL;
 }
 
+static PyObject* k_legs[4];  /* "FL" .. "RR" (LegsAttr attributes) */
+
+/* Three float64 values of an attribute / item (a C-contiguous float64 ndarray of >= 3 values). */
+static int get3_arr(PyObject* v, double* dst) {
+    if (!v || !PyArray_Check(v)) return 0;
+    PyArrayObject* a = (PyArrayObject*)v;
+    if (PyArray_TYPE(a) != NPY_FLOAT64 || PyArray_SIZE(a) < 3 || !PyArray_IS_C_CONTIGUOUS(a)) return 0;
+    memcpy(dst, PyArray_DATA(a), 3 * sizeof(double));
+    return 1;
+}
+static int get_legs(PyObject* legs, double* dst) {  /* a LegsAttr's FL FR RL RR rows -> dst[12] */
+    for (int l = 0; l < 4; ++l) {
+        PyObject* v = PyObject_GetAttr(legs, k_legs[l]);
+        if (!v) {
+            PyErr_Clear();
+            return 0;
+        }
+        const int ok = get3_arr(v, dst + 3 * l);
+        Py_DECREF(v);
+        if (!ok) return 0;
+    }
+    return 1;
+}
+
+/* foothold_step(tamols, terrain, params, ctx, io, state, ref_base, seeds, hips, base_lin_vel, base_ori, contact_sequence,
+ *               best, previous_contact, master_key, calls, best_buf, contact_buf, result, params_per_leg, rng)
+ * helpers/foothold_pipeline.py TamolsMpcStep._step_fused's staging and its one srbd_foothold_mpc_step call (the
+ * key split of compute_control's with_newkey included):
+ * -> None (an input form not handled here: nothing touched), or
+ *    (rc, stage, current_contact, master_key, calls) when a call of the chain failed, or
+ *    (0, 3, current_contact, master_key, calls, grf (4, 3) float64, predicted_state (24,) float32, best (P,) float32) */
+static PyObject* foothold_step(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+    (void)self;
+    if (nargs != 21) {
+        PyErr_SetString(PyExc_TypeError, "foothold_step takes 21 arguments");
+        return NULL;
+    }
+    if (!g_foothold || !g_split) {
+        PyErr_SetString(PyExc_RuntimeError, "_srbd_fast: bind() first");
+        return NULL;
+    }
+    srbd_tamols_ctx* tam = (srbd_tamols_ctx*)addr_of(args[0]);
+    srbd_terrain* ter = (srbd_terrain*)addr_of(args[1]);
+    const srbd_tamols_params* prm = (const srbd_tamols_params*)addr_of(args[2]);
+    srbd_ctx* ctx = (srbd_ctx*)addr_of(args[3]);
+    srbd_foothold_io* io = (srbd_foothold_io*)addr_of(args[4]);
+    srbd_result* res = (srbd_result*)addr_of(args[18]);
+    const int ppl = (int)PyLong_AsLong(args[19]), rng = (int)PyLong_AsLong(args[20]);
+    const long long calls = PyLong_AsLongLong(args[15]);
+    if (PyErr_Occurred()) return NULL;
+    PyObject *state = args[5], *refb = args[6], *cs = args[11], *best = args[12], *prev = args[13], *mk = args[14];
+    PyObject *best_buf = args[16], *contact_buf = args[17];
+
+    /* ---- validate and gather */
+    double st[24], rb[12], sd[12], hp[12], fv[3], yaw;
+    for (int i = 0; i < 8; ++i)
+        if (!get3(state, k_state[i], st + 3 * i, NULL)) goto decline;
+    for (int i = 0; i < 4; ++i)
+        if (!get3(refb, k_ref[i], rb + 3 * i, NULL)) goto decline;
+    if (!get_legs(args[7], sd) || !get_legs(args[8], hp) || !get3_arr(args[9], fv)) goto decline;
+    {
+        PyObject* o = args[10];
+        if (!PyArray_Check(o) || PyArray_TYPE((PyArrayObject*)o) != NPY_FLOAT64 ||
+            PyArray_SIZE((PyArrayObject*)o) < 3 || !PyArray_IS_C_CONTIGUOUS((PyArrayObject*)o))
+            goto decline;
+        yaw = ((const double*)PyArray_DATA((PyArrayObject*)o))[2];
+    }
+    if (!PyArray_Check(cs)) goto decline;
+    PyArrayObject* ca = (PyArrayObject*)cs;
+    if (!PyArray_Check(contact_buf) || PyArray_TYPE((PyArrayObject*)contact_buf) != NPY_FLOAT32 ||
+        PyArray_NDIM((PyArrayObject*)contact_buf) != 2 || !PyArray_IS_C_CONTIGUOUS((PyArrayObject*)contact_buf)) {
+        PyErr_SetString(PyExc_TypeError, "contact_buf: float32 (4, H)");
+        return NULL;
+    }
+    const int H = (int)PyArray_DIM((PyArrayObject*)contact_buf, 1);
+    if (PyArray_NDIM(ca) != 2 || PyArray_DIM(ca, 0) != 4 || PyArray_DIM(ca, 1) < H || !PyArray_IS_C_CONTIGUOUS(ca) ||
+        PyArray_TYPE(ca) != NPY_FLOAT64)
+        goto decline;
+    if (!PyArray_Check(best_buf) || PyArray_TYPE((PyArrayObject*)best_buf) != NPY_FLOAT32 ||
+        !PyArray_IS_C_CONTIGUOUS((PyArrayObject*)best_buf)) {
+        PyErr_SetString(PyExc_TypeError, "best_buf: float32 C-contiguous");
+        return NULL;
+    }
+    const npy_intp P = PyArray_SIZE((PyArrayObject*)best_buf);
+    PyArrayObject* b = (PyArrayObject*)PyArray_FROM_OTF(best, NPY_FLOAT32, NPY_ARRAY_IN_ARRAY | NPY_ARRAY_FORCECAST);
+    if (!b) return NULL;
+    PyArrayObject* pv = (PyArrayObject*)PyArray_FROM_OTF(prev, NPY_FLOAT64, NPY_ARRAY_IN_ARRAY | NPY_ARRAY_FORCECAST);
+    if (!pv) {
+        Py_DECREF(b);
+        return NULL;
+    }
+    const int philox = rng == SRBD_RNG_PHILOX;
+    PyArrayObject* kk = (PyArrayObject*)PyArray_FROM_OTF(mk, philox ? NPY_UINT64 : NPY_UINT32,
+                                                         NPY_ARRAY_IN_ARRAY | NPY_ARRAY_FORCECAST);
+    if (!kk) {
+        Py_DECREF(b);
+        Py_DECREF(pv);
+        return NULL;
+    }
+    if (PyArray_SIZE(b) != P || PyArray_SIZE(pv) != 4 || PyArray_SIZE(kk) != 2) {
+        Py_DECREF(b);
+        Py_DECREF(pv);
+        Py_DECREF(kk);
+        goto decline;
+    }
+
+    /* ---- staging (as _step_fused) and the key split of with_newkey */
+    memcpy(io->state_in, st, sizeof(st));
+    memcpy(io->ref_base, rb, sizeof(rb));
+    memcpy(io->seeds, sd, sizeof(sd));
+    memcpy(io->hips, hp, sizeof(hp));
+    memcpy(io->forward_vel, fv, sizeof(fv));
+    const double* cd = (const double*)PyArray_DATA(ca);
+    const npy_intp cstr = PyArray_DIM(ca, 1);
+    for (int l = 0; l < 4; ++l) io->current_contact[l] = cd[(size_t)l * cstr];
+    memcpy(io->previous_contact, PyArray_DATA(pv), 4 * sizeof(double));
+    Py_DECREF(pv);
+    io->yaw = yaw;
+    float* cf = (float*)PyArray_DATA((PyArrayObject*)contact_buf);
+    for (int l = 0; l < 4; ++l)
+        for (int k = 0; k < H; ++k) cf[l * H + k] = (float)cd[(size_t)l * cstr + k];
+    float* bb = (float*)PyArray_DATA((PyArrayObject*)best_buf);
+    memcpy(bb, PyArray_DATA(b), sizeof(float) * (size_t)P);
+    Py_DECREF(b);
+    uint64_t seed, counter, nk0, nk1;
+    if (philox) {
+        const uint64_t* k = (const uint64_t*)PyArray_DATA(kk);
+        nk0 = k[0];
+        nk1 = k[1] + 1;
+        seed = nk0;
+        counter = nk1;
+    } else {
+        const uint32_t* k = (const uint32_t*)PyArray_DATA(kk);
+        uint32_t o[4];
+        g_split(k, 2, rng == SRBD_RNG_JAX ? 1 : 0, o);
+        nk0 = o[0];
+        nk1 = o[1];
+        seed = ((uint64_t)o[0] << 32) | o[1];
+        counter = (uint64_t)calls + 1;
+    }
+    Py_DECREF(kk);
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = g_foothold(tam, ter, prm, ctx, io, cf, H, bb, ppl, seed, counter, res);
+    Py_END_ALLOW_THREADS
+    PyObject* cur = new_1d(NPY_FLOAT64, 4, io->current_contact, sizeof(double));
+    PyObject* nk;
+    if (philox) {
+        const uint64_t k2[2] = {nk0, nk1};
+        nk = new_1d(NPY_UINT64, 2, k2, sizeof(uint64_t));
+    } else {
+        const uint32_t k2[2] = {(uint32_t)nk0, (uint32_t)nk1};
+        nk = new_1d(NPY_UINT32, 2, k2, sizeof(uint32_t));
+    }
+    if (!cur || !nk) {
+        Py_XDECREF(cur);
+        Py_XDECREF(nk);
+        return NULL;
+    }
+    const long long ncalls = philox ? calls : calls + 1;
+    if (rc != 0) return Py_BuildValue("(iiNNL)", rc, io->stage, cur, nk, ncalls);
+    npy_intp d43[2] = {4, 3};
+    PyObject* grf = PyArray_SimpleNew(2, d43, NPY_FLOAT64);
+    PyObject* pred = new_1d(NPY_FLOAT32, 24, res->predicted_state, sizeof(float));
+    PyObject* nb = new_1d(NPY_FLOAT32, P, bb, sizeof(float));
+    if (!grf || !pred || !nb) {
+        Py_XDECREF(grf);
+        Py_XDECREF(pred);
+        Py_XDECREF(nb);
+        Py_DECREF(cur);
+        Py_DECREF(nk);
+        return NULL;
+    }
+    double* g = (double*)PyArray_DATA((PyArrayObject*)grf);
+    for (int l = 0; l < 4; ++l)
+        for (int c = 0; c < 3; ++c) g[3 * l + c] = (double)res->grf[3 * l + c] * io->current_contact[l];
+    return Py_BuildValue("(iiNNLNNN)", 0, io->stage, cur, nk, ncalls, grf, pred, nb);
+decline:
+    if (PyErr_Occurred()) return NULL;
+    Py_RETURN_NONE;
+}
+
 static PyMethodDef methods[] = {
-    {"bind", bind, METH_VARARGS, "bind(interface_step_address, pgg_contact_sequence_address)"},
+    {"foothold_step", (PyCFunction)(void (*)(void))foothold_step, METH_FASTCALL,
+     "TamolsMpcStep's one-call step through srbd_foothold_mpc_step"},
+    {"bind", bind, METH_VARARGS, "bind(the library's entry point addresses)"},
     {"pgg_contact_sequence", (PyCFunction)(void (*)(void))pgg_contact_sequence, METH_FASTCALL,
      "pgg_contact_sequence(pgg_address, dts, lens) -> (4, cols) float64"},
     {"interface_step", (PyCFunction)(void (*)(void))interface_step, METH_FASTCALL,
@@ -278,6 +469,9 @@ PyMODINIT_FUNC PyInit__srbd_fast(void) {
         k_ref[i] = PyUnicode_InternFromString(REF_KEYS[i]);
         if (!k_state[i] || !k_ref[i]) return NULL;
     }
+    static const char* const legs[4] = {"FL", "FR", "RL", "RR"};
+    for (int l = 0; l < 4; ++l)
+        if (!(k_legs[l] = PyUnicode_InternFromString(legs[l]))) return NULL;
     k_zero = PyLong_FromLong(0);
     if (!k_zero) return NULL;
     return PyModule_Create(&moddef);

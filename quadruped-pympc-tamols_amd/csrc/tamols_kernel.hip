@@ -78,32 +78,32 @@ __device__ __forceinline__ void tamols_query_part(const TamolsArgs& a, int leg, 
 }
 
 // The same query on a raycast patch (TamolsJob::lattice): the patch points are ray_xy's rows x cols lattice about
-// the seed (spacing dist_x, dist_y, rotated by the yaw), so the nearest point is the per-axis nearest lattice row
-// and column (the squared distance separates in the lattice frame; clamped for a query off the patch).  Only the
-// 3 x 3 points about that one are scanned, in index order with strict < as the whole scan does: every point
-// outside them is farther by >= 2 spacings^2, so the first nearest point -- ties included -- is among them and the
-// height is the full scan's bit for bit.
+// the seed (spacing dist_x, dist_y, rotated by the yaw), so the squared distance separates in the lattice frame and
+// the nearest point is the per-axis nearest row and column -- one of the two lattice lines bracketing the query's
+// coordinate on each axis (clamped to the patch for a query off it; the bracket holds both lines of an exact tie).
+// Only those 2 x 2 points are scanned, in index order with strict < as the whole scan does, so the first nearest
+// point wins and the height is the full scan's bit for bit (the frame coordinate is computed with reciprocals: an
+// error far below half a spacing moves no bracket off the nearest line).
 __device__ __forceinline__ double tamols_query_lattice(const TamolsJob& j, int leg, int t, const double* px,
                                                        const double* py, const double* pz) {
     const TamolsArgs& a = j.a;
     double qx, qy;
     tamols_query_point(a, leg, t, px, py, qx, qy);
     const double ex = qx - a.seeds[3 * leg], ey = qy - a.seeds[3 * leg + 1];
-    // the window's centre needs no exact rounding (the 3 x 3 window absorbs an off-by-one): reciprocals, not divides
     const double u = (j.yaw_c * ex + j.yaw_s * ey) * j.inv_dx + (double)(j.rows - 1) * 0.5;
     const double v = (j.yaw_c * ey - j.yaw_s * ex) * j.inv_dy + (double)(j.cols - 1) * 0.5;
-    // fmax / fmin return the number when the other operand is NaN (a NaN query: no point is nearer, as in the scan)
-    const int i0 = (int)fmin(fmax(floor(u + 0.5), 0.0), (double)(j.rows - 1));
-    const int k0 = (int)fmin(fmax(floor(v + 0.5), 0.0), (double)(j.cols - 1));
+    // the lower bracketing line, clamped so the pair stays on the patch; fmax / fmin return the number when the
+    // other operand is NaN (a NaN query: no point is nearer, as in the scan)
+    const int i0 = (int)fmin(fmax(floor(u), 0.0), (double)(j.rows > 1 ? j.rows - 2 : 0));
+    const int k0 = (int)fmin(fmax(floor(v), 0.0), (double)(j.cols > 1 ? j.cols - 2 : 0));
+    const int ni = j.rows > 1 ? 2 : 1, nk = j.cols > 1 ? 2 : 1;
     double bd = INFINITY, bh = 0.0;
 #pragma unroll
-    for (int di = -1; di <= 1; ++di) {
-        const int i = i0 + di;
+    for (int di = 0; di < 2; ++di) {
 #pragma unroll
-        for (int dk = -1; dk <= 1; ++dk) {
-            const int k = k0 + dk;
-            if (i < 0 || i >= j.rows || k < 0 || k >= j.cols) continue;
-            const int idx = i * j.cols + k;
+        for (int dk = 0; dk < 2; ++dk) {
+            if (di >= ni || dk >= nk) continue;
+            const int idx = (i0 + di) * j.cols + k0 + dk;
             const double dx = qx - px[idx], dy = qy - py[idx];
             const double d2 = dx * dx + dy * dy;
             if (d2 < bd) {
@@ -115,16 +115,16 @@ __device__ __forceinline__ double tamols_query_lattice(const TamolsJob& j, int l
     return bh;
 }
 
-// Score of candidate (cx, cy) with its query heights h[0..NQ) (VFA:192-222): INFINITY when a hard
-// constraint fails.
-__device__ __forceinline__ double tamols_score(const TamolsArgs& a, int leg, double cx, double cy,
-                                               const double* h) {
+// Score of candidate (cx, cy) with its query heights h[0..NQ) (VFA:192-222): INFINITY when a hard constraint
+// fails.  In four parts, so four waves can form them at once (tamols_score_part); tamols_score is their serial
+// composition, the same float64 operations in the same order.
+//   part 0: the hard constraints (kinematic reach VFA:375-395, leg collision VFA:397-420): 0.0 or INFINITY
+//   part 1: edge (VFA:422-466)   part 2: roughness (VFA:468-521)   part 3: deviation, nominal, tracking, stability
+// and tamols_combine sums the weighted terms in the reference's order.
+__device__ __forceinline__ double tamols_part_hard(const TamolsArgs& a, int leg, double cx, double cy, const double* h) {
     const srbd_tamols_params& p = a.p;
-    const double dl = p.gradient_delta;
     const double hx = a.hips[3 * leg], hy = a.hips[3 * leg + 1], hz = a.hips[3 * leg + 2];
-    const double sx = a.seeds[3 * leg], sy = a.seeds[3 * leg + 1], sz = a.seeds[3 * leg + 2];
     const double cz = h[0] + 0.005;  // VFA:192
-    // kinematic feasibility (VFA:375-395)
     {
         const double dx = cx - hx, dy = cy - hy, dz = cz - hz;
         const double d = sqrt(dx * dx + dy * dy + dz * dz);
@@ -137,19 +137,25 @@ __device__ __forceinline__ double tamols_score(const TamolsArgs& a, int leg, dou
             if (!(p.l_min <= d2 && d2 <= p.l_max)) return INFINITY;
         }
     }
-    // leg collision (VFA:397-420)
     for (int i = 0; i < 5; ++i) {
         const double al = p.alphas[i];
         const double zz = (1.0 - al) * hz + al * cz;
         const double hg = h[1 + i] - 0.02;
         if (zz < (hg + 0.02)) return INFINITY;
     }
-    // edge (VFA:422-466)
+    return 0.0;
+}
+__device__ __forceinline__ double tamols_part_edge(const TamolsArgs& a, const double* h) {
+    const srbd_tamols_params& p = a.p;
+    const double dl = p.gradient_delta;
     const double gx = fabs(h[6] - h[7]) / (2 * dl);
     const double gy = fabs(h[8] - h[9]) / (2 * dl);
     const double g = sqrt(gx * gx + gy * gy);
-    const double edge = g <= p.slope_threshold ? 0.0 : g - p.slope_threshold;
-    // roughness (VFA:468-521): least-squares plane on the symmetric 3x3 design (closed form)
+    return g <= p.slope_threshold ? 0.0 : g - p.slope_threshold;
+}
+// roughness: least-squares plane on the symmetric 3x3 design (closed form)
+__device__ __forceinline__ double tamols_part_rough(const TamolsArgs& a, const double* h) {
+    const double dl = a.p.gradient_delta;
     double xs[9], ys[9], sxh = 0, syh = 0, sxx = 0, syy = 0, sh = 0;
     for (int g2 = 0; g2 < 9; ++g2) {
         xs[g2] = (double)(g2 / 3 - 1) * dl;
@@ -169,15 +175,21 @@ __device__ __forceinline__ double tamols_score(const TamolsArgs& a, int leg, dou
     mr = mr / 9.0;
     double var = 0;
     for (int g2 = 0; g2 < 9; ++g2) var += (r[g2] - mr) * (r[g2] - mr);
-    const double rough = var / 9.0;
-    // deviation (VFA:344)
+    return var / 9.0;
+}
+// deviation (VFA:344), nominal kinematics (VFA:523-553, l_des = (0, 0, -h_des)), reference tracking (VFA:555-609),
+// stability (VFA:611-714): the raw terms
+__device__ __forceinline__ void tamols_part_rest(const TamolsArgs& a, int leg, double cx, double cy, const double* h,
+                                                 double& dev, double& nom, double& track, double& stab) {
+    const srbd_tamols_params& p = a.p;
+    const double hx = a.hips[3 * leg], hy = a.hips[3 * leg + 1], hz = a.hips[3 * leg + 2];
+    const double sx = a.seeds[3 * leg], sy = a.seeds[3 * leg + 1], sz = a.seeds[3 * leg + 2];
+    const double cz = h[0] + 0.005;
     const double ddx = cx - sx, ddy = cy - sy, ddz = cz - sz;
-    const double dev = ddx * ddx + ddy * ddy + ddz * ddz;
-    // nominal kinematics (VFA:523-553), l_des = (0, 0, -h_des)
+    dev = ddx * ddx + ddy * ddy + ddz * ddz;
     const double nx = hx - (cx - 0.0), ny = hy - (cy - 0.0), nz2 = hz - (cz - (-p.h_des));
-    const double nom = nx * nx + ny * ny + nz2 * nz2;
-    // reference tracking (VFA:555-609)
-    double track = 0.0;
+    nom = nx * nx + ny * ny + nz2 * nz2;
+    track = 0.0;
     if (!a.has_vel) {
         const double dx = cx - sx;
         track = dx < 0 ? dx * dx : 0.0;
@@ -188,8 +200,7 @@ __device__ __forceinline__ double tamols_score(const TamolsArgs& a, int leg, dou
             if ((vx > 0 && dx < 0) || (vx < 0 && dx > 0)) track = dx * dx;
         }
     }
-    // stability (VFA:611-714): distance of the predicted CoM to the diagonal support segment
-    double stab = 0.0;
+    stab = 0.0;
     if (a.has_base && a.has_feet && a.contact[leg] != 1) {
         const int dg = 3 - leg;  // FL<->RR, FR<->RL
         const double vx = a.has_vel ? a.vel[0] : 0.0, vy = a.has_vel ? a.vel[1] : 0.0;
@@ -209,11 +220,20 @@ __device__ __forceinline__ double tamols_score(const TamolsArgs& a, int leg, dou
         }
         if (d > p.stability_margin) stab = (d - p.stability_margin) * (d - p.stability_margin);
     }
-    return 0.0 + edge * p.w_edge + rough * p.w_rough + dev * p.w_dev + nom * p.w_nominal + track * p.w_tracking +
+}
+// VFA:222: 0.0 + edge w_edge + rough w_rough + dev w_dev + nom w_nominal + track w_tracking + stab w_stability
+__device__ __forceinline__ double tamols_combine(const srbd_tamols_params& p, double e, double r, double dev,
+                                                 double nom, double track, double stab) {
+    return 0.0 + e * p.w_edge + r * p.w_rough + dev * p.w_dev + nom * p.w_nominal + track * p.w_tracking +
            stab * p.w_stability;
 }
+__device__ __forceinline__ double tamols_score(const TamolsArgs& a, int leg, double cx, double cy, const double* h) {
+    if (tamols_part_hard(a, leg, cx, cy, h) != 0.0) return INFINITY;
+    double dev, nom, track, stab;
+    tamols_part_rest(a, leg, cx, cy, h, dev, nom, track, stab);
+    return tamols_combine(a.p, tamols_part_edge(a, h), tamols_part_rough(a, h), dev, nom, track, stab);
+}
 
-// candidates per block, max: every candidate when a leg runs in one block (TamolsJob::lattice)
 constexpr int TAMOLS_SLICE = TAMOLS_MAXCAND;
 static_assert(TAMOLS_BPL <= 64, "the merge loads one slice partial per lane of one wave");
 
@@ -227,6 +247,8 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
     __shared__ double rbest[TAMOLS_THREADS];
     __shared__ int rhit[TAMOLS_THREADS];
     __shared__ int last;
+    __shared__ int plist[TAMOLS_LDS_PRIMS];  // staged primitives that can touch this leg's patch (culled)
+    __shared__ int pn;
     extern __shared__ uint4 scene[];  // the terrain's primitives (+ box yaw cos / sin) when they fit
     const TamolsArgs& a = j.a;
     const int leg = blockIdx.y, b = blockIdx.x, NB = gridDim.x, tid = threadIdx.x, T = blockDim.x;
@@ -244,11 +266,31 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
         const int np = j.t.nprims;
         const bool staged = np > 0 && np <= TAMOLS_LDS_PRIMS;
         const int w = np * (int)(sizeof(srbd_terrain_prim) / 16);
+        int nlist = np;
         if (staged) {  // stage the scene: every ray re-reads every primitive
             const uint4* src = reinterpret_cast<const uint4*>(j.t.prims);
             const uint4* srcc = reinterpret_cast<const uint4*>(j.t.cs);
+            if (tid == 0) pn = 0;
             for (int i = tid; i < w + np; i += T) scene[i] = i < w ? src[i] : srcc[i - w];
             __syncthreads();
+            // cull: a primitive whose bounding circle (cylinder radius a, box half-diagonal) clears the patch's
+            // (centre the seed, radius the half-diagonal) by a margin holds no ray of the patch.  A ray's result
+            // is a maximum over primitives, so the list's order (atomic slots) does not matter.
+            {
+                const double hx = 0.5 * (double)(j.rows - 1) * fabs(j.dist_x), hy = 0.5 * (double)(j.cols - 1) * fabs(j.dist_y);
+                const double rp = sqrt(hx * hx + hy * hy);
+                const srbd_terrain_prim* sp = reinterpret_cast<const srbd_terrain_prim*>(scene);
+                for (int q = tid; q < np; q += T) {
+                    const srbd_terrain_prim& pr = sp[q];
+                    const double r = pr.type == SRBD_PRIM_BOX ? sqrt(pr.a * pr.a + pr.b * pr.b) : fabs(pr.a);
+                    const double dx = pr.cx - a.seeds[3 * leg], dy = pr.cy - a.seeds[3 * leg + 1];
+                    const double lim = (r + rp) * 1.000001 + 1e-9;
+                    // keep unless clearly outside (NaN / inf geometry is kept: the walk decides as before)
+                    if (!(dx * dx + dy * dy > lim * lim)) plist[atomicAdd(&pn, 1)] = q;
+                }
+            }
+            __syncthreads();
+            nlist = pn;
             TAM_STAMP(6);
         }
         // G lanes per ray, each walking a contiguous share of the primitives (the ray's result is a max).
@@ -257,6 +299,7 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
         const int ncp = (nc + 63) & ~63;
         int G = 8;  // the most of 8, 4, 2 that fit the block, else 1 lane per ray in chunks
         while (G > 1 && G * ncp > T) G >>= 1;
+        while (G > 1 && staged && G * 4 > nlist) G >>= 1;  // a short culled list: fewer lanes per ray
         for (int u0 = 0; u0 < G * ncp; u0 += T) {
             const int u = u0 + tid, part = u / ncp, i = u - part * ncp;
             const bool on = part < G && i < nc;
@@ -268,9 +311,9 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
                 if (part == 0) ray_walk_fields(j.t, x, y, j.ray_z, best, hit);
                 // two call sites, so the staged walk reads through LDS-typed pointers (ds_read, not flat)
                 if (staged)
-                    ray_walk_prims(reinterpret_cast<const srbd_terrain_prim*>(scene),
-                                   reinterpret_cast<const double*>(scene + w), part * np / G, (part + 1) * np / G,
-                                   x, y, j.ray_z, best, hit);
+                    ray_walk_list(reinterpret_cast<const srbd_terrain_prim*>(scene),
+                                  reinterpret_cast<const double*>(scene + w), plist, part * nlist / G,
+                                  (part + 1) * nlist / G, x, y, j.ray_z, best, hit);
                 else
                     ray_walk_prims(j.t.prims, j.t.cs, part * np / G, (part + 1) * np / G, x, y, j.ray_z, best, hit);
             }
@@ -307,9 +350,16 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
     // ---- phase A: this block's candidates [c0, c1), their queries (+ the seed on block 0)
     const int c0 = (int)((long)b * nc / NB), c1 = (int)((long)(b + 1) * nc / NB);
     const int nown = (c1 - c0) * TAMOLS_NQ, nloc = nown + (b == 0 ? 1 : 0);
-    if (j.lattice) {  // a raycast lattice patch: nine points per query
-        for (int t = tid; t < nloc; t += T)
-            nn[t] = tamols_query_lattice(j, leg, t < nown ? c0 * TAMOLS_NQ + t : nc * TAMOLS_NQ, px, py, pz) + 0.02;
+    if (j.lattice) {  // a raycast lattice patch: four points per query
+        // lanes enumerate (sample q, candidate) candidate-fastest, so a wave's lanes share q (its branch of
+        // tamols_query_point and its alpha): uniform control flow; nn keeps the (candidate, q) layout
+        const int ncb = c1 - c0;
+        for (int u = tid; u < nloc; u += T) {
+            const int q = u < nown ? u / ncb : 0, cl = u < nown ? u - q * ncb : 0;
+            const int at = u < nown ? cl * TAMOLS_NQ + q : nloc - 1;
+            nn[at] = tamols_query_lattice(j, leg, u < nown ? (c0 + cl) * TAMOLS_NQ + q : nc * TAMOLS_NQ, px, py, pz) +
+                     0.02;
+        }
     } else {
         // Q lanes per query (aligned groups of Q consecutive lanes), each scanning a contiguous quarter of the
         // patch; the groups' (d2, first index) minima combine lowest-part-first, so the first nearest point of
@@ -338,10 +388,51 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
     TAM_STAMP(2);
 
     // ---- phase B
+    const int ncb = c1 - c0, ncp = (ncb + 63) & ~63;
+    if (j.lattice && 4 * ncp <= T) {
+        // the four parts of every candidate at once, each on waves of its own (part = wave-uniform); the terms go to
+        // query slots only their own part read (hard -> 1, edge -> 6, roughness -> 10, the rest -> 2..5; slot 0,
+        // the candidate's height, stays), written after a barrier, then one lane per candidate combines them
+        const int part = tid / ncp, cl = tid - part * ncp;
+        const bool on = part < 4 && cl < ncb;
+        double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
+        if (on) {
+            const double* h = nn + cl * TAMOLS_NQ;
+            const double cx = px[c0 + cl], cy = py[c0 + cl];
+            if (part == 0) t0 = tamols_part_hard(a, leg, cx, cy, h);
+            else if (part == 1) t0 = tamols_part_edge(a, h);
+            else if (part == 2) t0 = tamols_part_rough(a, h);
+            else tamols_part_rest(a, leg, cx, cy, h, t0, t1, t2, t3);
+        }
+        __syncthreads();
+        if (on) {
+            double* h = nn + cl * TAMOLS_NQ;
+            if (part == 0) {
+                h[1] = t0;
+            } else if (part == 1) {
+                h[6] = t0;
+            } else if (part == 2) {
+                h[10] = t0;
+            } else {
+                h[2] = t0;
+                h[3] = t1;
+                h[4] = t2;
+                h[5] = t3;
+            }
+        }
+        __syncthreads();
+        for (int c = c0 + tid; c < c1; c += T) {
+            const double* h = nn + (c - c0) * TAMOLS_NQ;
+            const double s = h[1] != 0.0 ? INFINITY : tamols_combine(a.p, h[6], h[10], h[2], h[3], h[4], h[5]);
+            sc[c - c0] = s;
+            if (j.scores) j.scores[(size_t)leg * nc + c] = s;
+        }
+    } else {
     for (int c = c0 + tid; c < c1; c += T) {
         const double s = tamols_score(a, leg, px[c], py[c], nn + (c - c0) * TAMOLS_NQ);
         sc[c - c0] = s;
         if (j.scores) j.scores[(size_t)leg * nc + c] = s;
+    }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's score / patch stores issued and done
     __syncthreads();
@@ -479,7 +570,7 @@ int tamols_prepare() {
 }
 
 void launch_tamols_fused(const TamolsJob& j, hipStream_t s) {
-    // a raycast lattice patch: one block per leg (nine points per query, no cross-block merge)
+    // a raycast lattice patch: one block per leg (four points per query, no cross-block merge)
     const int nb = j.lattice ? 1 : (j.a.ncand < TAMOLS_BPL ? j.a.ncand : TAMOLS_BPL);
     const int np = j.use_terrain ? j.t.nprims : 0;
     const size_t smem = (np > 0 && np <= TAMOLS_LDS_PRIMS) ? (sizeof(srbd_terrain_prim) + 2 * sizeof(double)) * np : 0;

@@ -47,6 +47,26 @@ __device__ __forceinline__ void ray_walk_prims(const srbd_terrain_prim* prims, c
     }
 }
 
+// The same over the primitives listed in idx[q0, q1) (the ones a patch can touch, TAMOLS's culled list).
+__device__ __forceinline__ void ray_walk_list(const srbd_terrain_prim* prims, const double* cs, const int* idx, int q0,
+                                              int q1, double x, double y, double ray_z, double& best, int& hit) {
+#pragma unroll 2
+    for (int n = q0; n < q1; ++n) {
+        const int q = idx[n];
+        const srbd_terrain_prim& pr = prims[q];
+        const double ux = x - pr.cx, uy = y - pr.cy;
+        bool in;
+        if (pr.type == SRBD_PRIM_BOX) {
+            const double cb = cs[2 * q], sb = cs[2 * q + 1];
+            const double u = cb * ux + sb * uy, v = cb * uy - sb * ux;
+            in = fabs(u) <= pr.a && fabs(v) <= pr.b;
+        } else {
+            in = ux * ux + uy * uy <= pr.a * pr.a;
+        }
+        if (in) ray_consider(pr.cz + pr.c, ray_z, best, hit);
+    }
+}
+
 // The ground plane and the height field (cells split along the (i, j)-(i+1, j+1) diagonal).
 __device__ __forceinline__ void ray_walk_fields(const TerrainDev& t, double x, double y, double ray_z, double& best,
                                                 int& hit) {

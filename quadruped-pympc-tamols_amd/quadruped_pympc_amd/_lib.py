@@ -232,8 +232,8 @@ def _load_fast():
         from . import _srbd_fast
     except ImportError:
         return None
-    _srbd_fast.bind(C.cast(lib.srbd_interface_step, C.c_void_p).value,
-                    C.cast(lib.srbd_pgg_contact_sequence, C.c_void_p).value)
+    _srbd_fast.bind(*(C.cast(getattr(lib, f), C.c_void_p).value for f in (
+        "srbd_interface_step", "srbd_pgg_contact_sequence", "srbd_foothold_mpc_step", "srbd_jax_split")))
     return _srbd_fast
 
 

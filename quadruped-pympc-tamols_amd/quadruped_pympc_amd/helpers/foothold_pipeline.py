@@ -103,6 +103,22 @@ class TamolsMpcStep:
         iface, ctrl, vfa = self.iface, self.iface.controller, self.vfa
         io = self._fused_io()
         a = self._io_np
+        ctx = ctrl.context
+        if _lib.fast is not None:  # the staging, the key split and the call in C (_srbd_fast)
+            res = _lib.SrbdResult()
+            r = _lib.fast.foothold_step(vfa.search.h.value, self.heightmaps.FL.terrain.h.value,
+                                        C.addressof(vfa._params()), ctx.h.value, C.addressof(io), state_current,
+                                        ref_base, ref_feet_pos, hip_pos, base_lin_vel, base_ori_euler_xyz,
+                                        contact_sequence, ctrl.best_control_parameters, iface.previous_contact_mpc,
+                                        ctrl.master_key, ctrl._calls, ctx._best, ctx._contact, C.addressof(res),
+                                        ctrl.num_control_parameters_single_leg, _lib.RNG_CODES[ctrl.rng])
+            if r is not None:
+                rc, stage, current_contact, key, calls = r[:5]
+                if stage >= 2:  # compute_control's with_newkey ran
+                    ctrl.master_key = key
+                    if ctrl.rng != "philox":
+                        ctrl._calls = calls
+                return self._fused_outputs(rc, res, current_contact, None if rc else r[5:], a["seeds"], ref_base)
         np.concatenate([state_current[k] for k in ("position", "linear_velocity", "orientation", "angular_velocity",
                                                    "foot_FL", "foot_FR", "foot_RL", "foot_RR")], out=a["state_in"])
         np.concatenate([ref_base[k] for k in ("ref_position", "ref_linear_velocity", "ref_orientation",
@@ -117,7 +133,6 @@ class TamolsMpcStep:
         a["current_contact"][:] = current_contact
         a["previous_contact"][:] = iface.previous_contact_mpc
         io.yaw = float(base_ori_euler_xyz[2])
-        ctx = ctrl.context
         H = ctx.cfg.horizon
         ctx._contact[...] = np.asarray(contact_sequence)[:, :H]
         ctx._best[...] = np.reshape(ctrl.best_control_parameters, ctx.P)
@@ -128,8 +143,17 @@ class TamolsMpcStep:
         rc = _lib.lib.srbd_foothold_mpc_step(vfa.search.h, self.heightmaps.FL.terrain.h, C.byref(vfa._params()),
                                              ctx.h, self._io_ref, ctx._a_contact, H, ctx._a_best,
                                              ctrl.num_control_parameters_single_leg, seed, counter, C.byref(res))
-        # the objects' state, as the Python chain leaves it -- also when a call of the chain failed (io.stage:
-        # the calls that completed), so an error leaves them as compute_adaptation / compute_control would
+        if io.stage < 2:  # compute_control's with_newkey had not run
+            ctrl.master_key, ctrl._calls = key0
+        return self._fused_outputs(rc, res, current_contact, None, seeds, ref_base)
+
+    def _fused_outputs(self, rc, res, current_contact, made, seeds, ref_base):
+        """The objects' state after srbd_foothold_mpc_step, as the Python chain leaves it -- also when a call of the
+        chain failed (io.stage: the calls that completed), so an error leaves them as compute_adaptation /
+        compute_control would -- and the step's 7-tuple.  made: (grf, predicted state, warm start) the C glue
+        already built, or None."""
+        iface, ctrl, vfa, io, a = self.iface, self.iface.controller, self.vfa, self._io, self._io_np
+        ctx = ctrl.context
         vfa.reset()
         if io.stage >= 1:
             hm = self._io_hm.copy()
@@ -150,9 +174,7 @@ class TamolsMpcStep:
                 m._data, m.pending = None, (seeds[3 * i:3 * i + 3].copy(), io.yaw)
         if io.stage >= 2:
             iface.previous_contact_mpc = current_contact
-            ctrl.best_control_parameters = ctx._best.copy()
-        else:  # compute_control's with_newkey had not run
-            ctrl.master_key, ctrl._calls = key0
+            ctrl.best_control_parameters = made[2] if made is not None else ctx._best.copy()
         if rc != _lib.OK:
             what = "srbd_tamols_run_terrain" if io.stage == 0 else "srbd_prepare_state" if io.stage == 1 else "srbd_step"
             msg = _lib.lib.srbd_tamols_last_error(vfa.search.h) if io.stage == 0 else _lib.last_error(ctx.h)
@@ -160,10 +182,14 @@ class TamolsMpcStep:
                                f"{msg.decode() if isinstance(msg, bytes) else msg}")
         ctx.step_id += 1
         ctrl.last_result = res
-        g = np.array(res.grf, dtype=np.float32).reshape(4, 3) * current_contact[:, None]  # as compute_control
+        if made is not None:
+            g, pred = made[0], made[1]
+        else:
+            g = np.array(res.grf, dtype=np.float32).reshape(4, 3) * current_contact[:, None]  # as compute_control
+            pred = np.array(res.predicted_state, dtype=np.float32)
         grfs = LegsAttr(FL=g[0], FR=g[1], RL=g[2], RR=g[3])
         footholds = LegsAttr(FL=fh[0], FR=fh[1], RL=fh[2], RR=fh[3])
-        return grfs, footholds, None, None, None, 1.4, np.array(res.predicted_state, dtype=np.float32)
+        return grfs, footholds, None, None, None, 1.4, pred
 
     def step(self, state_current: dict, ref_feet_pos: LegsAttr, hip_pos: LegsAttr, ref_base: dict,
              contact_sequence: np.ndarray, base_lin_vel: np.ndarray, base_ori_euler_xyz: np.ndarray,

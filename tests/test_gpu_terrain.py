@@ -155,7 +155,7 @@ def test_large_scene_fused_tamols(lib, n_box, n_cyl):
 
 @pytest.mark.parametrize("yaw", [0.0, 0.4, math.pi / 2, -2.3])
 def test_lattice_queries_equal_full_scan(lib, monkeypatch, yaw):
-    """The raycast patch's nearest-neighbour queries on the lattice (nine points per query, one block per leg)
+    """The raycast patch's nearest-neighbour queries on the lattice (four points per query, one block per leg)
     against every point scanned (SRBD_TAMOLS_LATTICE=0, 16 blocks per leg): every output bit-equal, with hips on
     half-lattice points (exact ties between two patch points: the first index wins both ways) and hips off the
     patch (queries clamped to its edge)."""
