@@ -264,42 +264,72 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
     // ---- patch (raycast, or the caller's) -> LDS; block 0 also hands the raycast patch back
     if (j.use_terrain) {
         const int np = j.t.nprims;
-        const bool staged = np > 0 && np <= TAMOLS_LDS_PRIMS;
+        // lattice mode: the primitives that can touch this leg's patch, culled straight from global memory into a
+        // compact list (the query stage `nn`, free until phase A, holds it); past CP_CAP of them, every primitive
+        // is walked from global memory.  Else the whole scene staged in the dynamic LDS (TAMOLS_LDS_PRIMS).
+        constexpr int CP_CAP = 128;
+        double* cpx = nn;
+        double* cpy = nn + CP_CAP;
+        double* cpa = nn + 2 * CP_CAP;   // box: half size x; cylinder: radius
+        double* cpb = nn + 3 * CP_CAP;   // box: half size y
+        double* cpt = nn + 4 * CP_CAP;   // top: cz + c
+        double* cpc = nn + 5 * CP_CAP;   // box yaw cos / sin
+        double* cps = nn + 6 * CP_CAP;
+        double* cpk = nn + 7 * CP_CAP;   // 1: box, 0: cylinder
+        static_assert(8 * 128 <= TAMOLS_SLICE * TAMOLS_NQ, "the compact list fits the query stage");
+        const bool compact = j.lattice && np > 0;
+        const bool staged = !compact && np > 0 && np <= TAMOLS_LDS_PRIMS;
         const int w = np * (int)(sizeof(srbd_terrain_prim) / 16);
         int nlist = np;
-        if (staged) {  // stage the scene: every ray re-reads every primitive
-            const uint4* src = reinterpret_cast<const uint4*>(j.t.prims);
-            const uint4* srcc = reinterpret_cast<const uint4*>(j.t.cs);
+        if (compact || staged) {
             if (tid == 0) pn = 0;
-            for (int i = tid; i < w + np; i += T) scene[i] = i < w ? src[i] : srcc[i - w];
+            if (staged) {  // stage the scene: every ray re-reads every primitive
+                const uint4* src = reinterpret_cast<const uint4*>(j.t.prims);
+                const uint4* srcc = reinterpret_cast<const uint4*>(j.t.cs);
+                for (int i = tid; i < w + np; i += T) scene[i] = i < w ? src[i] : srcc[i - w];
+            }
             __syncthreads();
-            // cull: a primitive whose bounding circle (cylinder radius a, box half-diagonal) clears the patch's
-            // (centre the seed, radius the half-diagonal) by a margin holds no ray of the patch.  A ray's result
-            // is a maximum over primitives, so the list's order (atomic slots) does not matter.
-            {
-                const double hx = 0.5 * (double)(j.rows - 1) * fabs(j.dist_x), hy = 0.5 * (double)(j.cols - 1) * fabs(j.dist_y);
-                const double rp = sqrt(hx * hx + hy * hy);
-                const srbd_terrain_prim* sp = reinterpret_cast<const srbd_terrain_prim*>(scene);
-                for (int q = tid; q < np; q += T) {
-                    const srbd_terrain_prim& pr = sp[q];
-                    const double r = pr.type == SRBD_PRIM_BOX ? sqrt(pr.a * pr.a + pr.b * pr.b) : fabs(pr.a);
-                    const double dx = pr.cx - a.seeds[3 * leg], dy = pr.cy - a.seeds[3 * leg + 1];
-                    const double lim = (r + rp) * 1.000001 + 1e-9;
-                    // keep unless clearly outside (NaN / inf geometry is kept: the walk decides as before)
-                    if (!(dx * dx + dy * dy > lim * lim)) plist[atomicAdd(&pn, 1)] = q;
+            // cull: a primitive whose bounding circle (cylinder radius a, box half-diagonal, bounded by |a| + |b|)
+            // clears the patch's (centre the seed, radius the half-diagonal) by a margin holds no ray of the patch.
+            // A ray's result is a maximum over primitives, so the list's order (atomic slots) does not matter.
+            const double hx = 0.5 * (double)(j.rows - 1) * fabs(j.dist_x), hy = 0.5 * (double)(j.cols - 1) * fabs(j.dist_y);
+            const double rp = sqrt(hx * hx + hy * hy);
+            const srbd_terrain_prim* sp = staged ? reinterpret_cast<const srbd_terrain_prim*>(scene) : j.t.prims;
+            for (int q = tid; q < np; q += T) {
+                const srbd_terrain_prim pr = sp[q];
+                const bool box = pr.type == SRBD_PRIM_BOX;
+                const double r = box ? fabs(pr.a) + fabs(pr.b) : fabs(pr.a);
+                const double dx = pr.cx - a.seeds[3 * leg], dy = pr.cy - a.seeds[3 * leg + 1];
+                const double lim = (r + rp) * 1.000001 + 1e-9;
+                // keep unless clearly outside (NaN / inf geometry is kept: the walk decides as before)
+                if (!(dx * dx + dy * dy > lim * lim)) {
+                    const int slot = atomicAdd(&pn, 1);
+                    if (staged) {
+                        plist[slot] = q;
+                    } else if (slot < CP_CAP) {
+                        cpx[slot] = pr.cx;
+                        cpy[slot] = pr.cy;
+                        cpa[slot] = pr.a;
+                        cpb[slot] = pr.b;
+                        cpt[slot] = pr.cz + pr.c;
+                        cpc[slot] = box ? j.t.cs[2 * q] : 0.0;
+                        cps[slot] = box ? j.t.cs[2 * q + 1] : 0.0;
+                        cpk[slot] = box ? 1.0 : 0.0;
+                    }
                 }
             }
             __syncthreads();
             nlist = pn;
             TAM_STAMP(6);
         }
+        const bool listed = staged || (compact && nlist <= CP_CAP);
         // G lanes per ray, each walking a contiguous share of the primitives (the ray's result is a max).
         // Lanes of one wave share the share (lane -> ray i = u mod ncp, share = u / ncp, ncp = nc rounded
         // up to the wave): the primitive loads are LDS broadcasts and the box / cylinder branch is uniform.
         const int ncp = (nc + 63) & ~63;
         int G = 8;  // the most of 8, 4, 2 that fit the block, else 1 lane per ray in chunks
         while (G > 1 && G * ncp > T) G >>= 1;
-        while (G > 1 && staged && G * 4 > nlist) G >>= 1;  // a short culled list: fewer lanes per ray
+        while (G > 1 && listed && G * 4 > nlist) G >>= 1;  // a short culled list: fewer lanes per ray
         for (int u0 = 0; u0 < G * ncp; u0 += T) {
             const int u = u0 + tid, part = u / ncp, i = u - part * ncp;
             const bool on = part < G && i < nc;
@@ -310,7 +340,20 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
             if (on) {
                 if (part == 0) ray_walk_fields(j.t, x, y, j.ray_z, best, hit);
                 // two call sites, so the staged walk reads through LDS-typed pointers (ds_read, not flat)
-                if (staged)
+                if (compact && listed) {  // the compact list: the same float64 tests as ray_walk_prims
+                    for (int n = part * nlist / G; n < (part + 1) * nlist / G; ++n) {
+                        const double ux = x - cpx[n], uy = y - cpy[n];
+                        bool in;
+                        if (cpk[n] != 0.0) {
+                            const double cb = cpc[n], sb = cps[n];
+                            const double uu = cb * ux + sb * uy, vv = cb * uy - sb * ux;
+                            in = fabs(uu) <= cpa[n] && fabs(vv) <= cpb[n];
+                        } else {
+                            in = ux * ux + uy * uy <= cpa[n] * cpa[n];
+                        }
+                        if (in) ray_consider(cpt[n], j.ray_z, best, hit);
+                    }
+                } else if (staged)
                     ray_walk_list(reinterpret_cast<const srbd_terrain_prim*>(scene),
                                   reinterpret_cast<const double*>(scene + w), plist, part * nlist / G,
                                   (part + 1) * nlist / G, x, y, j.ray_z, best, hit);
@@ -573,7 +616,8 @@ void launch_tamols_fused(const TamolsJob& j, hipStream_t s) {
     // a raycast lattice patch: one block per leg (four points per query, no cross-block merge)
     const int nb = j.lattice ? 1 : (j.a.ncand < TAMOLS_BPL ? j.a.ncand : TAMOLS_BPL);
     const int np = j.use_terrain ? j.t.nprims : 0;
-    const size_t smem = (np > 0 && np <= TAMOLS_LDS_PRIMS) ? (sizeof(srbd_terrain_prim) + 2 * sizeof(double)) * np : 0;
+    // the staged scene's dynamic LDS (not in lattice mode: its culled list lives in the static query stage)
+    const size_t smem = (!j.lattice && np > 0 && np <= TAMOLS_LDS_PRIMS) ? (sizeof(srbd_terrain_prim) + 2 * sizeof(double)) * np : 0;
     hipLaunchKernelGGL(tamols_fused_kernel, dim3(nb, 4), dim3(TAMOLS_THREADS), smem, s, j);
 }
 
