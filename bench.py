@@ -357,7 +357,8 @@ def tamols_latency(calls: int):
     lat = np.array(lat[10:]) * 1e3
     return {"p50_ms": round(float(np.percentile(lat, 50)), 4), "p99_ms": round(float(np.percentile(lat, 99)), 4),
             "calls": calls, "valid_legs": int(out["valid"].sum()),
-            "path": "srbd_tamols_run_terrain: 4 x 13 x 7 raycast patches + TAMOLS, stepping_stones_medium"}
+            "path": "srbd_tamols_run_terrain: 4 x 13 x 7 raycast patches + TAMOLS, stepping_stones_medium",
+            "cadence": "every call adapts (the reference adapts at the swing apex only, wb_interface.py:230-246)"}
 
 
 def c4_pipeline_latency(steps: int):
@@ -394,6 +395,8 @@ def c4_pipeline_latency(steps: int):
             "p50_ms": round(float(np.percentile(lat, 50)) * 1e3, 4),
             "p99_ms": round(float(np.percentile(lat, 99)) * 1e3, 4), "steps": steps, "valid_legs": int(valid),
             "workload": w.name, "fused": bool(fused),
+            "cadence": "TAMOLS runs on every MPC step here; the reference adapts only at the swing apex "
+                       "(wb_interface.py:230-246), so this is an upper bound on its per-step cost",
             "path": "TamolsMpcStep.step: GpuHeightMap x4 (lazy) -> VisualFootholdAdaptation.compute_adaptation "
                     "(srbd_tamols_run_terrain: raycast + TAMOLS, one launch) -> ref_state -> "
                     "SRBDControllerInterface.compute_control (srbd_prepare_state, srbd_step MPPI N=10000 H=12); "
@@ -595,6 +598,11 @@ def main(argv=None):
         sys.exit(spawn_ranks(args, argv))  # before torch / the HIP library are loaded
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # exactly one line on stdout: native libraries (RCCL's version banner at communicator setup, ...) print to fd 1, so
+    # fd 1 is pointed at stderr for the run and the JSON line goes to the saved stdout
+    out_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     sys.path.insert(0, os.path.join(ROOT, "quadruped-pympc-tamols_amd"))
     if world > 1 or args.sharded:
         import torch  # noqa: F401  -- before libsrbd_hip.so: one HIP runtime per process (see _lib.py)
@@ -699,7 +707,10 @@ def main(argv=None):
         line["interface_step_armed"] = interface_latency(w, args.extras, armed=True)
         line["tamols_c4"] = tamols_latency(args.extras)
         line["c4"] = c4_pipeline_latency(args.extras)
-    print(json.dumps(line), flush=True)
+    sys.stdout.flush()
+    buf = (json.dumps(line) + "\n").encode()
+    while buf:
+        buf = buf[os.write(out_fd, buf):]
 
 
 if __name__ == "__main__":
