@@ -388,19 +388,21 @@ def c4_pipeline_latency(steps: int):
     assert np.isfinite(out[6]).all()
     valid = sum(pipe.last_constraints[n] is not None for n in ("FL", "FR", "RL", "RR"))
     fused = pipe._fusable()
+    chained = pipe.controller.context.foothold_chained()
     pipe.close()
     ter.close()
     lat = np.array(lat[20:])
     return {"value": round(w.num_samples / float(lat.mean()), 1), "unit": "rollouts/s",
             "p50_ms": round(float(np.percentile(lat, 50)) * 1e3, 4),
             "p99_ms": round(float(np.percentile(lat, 99)) * 1e3, 4), "steps": steps, "valid_legs": int(valid),
-            "workload": w.name, "fused": bool(fused),
+            "workload": w.name, "fused": bool(fused), "chained_steps": int(chained),
             "cadence": "TAMOLS runs on every MPC step here; the reference adapts only at the swing apex "
                        "(wb_interface.py:230-246), so this is an upper bound on its per-step cost",
             "path": "TamolsMpcStep.step: GpuHeightMap x4 (lazy) -> VisualFootholdAdaptation.compute_adaptation "
                     "(srbd_tamols_run_terrain: raycast + TAMOLS, one launch) -> ref_state -> "
                     "SRBDControllerInterface.compute_control (srbd_prepare_state, srbd_step MPPI N=10000 H=12); "
-                    "fused: the same calls chained in C by srbd_foothold_mpc_step"}
+                    "fused: one host call, srbd_foothold_mpc_step -- chained on the device (the TAMOLS launch writes "
+                    "the step's input, the rollout launch queued behind it, one host wait) when the context allows"}
 
 
 # ---------------------------------------------------------------------------------------------- runs

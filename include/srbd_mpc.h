@@ -137,6 +137,9 @@ int srbd_debug_arm_delay(srbd_ctx* ctx, uint32_t delay_us);
  * the tail block's bounded wait (2 s) times out and the step fails with SRBD_E_HIP; the call resets the
  * hand-off state, and the following step is exact again. */
 int srbd_debug_split_drop(srbd_ctx* ctx);
+/* srbd_foothold_mpc_step calls on this context that ran chained on the device (TAMOLS writing the step's input;
+ * one host wait), since the context was created. */
+int srbd_foothold_chained(const srbd_ctx* ctx, int64_t* n);
 
 /*
  * Gait-adaptive sampling (centroidal_nmpc_jax_gait_adaptive.py; replaces

@@ -145,6 +145,7 @@ struct srbd_ctx {
     uint64_t arm_seed = 0, arm_ctr = 0;
     std::chrono::steady_clock::time_point arm_t0;
     int64_t arm_served = 0, arm_cancelled = 0;
+    int64_t foothold_chained = 0;  // srbd_foothold_mpc_step calls run chained (srbd_foothold_chain)
     std::string err;
 };
 
@@ -954,6 +955,12 @@ extern "C" int srbd_armed_refired(const srbd_ctx* c, int64_t* refired) {
 extern "C" int srbd_debug_arm_delay(srbd_ctx* c, uint32_t delay_us) {
     if (!c) return SRBD_E_INVALID;
     c->arm_test_delay_us = delay_us;
+    return SRBD_OK;
+}
+
+extern "C" int srbd_foothold_chained(const srbd_ctx* c, int64_t* n) {
+    if (!c || !n) return SRBD_E_INVALID;
+    *n = c->foothold_chained;
     return SRBD_OK;
 }
 
@@ -2187,7 +2194,8 @@ struct srbd_tamols_ctx {
     double* h_hm = nullptr;  // host-mapped heightmaps: in (srbd_tamols_run) or out (run_terrain)
     double* d_hm_host = nullptr;
     double* d_part = nullptr;  // per-block partials
-    unsigned* d_cnt = nullptr;  // block / leg counters (zero between calls)
+    unsigned* d_cnt = nullptr;  // block / leg counters, [4] the feed's leg arrivals (zero between calls)
+    double* d_feed = nullptr;   // the feed's footholds (srbd_foothold_mpc_step's chained form)
     uint32_t* h_flag = nullptr;
     uint32_t* d_flag = nullptr;
     uint32_t seq = 0;
@@ -2211,7 +2219,8 @@ extern "C" int srbd_tamols_create(int32_t device_id, srbd_tamols_ctx** out) {
               hipHostGetDevicePointer((void**)&t->d_flag, t->h_flag, 0) == hipSuccess &&
               hipMalloc((void**)&t->d_part, sizeof(double) * 4 * TAMOLS_BPL * 4) == hipSuccess &&
               hipMalloc((void**)&t->d_cnt, sizeof(unsigned) * 8) == hipSuccess &&
-              hipMemset(t->d_cnt, 0, sizeof(unsigned) * 8) == hipSuccess && tamols_prepare() == 0 &&
+              hipMemset(t->d_cnt, 0, sizeof(unsigned) * 8) == hipSuccess &&
+              hipMalloc((void**)&t->d_feed, sizeof(double) * 12) == hipSuccess && tamols_prepare() == 0 &&
               hipDeviceSynchronize() == hipSuccess;
     if (!ok) {
         srbd_tamols_destroy(t);
@@ -2229,6 +2238,7 @@ extern "C" void srbd_tamols_destroy(srbd_tamols_ctx* t) {
     if (t->stream) (void)hipStreamSynchronize(t->stream);
     (void)hipFree(t->d_part);
     (void)hipFree(t->d_cnt);
+    (void)hipFree(t->d_feed);
     (void)hipFree(t->d_dbg);
     if (t->h_out) (void)hipHostFree(t->h_out);
     if (t->h_hm) (void)hipHostFree(t->h_hm);
@@ -2268,12 +2278,10 @@ static int tamols_reserve(srbd_tamols_ctx* t, int nc) {
     return SRBD_OK;
 }
 
-// Launch one call and wait for its published sequence number (bounded: the stream is polled now and
-// then, so a fault or a launch failure surfaces as an error instead of a hang).
-static int tamols_launch_wait(srbd_tamols_ctx* t, TamolsJob& j, const double* seeds, const double* hips,
-                              const double* vel, const double* base, const int32_t* contact, const double* feet,
-                              const srbd_tamols_params* p, int rows, int cols, double* out_fh, double* out_box,
-                              int32_t* out_valid, double* out_scores, double* out_seedh) {
+// One call's arguments, output pointers and sequence number.
+static void tamols_job_fill(srbd_tamols_ctx* t, TamolsJob& j, const double* seeds, const double* hips,
+                            const double* vel, const double* base, const int32_t* contact, const double* feet,
+                            const srbd_tamols_params* p, int rows, int cols, bool scores) {
     const int nc = rows * cols;
     TamolsArgs& a = j.a;
     memset(&a, 0, sizeof(a));
@@ -2296,26 +2304,47 @@ static int tamols_launch_wait(srbd_tamols_ctx* t, TamolsJob& j, const double* se
     a.p = *p;
     j.rows = rows;
     j.cols = cols;
-    j.scores = out_scores ? t->d_out_host : nullptr;
+    j.scores = scores ? t->d_out_host : nullptr;
     j.out = t->d_out_host + 4 * (size_t)nc;
     j.part = t->d_part;
     j.cnt = t->d_cnt;
     j.flag = t->d_flag;
     j.seq = ++t->seq;
     j.dbg = t->d_dbg;
+}
+
+static bool tamols_published(const srbd_tamols_ctx* t, uint32_t seq) {  // every leg's word holds the call's number
+    for (int l = 0; l < 4; ++l)
+        if (__atomic_load_n(t->h_flag + l, __ATOMIC_ACQUIRE) != seq) return false;
+    return true;
+}
+
+// The outputs of a published call (host-mapped) into the caller's arrays.
+static void tamols_outputs(const srbd_tamols_ctx* t, int nc, double* out_fh, double* out_box, int32_t* out_valid,
+                           double* out_scores, double* out_seedh) {
+    const double* h = t->h_out + 4 * (size_t)nc;
+    memcpy(out_fh, h, sizeof(double) * 12);
+    memcpy(out_box, h + 12, sizeof(double) * 24);
+    if (out_seedh) memcpy(out_seedh, h + 36, sizeof(double) * 4);
+    memcpy(out_valid, h + 40, sizeof(int32_t) * 4);
+    if (out_scores) memcpy(out_scores, t->h_out, sizeof(double) * 4 * nc);
+}
+
+// Launch one call and wait for its published sequence number (bounded: the stream is polled now and
+// then, so a fault or a launch failure surfaces as an error instead of a hang).
+static int tamols_launch_wait(srbd_tamols_ctx* t, TamolsJob& j, const double* seeds, const double* hips,
+                              const double* vel, const double* base, const int32_t* contact, const double* feet,
+                              const srbd_tamols_params* p, int rows, int cols, double* out_fh, double* out_box,
+                              int32_t* out_valid, double* out_scores, double* out_seedh) {
+    tamols_job_fill(t, j, seeds, hips, vel, base, contact, feet, p, rows, cols, out_scores != nullptr);
     launch_tamols_fused(j, t->stream);
     TAM_TRY(t, hipGetLastError());
-    const auto published = [&] {  // every leg's word holds this call's sequence number
-        for (int l = 0; l < 4; ++l)
-            if (__atomic_load_n(t->h_flag + l, __ATOMIC_ACQUIRE) != j.seq) return false;
-        return true;
-    };
     for (uint64_t it = 1;; ++it) {
-        if (published()) break;
+        if (tamols_published(t, j.seq)) break;
         if ((it & 4095) == 0) {
             const hipError_t e = hipStreamQuery(t->stream);
             if (e == hipSuccess) {
-                if (published()) break;
+                if (tamols_published(t, j.seq)) break;
                 t->err = "TAMOLS launch completed without publishing its outputs";
                 return SRBD_E_HIP;
             }
@@ -2323,13 +2352,28 @@ static int tamols_launch_wait(srbd_tamols_ctx* t, TamolsJob& j, const double* se
         }
         __builtin_ia32_pause();
     }
-    const double* h = t->h_out + 4 * (size_t)nc;
-    memcpy(out_fh, h, sizeof(double) * 12);
-    memcpy(out_box, h + 12, sizeof(double) * 24);
-    if (out_seedh) memcpy(out_seedh, h + 36, sizeof(double) * 4);
-    memcpy(out_valid, h + 40, sizeof(int32_t) * 4);
-    if (out_scores) memcpy(out_scores, t->h_out, sizeof(double) * 4 * nc);
+    tamols_outputs(t, rows * cols, out_fh, out_box, out_valid, out_scores, out_seedh);
     return SRBD_OK;
+}
+
+// The raycast patches' part of a terrain job: centres = the seeds, one yaw.
+static void tamols_terrain_job(TamolsJob& j, const srbd_terrain* ter, double yaw, double dist_x, double dist_y,
+                               double ray_z) {
+    j.use_terrain = 1;
+    j.t = ter->dev;
+    j.yaw_c = cos(yaw);  // the same host cos / sin terrain_enqueue forms for a patch's yaw
+    j.yaw_s = sin(yaw);
+    j.dist_x = dist_x;
+    j.dist_y = dist_y;
+    j.inv_dx = 1.0 / dist_x;
+    j.inv_dy = 1.0 / dist_y;
+    j.ray_z = ray_z;
+    // the raycast patch is ray_xy's lattice: four points per nearest-neighbour query, one block per leg
+    // (SRBD_TAMOLS_LATTICE=0: every point scanned, 16 blocks per leg -- the same results)
+    const char* le = getenv("SRBD_TAMOLS_LATTICE");
+    const bool lattice_env = !(le && le[0] == '0');
+    j.lattice = lattice_env && std::isfinite(dist_x) && std::isfinite(dist_y) && dist_x > 0.0 && dist_y > 0.0 &&
+                std::isfinite(j.yaw_c) && std::isfinite(j.yaw_s);
 }
 
 extern "C" int srbd_tamols_run(srbd_tamols_ctx* t, const double* hm, int32_t rows, int32_t cols, const double* seeds,
@@ -2376,26 +2420,132 @@ extern "C" int srbd_tamols_run_terrain(srbd_tamols_ctx* t, srbd_terrain* ter, do
     if (int rc = tamols_reserve(t, nc)) return rc;
     TamolsJob j;
     memset(&j, 0, sizeof(j));
-    j.use_terrain = 1;
-    j.t = ter->dev;
-    j.yaw_c = cos(yaw);  // the same host cos / sin terrain_enqueue forms for a patch's yaw
-    j.yaw_s = sin(yaw);
-    j.dist_x = dist_x;
-    j.dist_y = dist_y;
-    j.inv_dx = 1.0 / dist_x;
-    j.inv_dy = 1.0 / dist_y;
-    j.ray_z = ray_z;
-    // the raycast patch is ray_xy's lattice: four points per nearest-neighbour query, one block per leg
-    // (SRBD_TAMOLS_LATTICE=0: every point scanned, 16 blocks per leg -- the same results)
-    const char* le = getenv("SRBD_TAMOLS_LATTICE");
-    const bool lattice_env = !(le && le[0] == '0');
-    j.lattice = lattice_env && std::isfinite(dist_x) && std::isfinite(dist_y) && dist_x > 0.0 && dist_y > 0.0 &&
-                std::isfinite(j.yaw_c) && std::isfinite(j.yaw_s);
+    tamols_terrain_job(j, ter, yaw, dist_x, dist_y, ray_z);
     j.hm_out = out_hm ? t->d_hm_host : nullptr;
     const int rc = tamols_launch_wait(t, j, seeds, hips, vel, base, contact, feet, p, rows, cols, out_fh, out_box,
                                       out_valid, out_scores, out_seedh);
     if (!rc && out_hm) memcpy(out_hm, t->h_hm, sizeof(double) * 12 * nc);
     return rc;
+}
+
+// srbd_foothold_mpc_step chained on the device (srbd_host.cpp calls this first; 1 = not taken, the caller runs the
+// sequential chain).  The TAMOLS launch and the MPC step's rollout launch go onto the MPC context's stream back to
+// back: the TAMOLS launch also writes the step's device StepInput (TamolsJob::Feed -- the reference's feet = the
+// footholds, swing feet = the footholds, cost_feet), so the host waits once, for the step, instead of for TAMOLS,
+// then staging the step, then for the step.  The inputs are the ones the sequential chain stages (fill_input over
+// prepare_state's outputs rounded to float), so the results are the same bits (tests/test_gpu_foothold_step.py).
+// Taken for unsharded, unarmed MPPI / random-sampling contexts without the gait-adaptive rollout or cost terms, the
+// step input fitting the kernel argument (P <= KSI_MAXP); SRBD_FOOTHOLD_CHAIN=0 turns it off.
+extern "C" int srbd_foothold_chain(srbd_tamols_ctx* t, srbd_terrain* ter, const srbd_tamols_params* p, srbd_ctx* c,
+                                   srbd_foothold_io* io, const float* contact, int32_t stride, float* best,
+                                   int32_t ppl, uint64_t seed, uint64_t counter, srbd_result* out) {
+    constexpr int DECLINED = 1;
+    const ModelConst& mc = c->mc;
+    const char* env = getenv("SRBD_FOOTHOLD_CHAIN");
+    if ((env && env[0] == '0') || c->cfg.world_size > 1 || c->arm_mode || mc.method == SRBD_CEM_MPPI || mc.ga ||
+        mc.cost_on || mc.P > KSI_MAXP || t->device != c->cfg.device_id || ter->device != t->device)
+        return DECLINED;
+    const int rows = io->rows, cols = io->cols, nc = rows * cols;
+    const int nwords = (int)((offsetof(StepInput, best) + sizeof(float) * (size_t)mc.P) / 16);
+    if (rows < 1 || cols < 1 || nc > TAMOLS_MAXCAND || nwords > TAMOLS_THREADS || stride < mc.H) return DECLINED;
+    for (int l = 0; l < 4; ++l)  // prepare_state's lift-off zeroing would index past best[P]
+        if ((l + 1) * (size_t)ppl > (size_t)mc.P) return DECLINED;
+    arm_cancel_others();
+    HIP_TRY(c, hipSetDevice(c->cfg.device_id));
+    if (int rc = tamols_reserve(t, nc)) return fail(c, rc, t->err);
+    // prepare_state's warm-start zeroing (NMPC:563-627) reads only the contacts; the feet it substitutes are the
+    // footholds, written on the device by the feed
+    for (int l = 0; l < 4; ++l)
+        if (io->previous_contact[l] == 1.0 && io->current_contact[l] == 0.0)
+            for (int k = 0; k < ppl; ++k) best[l * ppl + k] = 0.0f;
+    float st[24], rf[24];
+    for (int i = 0; i < 24; ++i) st[i] = (float)io->state_in[i];
+    for (int i = 0; i < 12; ++i) {
+        rf[i] = (float)io->ref_base[i];
+        rf[12 + i] = 0.0f;  // the feed's
+    }
+    int rc = fill_input(&c->cfg, mc, c->h_in, st, rf, contact, stride, best, nullptr, seed, counter);
+    if (rc) return fail(c, rc, "invalid step arguments");
+    c->h_in->noise_scaled = 0;
+    c->h_out->status = 0;  // check_handoff
+    StepInputK ksi;
+    fill_ksi(c, &ksi);
+    int32_t cint[4];
+    for (int l = 0; l < 4; ++l) cint[l] = (int32_t)io->current_contact[l];
+    TamolsJob j;
+    memset(&j, 0, sizeof(j));
+    tamols_terrain_job(j, ter, io->yaw, io->dist_x, io->dist_y, io->ray_z);
+    j.hm_out = io->heightmaps ? t->d_hm_host : nullptr;
+    tamols_job_fill(t, j, io->seeds, io->hips, io->forward_vel, io->state_in, cint, io->state_in + 12, p, rows, cols,
+                    io->scores != nullptr);
+    j.feed.in = c->d_in;
+    j.feed.fh = t->d_feed;
+    j.feed.cnt = t->d_cnt + 4;
+    j.feed.nwords = nwords;
+    for (int l = 0; l < 4; ++l) j.feed.swing[l] = io->current_contact[l] == 0.0;
+    for (int i = 0; i < 12; ++i) j.feed.q[i] = c->cfg.q_diag[12 + i];
+    // cost_feet = sum (e q) e over the feet: with zero feet weights it is +0 whenever every e is finite -- the case
+    // when the seeds, the state's feet, the patch geometry and the scene are bounded (the footholds, candidates or
+    // seeds at raycast heights, then round to finite floats) -- so the host's value stands and each leg writes its
+    // own feet; else the last leg sums it on the device
+    {
+        const auto ok = [](double v) { return std::isfinite(v) && fabs(v) < 1e30; };
+        // a ray misses (miss_z) unless the ground plane lies at or below its start
+        const bool hits = ter->dev.has_ground && ter->dev.ground_z <= io->ray_z;
+        bool known = ter->bounded && ok(io->ray_z) && ok(io->dist_x * rows) && ok(io->dist_y * cols) &&
+                     (hits || ok(ter->dev.miss_z));
+        for (int i = 0; i < 12 && known; ++i)
+            known = j.feed.q[i] == 0.0f && ok(io->seeds[i]) && ok(io->state_in[12 + i]);
+        j.feed.cf_known = known;
+        if (known) {  // fill_input's sum over the staged (finite) feet is +0 already; stated here
+            const float z = 0.0f;
+            c->h_in->cost_feet = z;
+            memcpy(ksi.head + offsetof(StepInput, cost_feet), &z, sizeof(z));
+        }
+    }
+    // the step's draws: the previous step's prefetch, else drawn now -- queued ahead of TAMOLS (they do not read it)
+    int buf = 0;
+    if ((rc = acquire_noise(c, nullptr, seed, counter, &buf))) return rc;
+    launch_tamols_fused(j, c->stream, &ksi);
+    HIP_TRY(c, hipGetLastError());
+    const bool fuse = fusable(c);
+    const Publish pub{c->d_flag, ++c->seq, nullptr};
+    const int nflags = enqueue_device_step(c, buf, nullptr, c->d_out_host, 0, 0, fuse, pub);
+    HIP_TRY(c, hipGetLastError());
+    if (fuse) {
+        c->pref_valid = true;
+        c->pref_buf = 1 - buf;
+        c->pref_seed = next_seed(c, seed);
+        c->pref_ctr = counter + 1;
+    }
+    // a launch that stopped part-way can leave the feed's arrival count behind: cleared on every failure from here
+    const auto failed = [&](int r) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipMemset(t->d_cnt + 4, 0, sizeof(unsigned));
+        return r;
+    };
+    if ((rc = nflags == TAGGED_OUT ? wait_tagged(c, pub.seq) : wait_published(c, pub.seq, nflags))) return failed(rc);
+    if (!tamols_published(t, j.seq)) {  // stream order: TAMOLS completed before the step began
+        (void)hipStreamSynchronize(c->stream);
+        if (!tamols_published(t, j.seq))
+            return failed(fail(c, SRBD_E_HIP, "TAMOLS launch completed without publishing its outputs"));
+    }
+    tamols_outputs(t, nc, io->footholds, io->boxes, io->valid, io->scores, io->seed_heights);
+    if (io->heightmaps) memcpy(io->heightmaps, t->h_hm, sizeof(double) * 12 * nc);
+    io->stage = 1;
+    // prepare_state's outputs as the sequential chain reports them (the step used their float roundings)
+    memcpy(io->ref_out, io->ref_base, sizeof(double) * 12);
+    memcpy(io->ref_out + 12, io->footholds, sizeof(double) * 12);
+    memcpy(io->state_out, io->state_in, sizeof(double) * 24);
+    for (int l = 0; l < 4; ++l)
+        if (io->current_contact[l] == 0.0) memcpy(io->state_out + 12 + 3 * l, io->footholds + 3 * l, sizeof(double) * 3);
+    io->stage = 2;
+    if ((rc = check_handoff(c))) return failed(rc);
+    c->input_ready = true;
+    copy_out(c, best, nullptr, out);
+    io->stage = 3;
+    ++c->foothold_chained;
+    return SRBD_OK;
 }
 
 // Diagnostic: stamp the phases of the following calls (enable != 0), or read the last call's stamps:

@@ -142,9 +142,15 @@ extern "C" int srbd_prepare_state(const double state_in[24], const double ref_in
     return SRBD_OK;
 }
 
+// srbd_api.hip: the chained form (TAMOLS writes the step's device input; one host wait), 1 when not taken.
+extern "C" int srbd_foothold_chain(srbd_tamols_ctx* t, srbd_terrain* ter, const srbd_tamols_params* p, srbd_ctx* c,
+                                   srbd_foothold_io* io, const float* contact, int32_t stride, float* best,
+                                   int32_t ppl, uint64_t seed, uint64_t counter, srbd_result* out);
+
 // helpers/foothold_pipeline.py TamolsMpcStep.step in one host call (include/srbd_mpc.h).  The base position and
 // the current feet TAMOLS reads are the state's own (state_in[0:3], state_in[12:24]); its contact flags are the
-// current contact truncated to int32 (VFA's astype).
+// current contact truncated to int32 (VFA's astype).  Chained on the device where the context allows it, else the
+// calls in sequence below; the same results either way.
 extern "C" int srbd_foothold_mpc_step(srbd_tamols_ctx* tamols, srbd_terrain* terrain, const srbd_tamols_params* params,
                                       srbd_ctx* ctx, srbd_foothold_io* io, const float* contact,
                                       int32_t contact_stride, float* best_params, int32_t params_per_leg,
@@ -152,6 +158,9 @@ extern "C" int srbd_foothold_mpc_step(srbd_tamols_ctx* tamols, srbd_terrain* ter
     if (!tamols || !terrain || !params || !ctx || !io || !contact || !best_params || !out || params_per_leg < 1)
         return SRBD_E_INVALID;
     io->stage = 0;
+    const int chained = srbd_foothold_chain(tamols, terrain, params, ctx, io, contact, contact_stride, best_params,
+                                            params_per_leg, seed, counter, out);
+    if (chained != 1) return chained;
     int32_t cint[4];
     for (int l = 0; l < 4; ++l) cint[l] = (int32_t)io->current_contact[l];
     int rc = srbd_tamols_run_terrain(tamols, terrain, io->yaw, io->rows, io->cols, io->dist_x, io->dist_y, io->ray_z,

@@ -206,6 +206,9 @@ struct srbd_terrain {
     size_t cap_job = 0, cap_out = 0;
     double* h_job = nullptr;  // pinned staging of the job inputs
     srbd::TerrainDev dev{};
+    // every scene value (primitives, height field, the ground height) finite and below 1e30 in magnitude, so every
+    // raycast height that hits is a finite double well inside float's range (srbd_foothold_chain's cost_feet)
+    bool bounded = false;
     std::string err;
 };
 
@@ -240,8 +243,23 @@ struct TamolsJob {
     uint32_t* flag;      // host-mapped publish words, one per leg
     uint32_t seq;
     uint64_t* dbg;       // diagnostic phase stamps (4 x TAMOLS_BPL x 8) or NULL
+    // The chained foothold step (srbd_foothold_mpc_step): the launch also writes the MPC step's device StepInput,
+    // so the rollout launch queued behind it needs no host round trip.  Block (0, 0) copies the host step input
+    // (the kernel argument, launch_tamols_fused's ksi) except the words holding the feet and cost_feet; the last
+    // leg to finish writes those: the reference's feet = the footholds, swing feet of the state = the footholds
+    // (prepare_state), cost_feet over them as fill_input sums it.
+    struct Feed {
+        StepInput* in;   // device StepInput of the MPC context (NULL: no feed)
+        double* fh;      // 12 doubles of device scratch: the legs' footholds
+        unsigned* cnt;   // leg arrival counter (device, zero between calls)
+        int nwords;      // 16-byte words of StepInput to copy (the prefix and best[P])
+        int swing[4];    // current contact == 0: the state's foot is the foothold
+        float q[12];     // q_diag[12..24)
+        int cf_known;    // the host's cost_feet stands (zero feet weights, bounded inputs): each leg writes its own
+                         // feet, no cross-leg step
+    } feed;
 };
-void launch_tamols_fused(const TamolsJob& j, hipStream_t s);
+void launch_tamols_fused(const TamolsJob& j, hipStream_t s, const StepInputK* ksi = nullptr);
 int tamols_prepare();  // once per context: the staged scene's dynamic LDS limit (0 on success)
 
 }  // namespace srbd

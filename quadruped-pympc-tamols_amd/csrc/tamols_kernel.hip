@@ -238,9 +238,27 @@ constexpr int TAMOLS_SLICE = TAMOLS_MAXCAND;
 static_assert(TAMOLS_BPL <= 64, "the merge loads one slice partial per lane of one wave");
 
 __device__ void tamols_leg_out(const TamolsJob& j, int leg, int bi, const double* px, const double* py, double bh,
-                               double seedh);
+                               double seedh, bool feed);
 
-__global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const TamolsJob j) {
+// StepInput's 16-byte words the feed's last leg writes (TamolsJob::Feed): the state's and the reference's feet,
+// and the word holding cost_feet.
+constexpr int FEED_SF = (int)(offsetof(StepInput, state) + 48) / 16;
+constexpr int FEED_RF = (int)(offsetof(StepInput, ref) + 48) / 16;
+constexpr int FEED_CF = (int)offsetof(StepInput, cost_feet) / 16;
+static_assert((offsetof(StepInput, state) + 48) % 16 == 0 && (offsetof(StepInput, ref) + 48) % 16 == 0,
+              "the feet are whole 16-byte words");
+static_assert(FEED_CF != FEED_SF && FEED_CF != FEED_SF + 1 && FEED_CF != FEED_SF + 2 && FEED_CF != FEED_RF &&
+                  FEED_CF != FEED_RF + 1 && FEED_CF != FEED_RF + 2,
+              "cost_feet lies outside the feet words");
+__device__ __forceinline__ bool feed_patch_word(int w, bool cf_known) {
+    return (w >= FEED_SF && w < FEED_SF + 3) || (w >= FEED_RF && w < FEED_RF + 3) || (w == FEED_CF && !cf_known);
+}
+
+
+// FEED: the kernel's first argument is the MPC step's input (StepInputK), read in the kernarg segment.
+template <bool FEED>
+__global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const std::conditional_t<FEED, StepInputK, KsNone> ksi,
+                                                                       const TamolsJob j) {
     __shared__ double px[TAMOLS_MAXCAND], py[TAMOLS_MAXCAND], pz[TAMOLS_MAXCAND];
     __shared__ double nn[TAMOLS_SLICE * TAMOLS_NQ + 1];
     __shared__ double sc[TAMOLS_SLICE];
@@ -259,6 +277,22 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                  \
         j.dbg[((size_t)leg * NB + b) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                  \
     }
+    if constexpr (FEED) {  // grid row 4: the MPC step's input, less the words the last leg writes (one writer per word)
+        (void)ksi;
+        if (leg == 4) {
+            if (b == 0 && tid < j.feed.nwords && !feed_patch_word(tid, j.feed.cf_known)) {
+                const auto src = (const __attribute__((address_space(4))) uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
+                uint4 v;
+                v.x = src[4 * tid];
+                v.y = src[4 * tid + 1];
+                v.z = src[4 * tid + 2];
+                v.w = src[4 * tid + 3];
+                reinterpret_cast<uint4*>(j.feed.in)[tid] = v;
+            }
+            return;
+        }
+    }
+
     TAM_STAMP(0);
 
     // ---- patch (raycast, or the caller's) -> LDS; block 0 also hands the raycast patch back
@@ -512,7 +546,8 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
                 bs = rbest[w];
                 bi = rhit[w];
             }
-        tamols_leg_out(j, leg, bs < INFINITY ? bi : -1, px, py, bs < INFINITY ? nn[bi * TAMOLS_NQ] : 0.0, nn[nloc - 1]);
+        tamols_leg_out(j, leg, bs < INFINITY ? bi : -1, px, py, bs < INFINITY ? nn[bi * TAMOLS_NQ] : 0.0, nn[nloc - 1],
+                       FEED);
         TAM_STAMP(5);
         return;
     }
@@ -563,25 +598,52 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const Tamo
     const double seedh = __shfl(pseed, 0);
     if (tid != 0) return;
     __hip_atomic_store(j.cnt + leg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next call
-    tamols_leg_out(j, leg, bi, px, py, bh, seedh);
+    tamols_leg_out(j, leg, bi, px, py, bh, seedh, FEED);
     TAM_STAMP(5);
 #undef TAM_STAMP
+}
+
+// The feed's last leg (one lane): the feet words and the cost_feet word of the MPC step's StepInput.  The
+// footholds are rounded to float as the host's step staging rounds them; cost_feet is fill_input's sum
+// cf = cf + (e * q) * e over the twelve feet coordinates, e = state - ref, in float without contraction.
+__device__ void tamols_feed_finish(const TamolsJob& j) {
+    const TamolsJob::Feed& f = j.feed;
+    const auto kf = (const __attribute__((address_space(4))) float*)__builtin_amdgcn_kernarg_segment_ptr();
+    float st[12], rf[12];
+    for (int i = 0; i < 12; ++i) {
+        const double h = __hip_atomic_load(f.fh + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        rf[i] = (float)h;
+        st[i] = f.swing[i / 3] ? rf[i] : kf[4 * FEED_SF + i];
+    }
+    float cf = 0.0f;
+    for (int i = 0; i < 12; ++i) {
+        const float e = __fsub_rn(st[i], rf[i]);
+        cf = __fadd_rn(cf, __fmul_rn(__fmul_rn(e, f.q[i]), e));
+    }
+    float* in = reinterpret_cast<float*>(f.in);
+    for (int i = 0; i < 12; ++i) {
+        in[4 * FEED_SF + i] = st[i];
+        in[4 * FEED_RF + i] = rf[i];
+    }
+    constexpr int cfi = (int)offsetof(StepInput, cost_feet) / 4;
+    for (int i = 4 * FEED_CF; i < 4 * FEED_CF + 4; ++i) in[i] = i == cfi ? cf : kf[i];
 }
 
 // The leg's outputs (one lane): foothold, box and validity of candidate bi (-1: none feasible), its query height bh,
 // the seed height; then the leg publishes the call's sequence number on its own host word.
 __device__ void tamols_leg_out(const TamolsJob& j, int leg, int bi, const double* px, const double* py, double bh,
-                               double seedh) {
+                               double seedh, bool feed) {
     const TamolsArgs& a = j.a;
     const srbd_tamols_params& p = a.p;
     double* F = j.out + 3 * leg;  // [fh 12 | box 24 | seedh 4 | valid 4 x int32]
     double* B = j.out + 12 + 6 * leg;
     int* valid = reinterpret_cast<int*>(j.out + 40);
+    double f[3];
     if (bi >= 0) {  // VFA:193-222
         const double cx = px[bi], cy = py[bi], cz = bh + 0.005;
-        F[0] = cx;
-        F[1] = cy;
-        F[2] = cz;
+        f[0] = cx;
+        f[1] = cy;
+        f[2] = cz;
         B[0] = cx - p.box_dx;
         B[1] = cy - p.box_dy;
         B[2] = cz;
@@ -590,13 +652,31 @@ __device__ void tamols_leg_out(const TamolsJob& j, int leg, int bi, const double
         B[5] = cz;
         valid[leg] = 1;
     } else {  // VFA:223-228: no feasible candidate -> the seed at its terrain height
-        F[0] = a.seeds[3 * leg];
-        F[1] = a.seeds[3 * leg + 1];
-        F[2] = seedh;
+        f[0] = a.seeds[3 * leg];
+        f[1] = a.seeds[3 * leg + 1];
+        f[2] = seedh;
         for (int i = 0; i < 6; ++i) B[i] = NAN;
         valid[leg] = 0;
     }
+    for (int i = 0; i < 3; ++i) F[i] = f[i];
     j.out[36 + leg] = seedh;
+    if (feed && j.feed.cf_known) {  // this leg's feet of the step input (the words' other floats are other legs')
+        const auto kf = (const __attribute__((address_space(4))) float*)__builtin_amdgcn_kernarg_segment_ptr();
+        float* in = reinterpret_cast<float*>(j.feed.in);
+        for (int i = 0; i < 3; ++i) {
+            const float r = (float)f[i];
+            in[4 * FEED_RF + 3 * leg + i] = r;
+            in[4 * FEED_SF + 3 * leg + i] = j.feed.swing[leg] ? r : kf[4 * FEED_SF + 3 * leg + i];
+        }
+    } else if (feed) {  // the foothold write-through into the feed's scratch; the last leg to arrive writes the feet
+        for (int i = 0; i < 3; ++i)
+            __hip_atomic_store(j.feed.fh + 3 * leg + i, f[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (__hip_atomic_fetch_add(j.feed.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3u) {
+            __hip_atomic_store(j.feed.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next call
+            tamols_feed_finish(j);
+        }
+    }
     __threadfence_system();  // this leg's host-mapped outputs and its blocks' scores / patch (drained before)
     // the leg publishes on its own word: the host waits for all four (no cross-leg counter round trip)
     __hip_atomic_store(j.flag + leg, j.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -606,19 +686,25 @@ __device__ void tamols_leg_out(const TamolsJob& j, int leg, int bi, const double
 // TAMOLS_LDS_PRIMS x 80 B = 80 KB of dynamic LDS on top of ~23 KB static, above the default dynamic-LDS
 // limit a launch gets without the attribute (round-2 advisor finding; gfx950 has 160 KB per CU).
 int tamols_prepare() {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&tamols_fused_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)((sizeof(srbd_terrain_prim) + 2 * sizeof(double)) * TAMOLS_LDS_PRIMS));
-    return e == hipSuccess ? 0 : -1;
+    const int lds = (int)((sizeof(srbd_terrain_prim) + 2 * sizeof(double)) * TAMOLS_LDS_PRIMS);
+    const hipError_t e0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&tamols_fused_kernel<false>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    const hipError_t e1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&tamols_fused_kernel<true>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    return e0 == hipSuccess && e1 == hipSuccess ? 0 : -1;
 }
 
-void launch_tamols_fused(const TamolsJob& j, hipStream_t s) {
+// ksi != NULL: the feed (TamolsJob::Feed) -- the MPC step's input by value, the kernel's first argument.
+void launch_tamols_fused(const TamolsJob& j, hipStream_t s, const StepInputK* ksi) {
     // a raycast lattice patch: one block per leg (four points per query, no cross-block merge)
     const int nb = j.lattice ? 1 : (j.a.ncand < TAMOLS_BPL ? j.a.ncand : TAMOLS_BPL);
     const int np = j.use_terrain ? j.t.nprims : 0;
     // the staged scene's dynamic LDS (not in lattice mode: its culled list lives in the static query stage)
     const size_t smem = (!j.lattice && np > 0 && np <= TAMOLS_LDS_PRIMS) ? (sizeof(srbd_terrain_prim) + 2 * sizeof(double)) * np : 0;
-    hipLaunchKernelGGL(tamols_fused_kernel, dim3(nb, 4), dim3(TAMOLS_THREADS), smem, s, j);
+    if (ksi && j.feed.in)  // a fifth grid row copies the step input (off the legs' critical path)
+        hipLaunchKernelGGL(tamols_fused_kernel<true>, dim3(nb, 5), dim3(TAMOLS_THREADS), smem, s, *ksi, j);
+    else
+        hipLaunchKernelGGL(tamols_fused_kernel<false>, dim3(nb, 4), dim3(TAMOLS_THREADS), smem, s, KsNone{0}, j);
 }
 
 }  // namespace srbd

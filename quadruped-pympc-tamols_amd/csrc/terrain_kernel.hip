@@ -88,6 +88,19 @@ extern "C" int srbd_terrain_create(int32_t device_id, const srbd_terrain_prim* p
     t->dev.hf_y0 = hf_y0;
     t->dev.hf_dx = hf_dx;
     t->dev.hf_dy = hf_dy;
+    {
+        const auto ok = [](double v) { return std::isfinite(v) && fabs(v) < 1e30; };
+        bool b = !has_ground || ok(ground_z);  // miss_z: checked per call (a ray below the ground misses)
+        for (int q = 0; b && q < nprims; ++q) {
+            const srbd_terrain_prim& p = prims[q];
+            b = ok(p.cx) && ok(p.cy) && ok(p.cz) && ok(p.a) && ok(p.b) && ok(p.c) && ok(p.yaw);
+        }
+        if (hfield) {
+            b = b && ok(hf_x0) && ok(hf_y0) && ok(hf_dx) && ok(hf_dy);
+            for (size_t i = 0; b && i < (size_t)hf_nx * hf_ny; ++i) b = ok(hfield[i]);
+        }
+        t->bounded = b;
+    }
     auto bad = [&](hipError_t e) {
         const std::string m = std::string("terrain upload: ") + hipGetErrorString(e);
         srbd_terrain_destroy(t);

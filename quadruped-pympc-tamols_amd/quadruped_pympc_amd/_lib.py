@@ -100,6 +100,7 @@ SIGNATURES = {
     "srbd_armed_refired": (_I, [_P, C.POINTER(C.c_int64)]),
     "srbd_debug_arm_delay": (_I, [_P, C.c_uint32]),
     "srbd_debug_split_drop": (_I, [_P]),
+    "srbd_foothold_chained": (_I, [_P, C.POINTER(C.c_int64)]),
     "srbd_record_floats": (_I, [_P]),
     "srbd_record_floats_host": (_I, [C.POINTER(SrbdConfig)]),
     "srbd_shard_rows": (_I, [C.c_int64, _I, _I, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
@@ -623,6 +624,12 @@ class Context:
     def debug_split_drop(self):
         """srbd_debug_split_drop (tests): the next column-split merge's hand-off times out (the step fails)."""
         self.check(lib.srbd_debug_split_drop(self.h), "srbd_debug_split_drop")
+
+    def foothold_chained(self) -> int:
+        """srbd_foothold_chained: srbd_foothold_mpc_step calls on this context that ran chained on the device."""
+        a = C.c_int64(0)
+        self.check(lib.srbd_foothold_chained(self.h, C.byref(a)), "srbd_foothold_chained")
+        return int(a.value)
 
     def set_stream(self, stream_handle: int | None):
         """Launch on a caller-owned hipStream_t; None (or 0, the legacy null stream) -> the context's own."""
