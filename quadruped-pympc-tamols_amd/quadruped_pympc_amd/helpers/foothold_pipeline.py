@@ -90,7 +90,8 @@ class TamolsMpcStep:
                            ("state_in", "ref_base", "seeds", "hips", "forward_vel", "current_contact",
                             "previous_contact", "footholds", "boxes", "seed_heights", "valid")}
             self._io_scores = np.zeros((4, g.num_rows * g.num_cols))
-            self._io_hm = np.zeros((4, g.num_rows, g.num_cols, 3))
+            # (4, rows, cols, 3) as the call writes them, held as the maps' (rows, cols, 1, 3) layout
+            self._io_hm = np.zeros((4, g.num_rows, g.num_cols, 1, 3))
             io.scores, io.heightmaps = self._io_scores.ctypes.data, self._io_hm.ctypes.data
             self._io_ref = C.byref(io)
         return io
@@ -154,22 +155,26 @@ class TamolsMpcStep:
         already built, or None."""
         iface, ctrl, vfa, io, a = self.iface, self.iface.controller, self.vfa, self._io, self._io_np
         ctx = ctrl.context
-        vfa.reset()
-        if io.stage >= 1:
+        if io.stage >= 1:  # (compute_adaptation's reset, then its results: initialized again)
             hm = self._io_hm.copy()
-            for i, m in enumerate(self.heightmaps):
-                m._data, m.pending = hm[i][:, :, None, :], None
+            hms = self.heightmaps
+            hms.FL._data, hms.FR._data, hms.RL._data, hms.RR._data = hm
+            hms.FL.pending = hms.FR.pending = hms.RL.pending = hms.RR.pending = None
             fh = a["footholds"].reshape(4, 3).copy()
-            boxes, valid = a["boxes"].reshape(4, 2, 3), a["valid"]
+            f0, f1, f2, f3 = fh
+            valid = io.valid
             constraints = vfa.footholds_constraints
-            for i, n in enumerate(LEGS):
-                if valid[i]:
-                    constraints[n] = [boxes[i, 0].copy(), boxes[i, 1].copy()]
+            if valid[0] or valid[1] or valid[2] or valid[3]:
+                boxes = a["boxes"].reshape(4, 2, 3).copy()  # one copy; each leg's box corners are views of it
+                for i, b in enumerate(boxes):
+                    if valid[i]:
+                        constraints[LEGS[i]] = [b[0], b[1]]
             vfa.last_scores = self._io_scores.copy()
-            vfa.update_footholds_adaptation(LegsAttr(fh[0], fh[1], fh[2], fh[3]))
+            vfa.footholds_adaptation, vfa.initialized = LegsAttr(f0, f1, f2, f3), True
             self._ref_state, self._ref_src = None, (ref_base, fh, LegsAttr(*constraints))
             self.last_constraints = constraints
         else:  # the patches stay pending around the seeds (update_height_map ran, the search did not)
+            vfa.reset()
             for i, m in enumerate(self.heightmaps):
                 m._data, m.pending = None, (seeds[3 * i:3 * i + 3].copy(), io.yaw)
         if io.stage >= 2:
@@ -187,9 +192,7 @@ class TamolsMpcStep:
         else:
             g = np.array(res.grf, dtype=np.float32).reshape(4, 3) * current_contact[:, None]  # as compute_control
             pred = np.array(res.predicted_state, dtype=np.float32)
-        grfs = LegsAttr(FL=g[0], FR=g[1], RL=g[2], RR=g[3])
-        footholds = LegsAttr(FL=fh[0], FR=fh[1], RL=fh[2], RR=fh[3])
-        return grfs, footholds, None, None, None, 1.4, pred
+        return LegsAttr(*g), LegsAttr(f0, f1, f2, f3), None, None, None, 1.4, pred
 
     def step(self, state_current: dict, ref_feet_pos: LegsAttr, hip_pos: LegsAttr, ref_base: dict,
              contact_sequence: np.ndarray, base_lin_vel: np.ndarray, base_ori_euler_xyz: np.ndarray,
