@@ -384,7 +384,10 @@ extern "C" int srbd_create(const srbd_config* cfg, srbd_ctx** out) {
     // the four-lane kernel addresses noise through a buffer descriptor (31-bit byte offsets)
     if ((long long)mc.P * mc.ldn * 4 >= (1LL << 31)) c->mode = ROLLOUT_THREAD;
     c->threads = c->mode == ROLLOUT_QUAD ? 4 * quad_samples_per_block(mc.n_local) : rollout_threads(mc.n_local);
-    c->ks = ks_ok(mc, c->mode);  // srbd_step, and the xGMI sharded step (xg_step)
+    {  // srbd_step, and the xGMI sharded step (xg_step); SRBD_KS=0 at create: the upload kernel instead (A/B)
+        const char* e = getenv("SRBD_KS");
+        c->ks = ks_ok(mc, c->mode) && !(e && e[0] == '0');
+    }
     const int spb = rollout_spb(c->mode, c->threads);  // samples per rollout block
     c->nblocks = (mc.n_local + spb - 1) / spb;
     c->lpb = spb / LEAF_ROWS;
@@ -2196,8 +2199,8 @@ struct srbd_tamols_ctx {
     double* d_part = nullptr;  // per-block partials
     unsigned* d_cnt = nullptr;  // block / leg counters, [4] the feed's leg arrivals (zero between calls)
     double* d_feed = nullptr;   // the feed's footholds (srbd_foothold_mpc_step's chained form)
-    uint32_t* h_flag = nullptr;
-    uint32_t* d_flag = nullptr;
+    uint64_t* h_outt = nullptr;  // host-mapped tagged outputs, 4 x TAMOLS_OUT_WORDS (tamols_leg_out)
+    uint64_t* d_outt = nullptr;
     uint32_t seq = 0;
     size_t cap_cand = 0;
     uint64_t* d_dbg = nullptr;  // srbd_tamols_phases: stamps of the last call
@@ -2214,9 +2217,9 @@ extern "C" int srbd_tamols_create(int32_t device_id, srbd_tamols_ctx** out) {
     t->device = device_id;
     bool ok = hipSetDevice(device_id) == hipSuccess &&
               hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) == hipSuccess &&
-              hipHostMalloc((void**)&t->h_flag, sizeof(uint32_t) * 4, hipHostMallocMapped | hipHostMallocCoherent) ==
-                  hipSuccess &&
-              hipHostGetDevicePointer((void**)&t->d_flag, t->h_flag, 0) == hipSuccess &&
+              hipHostMalloc((void**)&t->h_outt, sizeof(uint64_t) * 4 * TAMOLS_OUT_WORDS,
+                            hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+              hipHostGetDevicePointer((void**)&t->d_outt, t->h_outt, 0) == hipSuccess &&
               hipMalloc((void**)&t->d_part, sizeof(double) * 4 * TAMOLS_BPL * 4) == hipSuccess &&
               hipMalloc((void**)&t->d_cnt, sizeof(unsigned) * 8) == hipSuccess &&
               hipMemset(t->d_cnt, 0, sizeof(unsigned) * 8) == hipSuccess &&
@@ -2226,7 +2229,7 @@ extern "C" int srbd_tamols_create(int32_t device_id, srbd_tamols_ctx** out) {
         srbd_tamols_destroy(t);
         return fail(nullptr, SRBD_E_HIP, "TAMOLS context allocation failed");
     }
-    for (int l = 0; l < 4; ++l) __atomic_store_n(t->h_flag + l, 0u, __ATOMIC_RELEASE);  // one word per leg
+    for (int w = 0; w < 4 * TAMOLS_OUT_WORDS; ++w) __atomic_store_n(t->h_outt + w, (uint64_t)0, __ATOMIC_RELEASE);
     *out = t;
     return SRBD_OK;
 }
@@ -2242,7 +2245,7 @@ extern "C" void srbd_tamols_destroy(srbd_tamols_ctx* t) {
     (void)hipFree(t->d_dbg);
     if (t->h_out) (void)hipHostFree(t->h_out);
     if (t->h_hm) (void)hipHostFree(t->h_hm);
-    if (t->h_flag) (void)hipHostFree(t->h_flag);
+    if (t->h_outt) (void)hipHostFree(t->h_outt);
     if (t->stream) (void)hipStreamDestroy(t->stream);
     delete t;
 }
@@ -2305,28 +2308,39 @@ static void tamols_job_fill(srbd_tamols_ctx* t, TamolsJob& j, const double* seed
     j.rows = rows;
     j.cols = cols;
     j.scores = scores ? t->d_out_host : nullptr;
-    j.out = t->d_out_host + 4 * (size_t)nc;
+    j.outt = t->d_outt;
     j.part = t->d_part;
     j.cnt = t->d_cnt;
-    j.flag = t->d_flag;
     j.seq = ++t->seq;
     j.dbg = t->d_dbg;
 }
 
-static bool tamols_published(const srbd_tamols_ctx* t, uint32_t seq) {  // every leg's word holds the call's number
+// Every leg's output words carry the call's number (a word is one 8-byte store: a tagged word holds that call's value;
+// checked from each leg's last word, the one the leg stores last in lane order).
+static bool tamols_published(const srbd_tamols_ctx* t, uint32_t seq) {
     for (int l = 0; l < 4; ++l)
-        if (__atomic_load_n(t->h_flag + l, __ATOMIC_ACQUIRE) != seq) return false;
+        for (int w = TAMOLS_OUT_USED - 1; w >= 0; --w)
+            if ((uint32_t)(__atomic_load_n(t->h_outt + l * TAMOLS_OUT_WORDS + w, __ATOMIC_ACQUIRE) >> 32) != seq)
+                return false;
     return true;
 }
 
 // The outputs of a published call (host-mapped) into the caller's arrays.
 static void tamols_outputs(const srbd_tamols_ctx* t, int nc, double* out_fh, double* out_box, int32_t* out_valid,
                            double* out_scores, double* out_seedh) {
-    const double* h = t->h_out + 4 * (size_t)nc;
-    memcpy(out_fh, h, sizeof(double) * 12);
-    memcpy(out_box, h + 12, sizeof(double) * 24);
-    if (out_seedh) memcpy(out_seedh, h + 36, sizeof(double) * 4);
-    memcpy(out_valid, h + 40, sizeof(int32_t) * 4);
+    for (int l = 0; l < 4; ++l) {
+        const uint64_t* w = t->h_outt + l * TAMOLS_OUT_WORDS;
+        const auto dbl = [&](int k) {  // double k of the leg's words (low half first)
+            const uint64_t b = (w[2 * k] & 0xFFFFFFFFull) | (w[2 * k + 1] << 32);
+            double d;
+            memcpy(&d, &b, sizeof(d));
+            return d;
+        };
+        for (int k = 0; k < 3; ++k) out_fh[3 * l + k] = dbl(k);
+        for (int k = 0; k < 6; ++k) out_box[6 * l + k] = dbl(3 + k);
+        if (out_seedh) out_seedh[l] = dbl(9);
+        out_valid[l] = (int32_t)(uint32_t)w[20];
+    }
     if (out_scores) memcpy(out_scores, t->h_out, sizeof(double) * 4 * nc);
 }
 

@@ -226,6 +226,11 @@ int terrain_enqueue(srbd_terrain* t, const double* centers, const double* yaws, 
 constexpr int TAMOLS_BPL = SRBD_TAMOLS_BPL;
 constexpr int TAMOLS_THREADS = 1024;
 constexpr int TAMOLS_LDS_PRIMS = 1024;  // scenes up to this many primitives are staged in LDS (80 KB)
+// A leg's outputs as 8-byte words (seq << 32 | 32 bits), each stored once, so the host polls the words themselves
+// (no fence and flag behind them): the foothold's 3 doubles (words 0-5, low half first), the box's 6 (6-17), the seed
+// height (18-19), the validity (20).
+constexpr int TAMOLS_OUT_WORDS = 24;
+constexpr int TAMOLS_OUT_USED = 21;
 struct TamolsJob {
     TamolsArgs a;
     int use_terrain;     // 1: raycast the patches from `t` (centres = the seeds), 0: read `hm`
@@ -237,10 +242,9 @@ struct TamolsJob {
     const double* hm;    // 4 x nc x 3 (device-visible) when !use_terrain
     double* hm_out;      // 4 x nc x 3 raycast patches or NULL
     double* scores;      // 4 x nc or NULL
-    double* out;         // fh 12 | boxes 24 | seed heights 4 | valid 4 x int32 (2 doubles)
+    uint64_t* outt;      // host-mapped, 4 x TAMOLS_OUT_WORDS tagged words (tamols_leg_out)
     double* part;        // 4 x TAMOLS_BPL x 4 partials (device)
     unsigned* cnt;       // 4 per-leg block counters (device, zero between calls)
-    uint32_t* flag;      // host-mapped publish words, one per leg
     uint32_t seq;
     uint64_t* dbg;       // diagnostic phase stamps (4 x TAMOLS_BPL x 8) or NULL
     // The chained foothold step (srbd_foothold_mpc_step): the launch also writes the MPC step's device StepInput,

@@ -14,8 +14,9 @@
 //   phase C: strict-< argmin over the slice in candidate order -> (score, index, height) partial.
 // The last block of a leg to finish (per-leg counter; partials stored write-through) merges them in block
 // order (strict <, so the first minimum over all candidates wins, VFA:185-190) and writes the leg's
-// foothold, box and validity and publishes the call's sequence number in its own host word.
-// Outputs go straight to host-mapped memory; the host spins on the flag (no copy, no stream sync).
+// foothold, box and validity as words tagged with the call's sequence number (TAMOLS_OUT_WORDS).
+// Outputs go straight to host-mapped memory; the host polls the tagged words (no copy, no stream sync, no
+// fence and flag behind the data).  A raycast lattice patch takes one block per leg (TamolsJob::lattice).
 // float64 keeps the host oracle's decisions (reach bounds, argmin) bit-for-bit comparable.
 #include "terrain_ray.h"
 
@@ -511,7 +512,7 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const std:
         if (j.scores) j.scores[(size_t)leg * nc + c] = s;
     }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's score / patch stores issued and done
+    if (NB != 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's score / patch stores done
     __syncthreads();
     TAM_STAMP(3);
 
@@ -538,10 +539,16 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const std:
             rbest[tid >> 6] = bs;
             rhit[tid >> 6] = bi;
         }
+        // this wave's host-mapped score / patch stores are done (their round trip overlapped with the argmin): the
+        // leg's outputs below are stored after every wave's
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid != 0) return;
+        if (tid >= 64) return;
+        // the host reads the scores / patch once it holds the tagged outputs: a system-scope release orders the
+        // block's (completed) host stores before them -- the stores of different addresses take different paths
+        if (j.scores || j.hm_out) __threadfence_system();
         TAM_STAMP(4);
-        for (int w = 1; w < (T + 63) / 64; ++w)
+        for (int w = 1; w < (T + 63) / 64; ++w)  // every lane of wave 0 folds the same values
             if (rbest[w] < bs || (rbest[w] == bs && rhit[w] < bi)) {
                 bs = rbest[w];
                 bi = rhit[w];
@@ -596,9 +603,8 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const std:
         }
     }
     const double seedh = __shfl(pseed, 0);
-    if (tid != 0) return;
-    __hip_atomic_store(j.cnt + leg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next call
-    tamols_leg_out(j, leg, bi, px, py, bh, seedh, FEED);
+    if (tid == 0) __hip_atomic_store(j.cnt + leg, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next call's
+    tamols_leg_out(j, leg, bi, px, py, bh, seedh, FEED);  // wave 0, every lane the same fold
     TAM_STAMP(5);
 #undef TAM_STAMP
 }
@@ -629,38 +635,46 @@ __device__ void tamols_feed_finish(const TamolsJob& j) {
     for (int i = 4 * FEED_CF; i < 4 * FEED_CF + 4; ++i) in[i] = i == cfi ? cf : kf[i];
 }
 
-// The leg's outputs (one lane): foothold, box and validity of candidate bi (-1: none feasible), its query height bh,
-// the seed height; then the leg publishes the call's sequence number on its own host word.
+// The leg's outputs (wave 0, every lane holding the same bi / bh / seedh): foothold, box and validity of candidate bi
+// (-1: none feasible), its query height bh, the seed height, as TAMOLS_OUT_USED tagged words (lane w stores word w,
+// system scope), so the host reads them as they land; the host-mapped scores / patch were stored before (every wave
+// waited for its stores before the block barrier that precedes this).
 __device__ void tamols_leg_out(const TamolsJob& j, int leg, int bi, const double* px, const double* py, double bh,
                                double seedh, bool feed) {
     const TamolsArgs& a = j.a;
     const srbd_tamols_params& p = a.p;
-    double* F = j.out + 3 * leg;  // [fh 12 | box 24 | seedh 4 | valid 4 x int32]
-    double* B = j.out + 12 + 6 * leg;
-    int* valid = reinterpret_cast<int*>(j.out + 40);
-    double f[3];
+    const int lane = (int)threadIdx.x & 63;
+    double f0, f1, f2, b0, b1, b2, b3, b4, b5;
+    int valid;
     if (bi >= 0) {  // VFA:193-222
-        const double cx = px[bi], cy = py[bi], cz = bh + 0.005;
-        f[0] = cx;
-        f[1] = cy;
-        f[2] = cz;
-        B[0] = cx - p.box_dx;
-        B[1] = cy - p.box_dy;
-        B[2] = cz;
-        B[3] = cx + p.box_dx;
-        B[4] = cy + p.box_dy;
-        B[5] = cz;
-        valid[leg] = 1;
+        f0 = px[bi];
+        f1 = py[bi];
+        f2 = bh + 0.005;
+        b0 = f0 - p.box_dx;
+        b1 = f1 - p.box_dy;
+        b2 = f2;
+        b3 = f0 + p.box_dx;
+        b4 = f1 + p.box_dy;
+        b5 = f2;
+        valid = 1;
     } else {  // VFA:223-228: no feasible candidate -> the seed at its terrain height
-        f[0] = a.seeds[3 * leg];
-        f[1] = a.seeds[3 * leg + 1];
-        f[2] = seedh;
-        for (int i = 0; i < 6; ++i) B[i] = NAN;
-        valid[leg] = 0;
+        f0 = a.seeds[3 * leg];
+        f1 = a.seeds[3 * leg + 1];
+        f2 = seedh;
+        b0 = b1 = b2 = b3 = b4 = b5 = NAN;
+        valid = 0;
     }
-    for (int i = 0; i < 3; ++i) F[i] = f[i];
-    j.out[36 + leg] = seedh;
-    if (feed && j.feed.cf_known) {  // this leg's feet of the step input (the words' other floats are other legs')
+    const int d = lane >> 1;
+    const double v = d == 0 ? f0 : d == 1 ? f1 : d == 2 ? f2 : d == 3 ? b0 : d == 4 ? b1 : d == 5 ? b2
+                   : d == 6 ? b3 : d == 7 ? b4 : d == 8 ? b5 : seedh;
+    const uint64_t bits = (uint64_t)__double_as_longlong(v);
+    const uint32_t half = lane == 20 ? (uint32_t)valid : (lane & 1) ? (uint32_t)(bits >> 32) : (uint32_t)bits;
+    if (lane < TAMOLS_OUT_USED)
+        __hip_atomic_store(j.outt + (size_t)TAMOLS_OUT_WORDS * leg + lane, ((uint64_t)j.seq << 32) | half,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (!feed || lane != 0) return;
+    const double f[3] = {f0, f1, f2};
+    if (j.feed.cf_known) {  // this leg's feet of the step input (the words' other floats are other legs')
         const auto kf = (const __attribute__((address_space(4))) float*)__builtin_amdgcn_kernarg_segment_ptr();
         float* in = reinterpret_cast<float*>(j.feed.in);
         for (int i = 0; i < 3; ++i) {
@@ -668,7 +682,7 @@ __device__ void tamols_leg_out(const TamolsJob& j, int leg, int bi, const double
             in[4 * FEED_RF + 3 * leg + i] = r;
             in[4 * FEED_SF + 3 * leg + i] = j.feed.swing[leg] ? r : kf[4 * FEED_SF + 3 * leg + i];
         }
-    } else if (feed) {  // the foothold write-through into the feed's scratch; the last leg to arrive writes the feet
+    } else {  // the foothold write-through into the feed's scratch; the last leg to arrive writes the feet
         for (int i = 0; i < 3; ++i)
             __hip_atomic_store(j.feed.fh + 3 * leg + i, f[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -677,9 +691,6 @@ __device__ void tamols_leg_out(const TamolsJob& j, int leg, int bi, const double
             tamols_feed_finish(j);
         }
     }
-    __threadfence_system();  // this leg's host-mapped outputs and its blocks' scores / patch (drained before)
-    // the leg publishes on its own word: the host waits for all four (no cross-leg counter round trip)
-    __hip_atomic_store(j.flag + leg, j.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Once per TAMOLS context (srbd_tamols_create, on its device): the staged scene needs up to

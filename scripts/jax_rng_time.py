@@ -18,7 +18,7 @@ for key in sys.argv[1:] or ["c2", "ns", "c5"]:
                            parametrization=w.parametrization, num_splines=w.num_splines, mass=w.mass,
                            inertia=w.inertia, dts=np.full(w.horizon, w.dt, np.float32), sigma_mppi=w.sigma)
     out = {"workload": w.name}
-    for rng in ("philox", "jax"):
+    for rng in os.environ.get("RNGS", "philox,jax").split(","):
         ctx = _lib.Context(cfg)
         if rng != "philox":
             ctx.set_rng(rng)
