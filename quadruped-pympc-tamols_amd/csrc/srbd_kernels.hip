@@ -174,8 +174,11 @@ __device__ void fast_tail(const ModelConst& mc, const StepInput* in, const float
 // itself -- every fourth step each lane the three column quads (its leg's three components) of the next four
 // steps: rng_item's Philox4x32-10 call and Box-Muller pairs, so the same bits.  No noise is read or written: the
 // values stay raw in `pre` as the ZST loads leave them, and the LDS stage feeds the epilogue as before.
+#ifndef SRBD_QUAD_WPE
+#define SRBD_QUAD_WPE 4  // waves per SIMD the four-lane kernels are compiled for (a build-time knob for A/B builds)
+#endif
 template <int KIND, int HT, int ST, bool CEMT, bool EXT, int FM = 0, bool KS = false, bool GEN = false>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) rollout_quad_kernel(
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SRBD_QUAD_WPE))) rollout_quad_kernel(
                                                            const std::conditional_t<KS, StepInputK, KsNone> ksi,
                                                            const ModelConst mc, const StepInput* __restrict__ in_dev,
                                                            const float* __restrict__ noise, float* __restrict__ costs,
