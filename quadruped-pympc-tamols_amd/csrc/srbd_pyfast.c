@@ -298,7 +298,9 @@ static int get_legs(PyObject* legs, double* dst) {  /* a LegsAttr's FL FR RL RR 
  * key split of compute_control's with_newkey included):
  * -> None (an input form not handled here: nothing touched), or
  *    (rc, stage, current_contact, master_key, calls) when a call of the chain failed, or
- *    (0, 3, current_contact, master_key, calls, grf (4, 3) float64, predicted_state (24,) float32, best (P,) float32) */
+ *    (0, 3, current_contact, master_key, calls, GRF rows (4 x (3,) float64, masked), predicted_state (24,) float32,
+ *     best (P,) float32, foothold rows (4 x (3,) float64), constraint boxes (4 x [lower, upper] | None),
+ *     patches (4 x (rows, cols, 1, 3) float64) | None, scores (4, rows cols) float64 | None) */
 static PyObject* foothold_step(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
     (void)self;
     if (nargs != 21) {
@@ -429,22 +431,82 @@ static PyObject* foothold_step(PyObject* self, PyObject* const* args, Py_ssize_t
     }
     const long long ncalls = philox ? calls : calls + 1;
     if (rc != 0) return Py_BuildValue("(iiNNL)", rc, io->stage, cur, nk, ncalls);
-    npy_intp d43[2] = {4, 3};
-    PyObject* grf = PyArray_SimpleNew(2, d43, NPY_FLOAT64);
+    /* the objects the step hands out, made here rather than as numpy views in Python (one array each) */
     PyObject* pred = new_1d(NPY_FLOAT32, 24, res->predicted_state, sizeof(float));
     PyObject* nb = new_1d(NPY_FLOAT32, P, bb, sizeof(float));
-    if (!grf || !pred || !nb) {
-        Py_XDECREF(grf);
+    PyObject* grows = PyTuple_New(4);  /* leg l's GRFs times current_contact[l], float64 (the mask's promotion) */
+    PyObject* frows = PyTuple_New(4);  /* the adapted footholds */
+    PyObject* boxes = PyTuple_New(4);  /* [lower corner, upper corner] of a valid leg, else None */
+    PyObject* hms = NULL;              /* the raycast patches, (rows, cols, 1, 3) each */
+    PyObject* scores = NULL;           /* (4, rows * cols) */
+    int ok = pred && nb && grows && frows && boxes;
+    for (int l = 0; ok && l < 4; ++l) {
+        double g[3];
+        for (int c = 0; c < 3; ++c) g[c] = (double)res->grf[3 * l + c] * io->current_contact[l];
+        PyObject* gr = new_1d(NPY_FLOAT64, 3, g, sizeof(double));
+        PyObject* fr = new_1d(NPY_FLOAT64, 3, io->footholds + 3 * l, sizeof(double));
+        PyObject* bx = NULL;
+        if (io->valid[l]) {
+            PyObject* lo = new_1d(NPY_FLOAT64, 3, io->boxes + 6 * l, sizeof(double));
+            PyObject* hi = new_1d(NPY_FLOAT64, 3, io->boxes + 6 * l + 3, sizeof(double));
+            bx = lo && hi ? PyList_New(2) : NULL;
+            if (bx) {
+                PyList_SET_ITEM(bx, 0, lo);
+                PyList_SET_ITEM(bx, 1, hi);
+            } else {
+                Py_XDECREF(lo);
+                Py_XDECREF(hi);
+            }
+        } else {
+            bx = Py_None;
+            Py_INCREF(bx);
+        }
+        if (gr) PyTuple_SET_ITEM(grows, l, gr);
+        if (fr) PyTuple_SET_ITEM(frows, l, fr);
+        if (bx) PyTuple_SET_ITEM(boxes, l, bx);
+        ok = gr && fr && bx;
+    }
+    const npy_intp nc = (npy_intp)io->rows * io->cols;
+    if (ok && io->heightmaps) {
+        hms = PyTuple_New(4);
+        npy_intp dh[4] = {io->rows, io->cols, 1, 3};
+        for (int l = 0; ok && hms && l < 4; ++l) {
+            PyObject* h = PyArray_SimpleNew(4, dh, NPY_FLOAT64);
+            if (h) {
+                memcpy(PyArray_DATA((PyArrayObject*)h), io->heightmaps + (size_t)l * nc * 3, sizeof(double) * 3 * nc);
+                PyTuple_SET_ITEM(hms, l, h);
+            }
+            ok = h != NULL;
+        }
+        ok = ok && hms;
+    }
+    if (ok && io->scores) {
+        npy_intp ds[2] = {4, nc};
+        scores = PyArray_SimpleNew(2, ds, NPY_FLOAT64);
+        if (scores) memcpy(PyArray_DATA((PyArrayObject*)scores), io->scores, sizeof(double) * 4 * nc);
+        ok = scores != NULL;
+    }
+    if (!ok) {
         Py_XDECREF(pred);
         Py_XDECREF(nb);
+        Py_XDECREF(grows);
+        Py_XDECREF(frows);
+        Py_XDECREF(boxes);
+        Py_XDECREF(hms);
+        Py_XDECREF(scores);
         Py_DECREF(cur);
         Py_DECREF(nk);
         return NULL;
     }
-    double* g = (double*)PyArray_DATA((PyArrayObject*)grf);
-    for (int l = 0; l < 4; ++l)
-        for (int c = 0; c < 3; ++c) g[3 * l + c] = (double)res->grf[3 * l + c] * io->current_contact[l];
-    return Py_BuildValue("(iiNNLNNN)", 0, io->stage, cur, nk, ncalls, grf, pred, nb);
+    if (!hms) {
+        hms = Py_None;
+        Py_INCREF(hms);
+    }
+    if (!scores) {
+        scores = Py_None;
+        Py_INCREF(scores);
+    }
+    return Py_BuildValue("(iiNNLNNNNNNN)", 0, io->stage, cur, nk, ncalls, grows, pred, nb, frows, boxes, hms, scores);
 decline:
     if (PyErr_Occurred()) return NULL;
     Py_RETURN_NONE;

@@ -43,7 +43,7 @@ class TamolsMpcStep:
         self.vfa = VisualFootholdAdaptation(LEGS, "tamols", cfg)
         self.iface = SRBDControllerInterface(cfg)
         self._ref_state = None
-        self._ref_src = None  # (ref_base, footholds (4, 3), constraints) of a fused step, made into a dict on demand
+        self._ref_src = None  # (ref_base, the 4 foothold rows, constraints) of a fused step, made into a dict on demand
         self.last_constraints = None
         self.fused = True  # srbd_foothold_mpc_step when the configuration allows (see _fusable)
         self._io = None
@@ -56,10 +56,10 @@ class TamolsMpcStep:
     def last_ref_state(self):
         """The ref_state the last step gave compute_control (wb_interface.py:268-285)."""
         if self._ref_src is not None:
-            ref_base, fh, constraints = self._ref_src
+            ref_base, rows, constraints = self._ref_src
             ref_state = dict(ref_base)
             for i, n in enumerate(LEGS):
-                ref_state["ref_foot_" + n] = fh[i:i + 1]
+                ref_state["ref_foot_" + n] = rows[i][None]  # (1, 3), as wb_interface.py:268-285 shapes it
                 ref_state["ref_foot_constraints_" + n] = constraints[n]
             self._ref_state, self._ref_src = ref_state, None
         return self._ref_state
@@ -151,10 +151,29 @@ class TamolsMpcStep:
     def _fused_outputs(self, rc, res, current_contact, made, seeds, ref_base):
         """The objects' state after srbd_foothold_mpc_step, as the Python chain leaves it -- also when a call of the
         chain failed (io.stage: the calls that completed), so an error leaves them as compute_adaptation /
-        compute_control would -- and the step's 7-tuple.  made: (grf, predicted state, warm start) the C glue
-        already built, or None."""
+        compute_control would -- and the step's 7-tuple.  made: the objects the C glue built for a completed step (GRF
+        rows, predicted state, warm start, foothold rows, constraint boxes, patches, scores), or None."""
         iface, ctrl, vfa, io, a = self.iface, self.iface.controller, self.vfa, self._io, self._io_np
         ctx = ctrl.context
+        if made is not None:  # rc == 0, every call completed
+            grows, pred, best, frows, boxes, hms, scores = made
+            maps = self.heightmaps
+            maps.FL._data, maps.FR._data, maps.RL._data, maps.RR._data = hms
+            maps.FL.pending = maps.FR.pending = maps.RL.pending = maps.RR.pending = None
+            constraints = vfa.footholds_constraints
+            for i, b in enumerate(boxes):
+                if b is not None:
+                    constraints[LEGS[i]] = b
+            vfa.last_scores = scores
+            footholds = LegsAttr(*frows)
+            vfa.footholds_adaptation, vfa.initialized = footholds, True
+            self._ref_state, self._ref_src = None, (ref_base, frows, LegsAttr(*constraints))
+            self.last_constraints = constraints
+            iface.previous_contact_mpc = current_contact
+            ctrl.best_control_parameters = best
+            ctx.step_id += 1
+            ctrl.last_result = res
+            return LegsAttr(*grows), LegsAttr(*frows), None, None, None, 1.4, pred
         if io.stage >= 1:  # (compute_adaptation's reset, then its results: initialized again)
             hm = self._io_hm.copy()
             hms = self.heightmaps
@@ -171,7 +190,7 @@ class TamolsMpcStep:
                         constraints[LEGS[i]] = [b[0], b[1]]
             vfa.last_scores = self._io_scores.copy()
             vfa.footholds_adaptation, vfa.initialized = LegsAttr(f0, f1, f2, f3), True
-            self._ref_state, self._ref_src = None, (ref_base, fh, LegsAttr(*constraints))
+            self._ref_state, self._ref_src = None, (ref_base, (f0, f1, f2, f3), LegsAttr(*constraints))
             self.last_constraints = constraints
         else:  # the patches stay pending around the seeds (update_height_map ran, the search did not)
             vfa.reset()
@@ -179,7 +198,7 @@ class TamolsMpcStep:
                 m._data, m.pending = None, (seeds[3 * i:3 * i + 3].copy(), io.yaw)
         if io.stage >= 2:
             iface.previous_contact_mpc = current_contact
-            ctrl.best_control_parameters = made[2] if made is not None else ctx._best.copy()
+            ctrl.best_control_parameters = ctx._best.copy()
         if rc != _lib.OK:
             what = "srbd_tamols_run_terrain" if io.stage == 0 else "srbd_prepare_state" if io.stage == 1 else "srbd_step"
             msg = _lib.lib.srbd_tamols_last_error(vfa.search.h) if io.stage == 0 else _lib.last_error(ctx.h)
@@ -187,11 +206,8 @@ class TamolsMpcStep:
                                f"{msg.decode() if isinstance(msg, bytes) else msg}")
         ctx.step_id += 1
         ctrl.last_result = res
-        if made is not None:
-            g, pred = made[0], made[1]
-        else:
-            g = np.array(res.grf, dtype=np.float32).reshape(4, 3) * current_contact[:, None]  # as compute_control
-            pred = np.array(res.predicted_state, dtype=np.float32)
+        g = np.array(res.grf, dtype=np.float32).reshape(4, 3) * current_contact[:, None]  # as compute_control
+        pred = np.array(res.predicted_state, dtype=np.float32)
         return LegsAttr(*g), LegsAttr(f0, f1, f2, f3), None, None, None, 1.4, pred
 
     def step(self, state_current: dict, ref_feet_pos: LegsAttr, hip_pos: LegsAttr, ref_base: dict,
