@@ -10,6 +10,11 @@
 //   three_launch_flag  three dependent kernels launched now, the third writes the flag
 //   armed3_flag        the same three kernels launched beforehand, the first spinning on a host-mapped
 //                      go word (bounded): host stores go, spins on the flag (pre-armed step)
+//   armed1_flag        one kernel launched beforehand (157 blocks x 256 threads, lane 0 of each block polling the
+//                      go word), block 0 writes the flag once go arrives
+//   armed1_read_flag   the same, each block then reading 1.5 KB of pinned host staging (system-scope loads) and
+//                      storing it to device memory before block 0 writes the flag
+//   args1k_flag        launch_flag with a 1.5 KB by-value argument (the step input's size class)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -48,6 +53,48 @@ __global__ void k_arm(const unsigned* go, unsigned seq) {
         }
     }
     __syncthreads();
+}
+
+struct Mid {
+    float v[384];
+};
+__global__ void k_flag_args1k(volatile unsigned* host_flag, unsigned seq, Mid b, float* sink) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        sink[0] = b.v[seq % 384];
+        __threadfence_system();
+        *host_flag = seq;
+    }
+}
+// Pre-armed single launch: every block's lane 0 polls go (bounded), the block passes a barrier; READ: the block
+// then loads 384 words of pinned host staging (system scope) and stores them to its device slot; block 0's lane 0
+// writes the flag.
+template <bool READ>
+__global__ void k_arm1(const unsigned* go, unsigned seq, const unsigned* stage, unsigned* dslot,
+                       volatile unsigned* host_flag) {
+    __shared__ int ok;
+    if (threadIdx.x == 0) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        int r = 1;
+        while (__hip_atomic_load(go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {
+                r = 0;
+                break;
+            }
+        }
+        ok = r;
+    }
+    __syncthreads();
+    if (READ) {
+        for (int i = threadIdx.x; i < 384; i += blockDim.x)
+            dslot[blockIdx.x * 384 + i] =
+                __hip_atomic_load(stage + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + (unsigned)ok;
+        __syncthreads();
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        __threadfence_system();
+        *host_flag = seq;
+    }
 }
 
 template <class F>
@@ -131,6 +178,38 @@ int main() {
     }
     std::nth_element(ta.begin(), ta.begin() + ta.size() / 2, ta.end());
     const double armed = ta[ta.size() / 2];
+    Mid mb{};
+    double cargs1k = p50([&](int i) {
+        k_flag_args1k<<<1, 64, 0, s>>>(dflag, (unsigned)i + 1, mb, sink);
+        spin((unsigned)i + 1);
+    });
+    unsigned* hstage;
+    hipHostMalloc((void**)&hstage, 4096, hipHostMallocMapped | hipHostMallocCoherent);
+    unsigned* dstage;
+    hipHostGetDevicePointer((void**)&dstage, hstage, 0);
+    unsigned* dslot;
+    hipMalloc(&dslot, 157 * 384 * 4);
+    double a1[2];
+    for (int rd = 0; rd < 2; ++rd) {
+        std::vector<double> tb;
+        for (int i = 0; i < 3100; ++i) {
+            const unsigned q = 200000u + 10000u * rd + (unsigned)i;
+            if (rd)
+                k_arm1<true><<<157, 256, 0, s>>>(dgo, q, dstage, dslot, dflag);
+            else
+                k_arm1<false><<<157, 256, 0, s>>>(dgo, q, dstage, dslot, dflag);
+            const auto w0 = std::chrono::steady_clock::now();
+            while (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w0).count() < 30.0) {
+            }
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int j = 0; j < 384; ++j) hstage[j] = q + j;
+            __atomic_store_n(hgo, q, __ATOMIC_RELEASE);
+            spin(q);
+            if (i >= 100) tb.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+        }
+        std::nth_element(tb.begin(), tb.begin() + tb.size() / 2, tb.end());
+        a1[rd] = tb[tb.size() / 2];
+    }
     hipGraph_t g;
     hipGraphExec_t ge;
     hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
@@ -144,7 +223,8 @@ int main() {
     });
     hipStreamSynchronize(s);
     printf("{\"launch_sync\": %.2f, \"launch_flag\": %.2f, \"args3k_flag\": %.2f, \"two_launch_flag\": %.2f, "
-           "\"h2d_launch_sync\": %.2f, \"graph2_sync\": %.2f, \"three_launch_flag\": %.2f, \"armed3_flag\": %.2f}\n",
-           a, bflag, cargs, two, h2d, gr, three, armed);
+           "\"h2d_launch_sync\": %.2f, \"graph2_sync\": %.2f, \"three_launch_flag\": %.2f, \"armed3_flag\": %.2f, "
+           "\"args1k_flag\": %.2f, \"armed1_flag\": %.2f, \"armed1_read_flag\": %.2f}\n",
+           a, bflag, cargs, two, h2d, gr, three, armed, cargs1k, a1[0], a1[1]);
     return 0;
 }
