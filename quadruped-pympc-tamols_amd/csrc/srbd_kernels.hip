@@ -51,9 +51,16 @@ constexpr int QP_NEXT2 = 0x52;  // lanes (0,1,2,3) <- (2,0,1,1): component c+2 (
 constexpr int QP_XOR1 = 0xB1;   // lanes (0,1,2,3) <- (1,0,3,2)
 constexpr int QP_XOR2 = 0x4E;   // lanes (0,1,2,3) <- (2,3,0,1)
 
+#ifndef SRBD_XS
+#define SRBD_XS 0  // experiment knob: quad permutations through ds_swizzle (the LDS crossbar) instead of DPP
+#endif
 template <int CTRL>
 __device__ __forceinline__ float qp(float v) {
+#if SRBD_XS
+    return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x8000 | CTRL));
+#else
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+#endif
 }
 __device__ __forceinline__ float sel3(int c, float a0, float a1, float a2) { return c == 0 ? a0 : (c == 1 ? a1 : a2); }
 
