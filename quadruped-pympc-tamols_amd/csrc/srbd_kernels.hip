@@ -54,6 +54,12 @@ constexpr int QP_XOR2 = 0x4E;   // lanes (0,1,2,3) <- (2,3,0,1)
 #ifndef SRBD_XS
 #define SRBD_XS 0  // experiment knob: quad permutations through ds_swizzle (the LDS crossbar) instead of DPP
 #endif
+#ifndef SRBD_PRIO
+#define SRBD_PRIO 0  // experiment knob: s_setprio of the rollout blocks' waves (the draw blocks stay at 0)
+#endif
+#ifndef SRBD_PRIO_MIN
+#define SRBD_PRIO_MIN 0  // ... for launches of at least this many rollout blocks
+#endif
 template <int CTRL>
 __device__ __forceinline__ float qp(float v) {
 #if SRBD_XS
@@ -213,6 +219,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(SRBD_Q
     }
     // blocks past the rollout grid generate the next step's noise on the CUs the rollout leaves idle
     SRBD_RSTAMP(0);
+#if SRBD_PRIO
+    // experiment knob: the rollout waves (horizon, epilogue, fold, tail) ahead of the draw waves in VALU arbitration
+    if ((int)blockIdx.x < nroll && nroll >= SRBD_PRIO_MIN) __builtin_amdgcn_s_setprio(SRBD_PRIO);
+#endif
     if ((int)blockIdx.x >= nroll) {
         rng_items(mc, in, next_rng, ((int)blockIdx.x - nroll) * (int)blockDim.x + (int)threadIdx.x,
                   ((int)gridDim.x - nroll) * (int)blockDim.x);
