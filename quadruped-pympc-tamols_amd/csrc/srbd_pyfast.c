@@ -72,13 +72,38 @@ static PyObject* pgg_contact_sequence(PyObject* self, PyObject* const* args, Py_
         return NULL;
     }
     srbd_pgg* g = (srbd_pgg*)addr_of(args[0]);
-    if (!g && PyErr_Occurred()) return NULL;
+    if (!g) {
+        if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "pgg_contact_sequence: null generator");
+        return NULL;
+    }
     PyArrayObject* d = (PyArrayObject*)PyArray_FROM_OTF(args[1], NPY_FLOAT64, NPY_ARRAY_IN_ARRAY);
     if (!d) return NULL;
     PyArrayObject* l = (PyArrayObject*)PyArray_FROM_OTF(args[2], NPY_INT32, NPY_ARRAY_IN_ARRAY | NPY_ARRAY_FORCECAST);
     if (!l) {
         Py_DECREF(d);
         return NULL;
+    }
+    if (PyArray_SIZE(l) < PyArray_SIZE(d) && g->gait_type != SRBD_GAIT_FULL_STANCE) {
+        /* fewer lengths than dts: the library reads lengths[j] for j < n_dts, so walk the reference's index first
+         * (PGG:111-115) -- it raises IndexError where it would read past the lengths */
+        const int32_t* lp = (const int32_t*)PyArray_DATA(l);
+        const npy_intp nl = PyArray_SIZE(l), nd = PyArray_SIZE(d);
+        npy_intp j = 0;
+        int past = 0;
+        for (int i = 1; i < g->horizon; ++i) {
+            if (j >= nl) {  /* lengths[j] read past the end */
+                past = 1;
+                break;
+            }
+            if (i >= lp[j]) ++j;
+            if (j >= nd) break;  /* dts[j] past the end: the library reports it */
+        }
+        if (past) {
+            Py_DECREF(d);
+            Py_DECREF(l);
+            PyErr_SetString(PyExc_IndexError, "compute_contact_sequence: contact_sequence_lenghts too short");
+            return NULL;
+        }
     }
     double out[8 * SRBD_MAX_HORIZON];
     const int H = g->horizon;

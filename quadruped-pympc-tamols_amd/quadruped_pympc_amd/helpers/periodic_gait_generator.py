@@ -24,6 +24,21 @@ def _check(rc, what):
     return rc
 
 
+def _check_lengths(lens, n_dts, horizon, gait_type):
+    """Raise IndexError where the reference's loop (PGG:111-115) would read contact_sequence_lenghts past its end
+    (the library reads lens[j] for j < n_dts only, so a shorter lengths array is walked here first)."""
+    if len(lens) >= n_dts or gait_type == FULL_STANCE:
+        return
+    j = 0
+    for i in range(1, horizon):
+        if j >= len(lens):
+            raise IndexError("compute_contact_sequence: contact_sequence_lenghts too short")
+        if i >= lens[j]:
+            j += 1
+        if j >= n_dts:
+            return  # dts[j] past the end: the library reports it
+
+
 class PeriodicGaitGenerator:
     def __init__(self, duty_factor, step_freq, gait_type, horizon):
         self._g = _lib.SrbdPgg()
@@ -78,6 +93,7 @@ class PeriodicGaitGenerator:
             return _lib.fast.pgg_contact_sequence(self._addr, contact_sequence_dts, contact_sequence_lenghts)
         key = (np.asarray(contact_sequence_dts, dtype=np.float64).tobytes(),
                np.asarray(contact_sequence_lenghts, dtype=np.int32).tobytes())
+        _check_lengths(np.frombuffer(key[1], dtype=np.int32), len(key[0]) // 8, self._g.horizon, self._g.gait_type)
         if key != self._seq_key:  # the 100 Hz caller passes the same arrays every step
             self._dts = np.frombuffer(key[0], dtype=np.float64).copy()
             self._lens = np.frombuffer(key[1], dtype=np.int32).copy()

@@ -382,6 +382,30 @@ def test_pgg_fast_glue_equals_python_path(monkeypatch, gait):
             a.compute_contact_sequence([0.02], [3])  # runs past the last dts entry (the reference: IndexError)
 
 
+@pytest.mark.parametrize("fast", [True, False])
+def test_pgg_short_lengths_follow_the_reference_loop(monkeypatch, fast):
+    """Fewer contact_sequence_lenghts than dts: the library reads lengths[j] for j < len(dts) only, so both paths walk
+    the reference's index (PGG:111-115) first -- IndexError exactly where the reference's loop would read past the
+    lengths, the reference's sequence where it never does (the scalar oracle restates that loop)."""
+    if not fast:
+        monkeypatch.setattr(_lib, "fast", None)
+    H = 12
+    ok_cases = [([0.01, 0.02], [12]), ([0.01, 0.02], [H - 1]), ([0.01, 0.02, 0.03], [4, 12])]
+    bad_cases = [([0.01, 0.02], [3]), ([0.01, 0.02, 0.03], [4, 8]), ([0.01, 0.02], [])]
+    for dts, lens in ok_cases:
+        a, b = PeriodicGaitGenerator(0.65, 1.4, 0, H), PGGOracle(0.65, 1.4, 0, H)
+        np.testing.assert_array_equal(a.compute_contact_sequence(dts, lens), b.compute_contact_sequence(dts, lens))
+    for dts, lens in bad_cases:
+        a, b = PeriodicGaitGenerator(0.65, 1.4, 0, H), PGGOracle(0.65, 1.4, 0, H)
+        with pytest.raises(IndexError):
+            b.compute_contact_sequence(dts, lens)
+        with pytest.raises(IndexError):
+            a.compute_contact_sequence(dts, lens)
+        # nothing ran here (the reference's loop has advanced its phases by the time it raises; the library's own
+        # error path restores them, as test_pgg_c_abi_argument_checks pins)
+        np.testing.assert_array_equal(a.phase_signal, [0.5, 1.0, 1.0, 0.5])
+
+
 def test_interface_glue_declines_other_inputs():
     """interface_step returns None (the Python sequence then runs) for inputs it does not take, before it touches
     the context, the staging or the library -- so no device is needed to check it."""
