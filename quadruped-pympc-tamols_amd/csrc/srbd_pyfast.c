@@ -169,9 +169,8 @@ static PyObject* interface_step(PyObject* self, PyObject* const* args, Py_ssize_
 
     /* ---- validate and gather (no side effects before every input is known to fit) */
     double st[24], rf[24];
-    PyObject* feet[4];
     for (int i = 0; i < 8; ++i) {
-        if (!get3(state, k_state[i], st + 3 * i, NULL) || !get3(ref, k_ref[i], rf + 3 * i, i >= 4 ? &feet[i - 4] : NULL)) {
+        if (!get3(state, k_state[i], st + 3 * i, NULL) || !get3(ref, k_ref[i], rf + 3 * i, NULL)) {
             if (PyErr_Occurred()) return NULL;
             Py_RETURN_NONE;
         }
@@ -277,7 +276,14 @@ static PyObject* interface_step(PyObject* self, PyObject* const* args, Py_ssize_
     if (!grf || !pred || !nb || !ns || !nk || !fh) goto fail;
     memcpy(PyArray_DATA((PyArrayObject*)grf), io->grf, sizeof(io->grf));
     for (int l = 0; l < 4; ++l) {
-        PyObject* f = PyObject_GetItem(feet[l], k_zero);  /* ref_state["ref_foot_*"][0] */
+        /* ref_state["ref_foot_*"][0], looked up again now: the GIL was released around the call, so a reference
+         * borrowed from the dict before it may no longer be alive */
+        PyObject* v = PyDict_GetItemWithError(ref, k_ref[4 + l]);  /* borrowed, used at once */
+        if (!v) {
+            if (!PyErr_Occurred()) PyErr_SetObject(PyExc_KeyError, k_ref[4 + l]);
+            goto fail;
+        }
+        PyObject* f = PyObject_GetItem(v, k_zero);
         if (!f) goto fail;
         PyTuple_SET_ITEM(fh, l, f);
     }
