@@ -331,7 +331,8 @@ static int get_legs(PyObject* legs, double* dst) {  /* a LegsAttr's FL FR RL RR 
  *    (rc, stage, current_contact, master_key, calls) when a call of the chain failed, or
  *    (0, 3, current_contact, master_key, calls, GRF rows (4 x (3,) float64, masked), predicted_state (24,) float32,
  *     best (P,) float32, foothold rows (4 x (3,) float64), constraint boxes (4 x [lower, upper] | None),
- *     patches (4 x (rows, cols, 1, 3) float64) | None, scores (4, rows cols) float64 | None) */
+ *     patches (4 x (rows, cols, 1, 3) float64), or without io->heightmaps the maps' pending (seed (3,), yaw) pairs,
+ *     scores (4, rows cols) float64 | None) */
 static PyObject* foothold_step(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
     (void)self;
     if (nargs != 21) {
@@ -508,6 +509,16 @@ static PyObject* foothold_step(PyObject* self, PyObject* const* args, Py_ssize_t
                 PyTuple_SET_ITEM(hms, l, h);
             }
             ok = h != NULL;
+        }
+        ok = ok && hms;
+    } else if (ok) {  /* patches not copied out: each map stays pending -- (its seed (3,), the yaw) -- and raycasts on
+                       * access (GpuHeightMap.data), the same values */
+        hms = PyTuple_New(4);
+        for (int l = 0; ok && hms && l < 4; ++l) {
+            PyObject* c = new_1d(NPY_FLOAT64, 3, io->seeds + 3 * l, sizeof(double));
+            PyObject* pnd = c ? Py_BuildValue("(Nd)", c, io->yaw) : NULL;
+            if (pnd) PyTuple_SET_ITEM(hms, l, pnd);
+            ok = pnd != NULL;
         }
         ok = ok && hms;
     }

@@ -43,7 +43,11 @@ __device__ __forceinline__ void tamols_query_point(const TamolsArgs& a, int leg,
             qx = cx;
             qy = cy;
         } else if (q <= 5) {  // VFA:406 p_leg = (1 - alpha) * hip + alpha * candidate
-            const double al = p.alphas[q - 1];
+            // alphas[q - 1] by selects over the five (uniform, scalar-loaded) values: indexed by the lane-varying q,
+            // the kernel-argument array was read with a per-lane memory load and a vmcnt(0) wait in the query phase
+            double al = p.alphas[0];
+#pragma unroll
+            for (int i = 1; i < 5; ++i) al = q - 1 == i ? p.alphas[i] : al;
             qx = (1.0 - al) * hx + al * cx;
             qy = (1.0 - al) * hy + al * cy;
         } else if (q <= 9) {  // VFA:443 offsets (+d,0), (-d,0), (0,+d), (0,-d)
@@ -545,7 +549,9 @@ __global__ void __launch_bounds__(TAMOLS_THREADS) tamols_fused_kernel(const std:
         __syncthreads();
         if (tid >= 64) return;
         // the host reads the scores / patch once it holds the tagged outputs: a system-scope release orders the
-        // block's (completed) host stores before them -- the stores of different addresses take different paths
+        // block's (completed) host stores before them -- the stores of different addresses take different paths.
+        // (System-scope stores of the scores / patch in place of the release measured far slower: one PCIe write
+        // per 8-byte store, C4 step p50 44 -> 80 us.)
         if (j.scores || j.hm_out) __threadfence_system();
         TAM_STAMP(4);
         for (int w = 1; w < (T + 63) / 64; ++w)  // every lane of wave 0 folds the same values

@@ -90,10 +90,12 @@ class TamolsMpcStep:
                            ("state_in", "ref_base", "seeds", "hips", "forward_vel", "current_contact",
                             "previous_contact", "footholds", "boxes", "seed_heights", "valid")}
             self._io_scores = np.zeros((4, g.num_rows * g.num_cols))
-            # (4, rows, cols, 3) as the call writes them, held as the maps' (rows, cols, 1, 3) layout
-            self._io_hm = np.zeros((4, g.num_rows, g.num_cols, 1, 3))
-            io.scores, io.heightmaps = self._io_scores.ctypes.data, self._io_hm.ctypes.data
+            # the patches are not copied out: the maps stay pending around the seeds and raycast on access (the same
+            # values); the scores only when vfa.keep_scores (without either, the TAMOLS launch stores nothing to the
+            # host but its outputs and needs no system release before them: C4 step -2 us)
+            io.heightmaps = None
             self._io_ref = C.byref(io)
+        io.scores = self._io_scores.ctypes.data if self.vfa.keep_scores else None
         return io
 
     def _step_fused(self, state_current, ref_feet_pos, hip_pos, ref_base, contact_sequence, base_lin_vel,
@@ -156,10 +158,10 @@ class TamolsMpcStep:
         iface, ctrl, vfa, io, a = self.iface, self.iface.controller, self.vfa, self._io, self._io_np
         ctx = ctrl.context
         if made is not None:  # rc == 0, every call completed
-            grows, pred, best, frows, boxes, hms, scores = made
+            grows, pred, best, frows, boxes, pending, scores = made
             maps = self.heightmaps
-            maps.FL._data, maps.FR._data, maps.RL._data, maps.RR._data = hms
-            maps.FL.pending = maps.FR.pending = maps.RL.pending = maps.RR.pending = None
+            maps.FL._data = maps.FR._data = maps.RL._data = maps.RR._data = None
+            maps.FL.pending, maps.FR.pending, maps.RL.pending, maps.RR.pending = pending
             constraints = vfa.footholds_constraints
             for i, b in enumerate(boxes):
                 if b is not None:
@@ -175,10 +177,8 @@ class TamolsMpcStep:
             ctrl.last_result = res
             return LegsAttr(*grows), LegsAttr(*frows), None, None, None, 1.4, pred
         if io.stage >= 1:  # (compute_adaptation's reset, then its results: initialized again)
-            hm = self._io_hm.copy()
-            hms = self.heightmaps
-            hms.FL._data, hms.FR._data, hms.RL._data, hms.RR._data = hm
-            hms.FL.pending = hms.FR.pending = hms.RL.pending = hms.RR.pending = None
+            for i, m in enumerate(self.heightmaps):  # pending around the seeds (raycast on access)
+                m._data, m.pending = None, (seeds[3 * i:3 * i + 3].copy(), io.yaw)
             fh = a["footholds"].reshape(4, 3).copy()
             f0, f1, f2, f3 = fh
             valid = io.valid
@@ -188,7 +188,7 @@ class TamolsMpcStep:
                 for i, b in enumerate(boxes):
                     if valid[i]:
                         constraints[LEGS[i]] = [b[0], b[1]]
-            vfa.last_scores = self._io_scores.copy()
+            vfa.last_scores = self._io_scores.copy() if vfa.keep_scores else None
             vfa.footholds_adaptation, vfa.initialized = LegsAttr(f0, f1, f2, f3), True
             self._ref_state, self._ref_src = None, (ref_base, (f0, f1, f2, f3), LegsAttr(*constraints))
             self.last_constraints = constraints

@@ -213,6 +213,9 @@ class VisualFootholdAdaptation:
         if adaptation_strategy == "tamols":
             self.tamols_params = cfg.simulation_params.get("tamols_params", {})
             self.robot_name = cfg.robot
+        # last_scores (an extension: the reference keeps no scores): the per-candidate TAMOLS scores of the last call,
+        # (4, rows * cols), kept when keep_scores is set -- copying them to the host costs the C4 step ~2 us
+        self.keep_scores = False
         self.last_scores = None
         self._params_src = self._params_struct = self._params_robot = None
 
@@ -277,14 +280,15 @@ class VisualFootholdAdaptation:
                 out = self.search.run_terrain(ter, yaw, seeds, hips, params, rows=g.num_rows, cols=g.num_cols,
                                               dist_x=g.dist_x, dist_y=g.dist_y, ray_z=g.ray_z,
                                               forward_vel=forward_vel, base_position=base_position,
-                                              current_contact=contact, current_feet_pos=feet)
+                                              current_contact=contact, current_feet_pos=feet,
+                                              want_scores=self.keep_scores)
                 for i, n in enumerate(names):
                     heightmaps[n].set_data(out["heightmaps"][i])
             else:
                 data = np.stack([np.asarray(heightmaps[n].data, dtype=np.float64)[:, :, 0, :] for n in names])
                 out = self.search.run(data, seeds, hips, params, forward_vel=forward_vel, base_position=base_position,
-                                      current_contact=contact, current_feet_pos=feet)
-            self.last_scores = out["scores"]
+                                      current_contact=contact, current_feet_pos=feet, want_scores=self.keep_scores)
+            self.last_scores = out.get("scores")
             for i, n in enumerate(names):
                 if out["valid"][i]:
                     reference_footholds[n] = out["footholds"][i].copy()
