@@ -10,7 +10,8 @@ With the plain ``Sampling_MPC`` and no solution shift, the whole sequence is one
 (``srbd_interface_step``: prepare_state, the key splits, CEM's sigma reset, the device steps and the GRF
 mask, in the same order), its arguments gathered and its results built by the ``_srbd_fast`` glue;
 the controller's attributes end as the Python sequence leaves them (``tests/test_gpu_interface_step.py``
-pins the two bit for bit).  ``SRBD_INTERFACE_FAST=0`` forces the Python sequence.
+pins the two bit for bit).  ``SRBD_INTERFACE_FAST=0`` when an interface is created makes it run the Python
+sequence.
 """
 from __future__ import annotations
 
@@ -44,6 +45,8 @@ class SRBDControllerInterface:
 
         self.controller = Sampling_MPC(cfg)
         self._fast = None  # _FastStep of the one-call path, made on the first eligible call
+        # read once: os.environ lookups cost ~1 us, a fifth of the Python around the one call
+        self._fast_env = os.environ.get("SRBD_INTERFACE_FAST") != "0"
 
     def __getstate__(self):  # a copy makes its own one-call staging (it caches raw addresses)
         d = dict(self.__dict__)
@@ -51,22 +54,24 @@ class SRBDControllerInterface:
         return d
 
     def __setstate__(self, d):
+        d.setdefault("_fast_env", True)
         self.__dict__.update(d)
 
     def _fast_step(self):
         """The one-call path when it makes exactly the Python sequence's calls: the glue is built, the plain
         Sampling_MPC (not the gait-adaptive one), no solution shift."""
         ctrl = self.controller
-        if _lib.fast is None or self._cfg.mpc_params["shift_solution"] or os.environ.get("SRBD_INTERFACE_FAST") == "0":
+        if not self._fast_env or _lib.fast is None or self._cfg.mpc_params["shift_solution"]:
             return None
-        from ..controllers.sampling import centroidal_nmpc_hip
-
-        if type(ctrl) is not centroidal_nmpc_hip.Sampling_MPC:
+        if type(ctrl) is not _SAMPLING_MPC:
             return None
-        # the controller's own methods, not instance-level replacements of the ones the sequence calls
+        # the controller's own methods, not instance-level replacements of the ones the sequence calls (four
+        # lookups: a set intersection with the instance dict cost 1 us)
+        d = ctrl.__dict__
+        if "prepare_state_and_reference" in d or "with_newkey" in d or "with_newsigma" in d or "shift_solution" in d:
+            return None
         jcc = ctrl.jitted_compute_control
-        if getattr(jcc, "__self__", None) is not ctrl or jcc.__func__ is not _OWN_COMPUTE.get(ctrl.sampling_method) \
-                or _PATCHABLE.intersection(ctrl.__dict__):
+        if getattr(jcc, "__self__", None) is not ctrl or jcc.__func__ is not _OWN_COMPUTE.get(ctrl.sampling_method):
             return None
         fs = self._fast
         if fs is None or fs.ctrl is not ctrl or fs.ctx is not ctrl._ctx:
@@ -117,12 +122,11 @@ class SRBDControllerInterface:
 def _own_compute():
     from ..controllers.sampling.centroidal_nmpc_hip import Sampling_MPC as S
 
-    return {"random_sampling": S.compute_control_random_sampling, "mppi": S.compute_control_mppi,
-            "cem_mppi": S.compute_control_cem_mppi}
+    return S, {"random_sampling": S.compute_control_random_sampling, "mppi": S.compute_control_mppi,
+               "cem_mppi": S.compute_control_cem_mppi}
 
 
-_OWN_COMPUTE = _own_compute()
-_PATCHABLE = frozenset(("prepare_state_and_reference", "with_newkey", "with_newsigma", "shift_solution"))
+_SAMPLING_MPC, _OWN_COMPUTE = _own_compute()
 
 
 class _FastStep:
@@ -170,8 +174,7 @@ class _FastStep:
             ctrl.sigma_cem_mppi = sigma
         ctrl.last_result = _lib.SrbdResult.from_buffer_copy(self.res)
         self.ctx.step_id += ctrl.num_sampling_iterations
-        return (LegsAttr(grf[0], grf[1], grf[2], grf[3]), LegsAttr(fh[0], fh[1], fh[2], fh[3]), None, None, None,
-                self.freq, pred)
+        return LegsAttr(*grf), LegsAttr(*fh), None, None, None, self.freq, pred
 
     def _failed(self, rc, stage, cur, f32_contact):
         """A call of the chain failed: leave the objects as the Python sequence leaves them, then raise as it does."""

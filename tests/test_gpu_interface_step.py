@@ -69,6 +69,7 @@ def test_one_call_equals_python_sequence(lib, monkeypatch, method, par, rng, ite
               num_sampling_iterations=iters, rng="jax" if rng == "jax_legacy" else rng,
               jax_threefry_partitionable=rng != "jax_legacy")
     fast, slow = SRBDControllerInterface(_cfg(**mp)), SRBDControllerInterface(_cfg(**mp))
+    slow._fast_env = False  # as SRBD_INTERFACE_FAST=0 at its creation
     pgg = PeriodicGaitGenerator(0.65, 1.4, 0, H)
     dts, lens = np.array([0.02]), np.array([H])
     lifts = 0
