@@ -840,7 +840,12 @@ __device__ __forceinline__ void block_topk_nodes(const float* __restrict__ recs,
         }
     }
     __syncthreads();
-    auto table_ranks = [&](const uint64_t* tab) {  // cnt[i] = entries of the K x K table below entry i
+    // cnt[i] = entries of the K x K table below entry i.  Every row is ascending (B: a node's K smallest record
+    // minima by rank, KEY_NONE after them; D: a record's key list, ascending, KEY_NONE-padded) and the keys are
+    // unique, so a row's count below y is its lower bound: found by binary lifting (five dependent LDS reads for
+    // K <= 16) -- the same count as comparing every entry, a third of the LDS traffic (C3: 1.3 us per call so)
+    static_assert(MAXK <= 31, "binary lifting from a step of 16");
+    auto table_ranks = [&](const uint64_t* tab) {
         for (int i = tid; i < KK * K; i += NT) {
             const int c = i / K, b = i - c * K;
             const uint64_t y = tab[c];
@@ -848,7 +853,8 @@ __device__ __forceinline__ void block_topk_nodes(const float* __restrict__ recs,
             const uint64_t* row = tab + b * K;
             int n = 0;
 #pragma unroll
-            for (int q = 0; q < MAXK; ++q) n += q < K && row[q] < y ? 1 : 0;  // all loads in flight together
+            for (int s = 16; s >= 1; s >>= 1)
+                if (n + s <= K && row[n + s - 1] < y) n += s;
             if (n) atomicAdd(&t.cnt[c], n);
         }
     };
