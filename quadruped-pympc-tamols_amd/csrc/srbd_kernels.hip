@@ -1073,8 +1073,10 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
     // Unsplit: the step outputs are assembled in LDS and written out in one burst at the end, so no
     // wave waits for a host store's completion mid-merge (a wave overwriting a register of a pending
     // store waits vmcnt(0), ~1 us for a PCIe write) and the publish waits for one round of them.
+    // A column split's tail block assembles its outputs (its tail columns of best, the GRFs, the prediction and the
+    // scalars) the same way and bursts only those (C3: its direct host stores cost ~1 us of register-reuse waits).
     float* osh = sh.osh;
-    const bool shadow = !split;
+    const bool shadow = !split || tailblk;
     auto ostore = [&](void* dst, float v) {
         if (shadow)
             osh[reinterpret_cast<float*>(dst) - reinterpret_cast<float*>(out)] = v;
@@ -1492,10 +1494,15 @@ __device__ __forceinline__ void merge_body(const ModelConst& mc, StepInput* __re
         constexpr int TAILF = (int)((sizeof(StepOutput) - offsetof(StepOutput, grf)) / sizeof(float));
         constexpr int TAIL0 = (int)(offsetof(StepOutput, grf) / sizeof(float));
         constexpr int SIG0 = (int)(offsetof(StepOutput, sigma) / sizeof(float));
-        const int nsig = cem ? P : 0;
+        constexpr int STAT = (int)(offsetof(StepOutput, status) / sizeof(float));
+        // unsplit: the whole StepOutput; a split's tail block: its columns of best, then grf .. the scalars except
+        // status (the host zeroed it; a late block ORs its bit in)
+        const int nb0 = split ? ncol : P;
+        const int nsig = cem && !split ? P : 0;
         float* o = reinterpret_cast<float*>(out);
-        for (int t = tid; t < P + nsig + TAILF; t += T) {
-            const int k = t < P ? t : (t < P + nsig ? SIG0 + (t - P) : TAIL0 + (t - P - nsig));
+        for (int t = tid; t < nb0 + nsig + TAILF; t += T) {
+            const int k = t < nb0 ? (split ? jc(t) : t) : (t < nb0 + nsig ? SIG0 + (t - nb0) : TAIL0 + (t - nb0 - nsig));
+            if (split && k == STAT) continue;
             if (sysout)
                 __hip_atomic_store(reinterpret_cast<uint32_t*>(o + k), __float_as_uint(osh[k]), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
