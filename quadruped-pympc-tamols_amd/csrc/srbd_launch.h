@@ -111,7 +111,10 @@ struct Publish {
 // chain != 0: also write the new parameters / sigma / RNG counter back into `in` (device warm start).
 // With step outputs and no rank record the merge is column-split over merge_blocks(mc) blocks, each
 // publishing flag[block]; returns the number of blocks that publish.
-constexpr int MERGE_SPLIT_COLS = 16;  // parameter columns per slice block (SRBD_MERGE_SPLIT_COLS overrides)
+#ifndef SRBD_MERGE_SPLIT_COLS
+#define SRBD_MERGE_SPLIT_COLS 4
+#endif
+constexpr int MERGE_SPLIT_COLS = SRBD_MERGE_SPLIT_COLS;  // parameter columns per slice block (-D overrides)
 constexpr int MERGE_MAX_BLOCKS = 64;  // publish flags the host context holds
 constexpr int MERGE_SPLIT_MIN_RECS = 256;
 int merge_split_cols(const ModelConst& mc);
